@@ -1,0 +1,191 @@
+"""Benchmark of the FRI-prover hot path on MI355X (BASELINE.json metric:
+"2^24-pt NTT field-elems/sec + Merkle leaves/sec; end-to-end proof wall-clock").
+
+A step is one 2^24-point forward NTT over BN254 Fr on HBM-resident synthetic
+data (BASELINE.md generator).  `value` = NTT field elements per second over all
+ranks.  The same JSON line also carries the Merkle leaves/s (2^24 32-B leaves),
+the 2^20 forward+inverse pair (config 2) and an FRI prove wall-clock.
+
+N > 1 GPUs: one process per GPU (torch.distributed.run), each rank transforms
+its own 2^24-point input (independent columns shard with no collective), so
+scaling is weak; timing is barrier-bracketed and the max over ranks is used.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "stark-pure-rust_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import stark_amd as S  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+MAD64_PEAK_TOPS = 19.66        # v_mad_u64_u32: quarter rate x 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+LOG_N = 24
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=LOG_N)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic(n, seed):
+    import oracle as O  # the synthetic generator only; not the checker here
+    return O.random_elements(n, seed)
+
+
+def timed_events(fn, stream, reps):
+    """Average ms per call of fn() on `stream`, HIP events around the region."""
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    start.record(stream)
+    for _ in range(reps):
+        fn()
+    end.record(stream)
+    end.synchronize()
+    return start.elapsed_time(end) / reps
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    torch.cuda.set_device(local)
+    ctx = S.Context(local)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    log_n = args.log_n
+    n = 1 << log_n
+    import oracle as O
+    w = O.root_of_unity(log_n)
+    host = synthetic(n, 0x5EED0000 + log_n + 7919 * rank)
+    buf = torch.from_numpy(host.view(np.int64)).to(f"cuda:{local}")
+    dptr = buf.data_ptr()
+
+    def step():
+        ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev_ms = timed_events(step, stream, args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * n * args.steps / elapsed
+
+    extras = {}
+    if not args.no_extras:
+        # config 2: 2^20 forward + inverse pair, bit-exact round trip checked
+        n20 = 1 << 20
+        w20 = O.root_of_unity(20)
+        h20 = synthetic(n20, 0x5EED0000 + 20)
+        b20 = torch.from_numpy(h20.view(np.int64)).to(f"cuda:{local}")
+
+        def pair():
+            ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=False, stream=sptr)
+            ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=True, stream=sptr)
+        pair()
+        pair_ms = timed_events(pair, stream, 10)
+        ok = bool(np.array_equal(b20.cpu().numpy().view(np.uint64).reshape(-1, 4), h20))
+        extras["ntt_2^20_fwd_inv_ms"] = round(pair_ms, 4)
+        extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
+        # inverse 2^24 throughput
+        inv_ms = timed_events(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream, 5)
+        extras["intt_2^24_elems_per_s"] = n / (inv_ms / 1000.0)
+        # Merkle: 2^24 leaves of 32 B (canonical Fp, the FRI / L-tree leaves)
+        tree = S.MerkleProofInPlace(ctx)
+        tree.update_dev(dptr, n, 32, stream=sptr)
+        mk_ms = timed_events(lambda: tree.update_dev(dptr, n, 32, stream=sptr), stream, 5)
+        extras["merkle_2^24x32B_leaves_per_s"] = n / (mk_ms / 1000.0)
+        extras["merkle_2^24x32B_ms"] = round(mk_ms, 4)
+        extras["merkle_roofline_frac"] = round(96.0 * n / (mk_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
+        del tree
+        # FRI prove wall clock at precision 2^23 (largest a reference proof can use, fri/src/utils.rs:88)
+        lf = 23
+        nf = 1 << lf
+        wf = O.root_of_unity(lf)
+        coef = synthetic(nf // 4, 0x5EED0000 + lf)
+        hf = np.zeros((nf, 4), dtype=np.uint64)
+        hf[: nf // 4] = coef
+        bf = torch.from_numpy(hf.view(np.int64)).to(f"cuda:{local}")
+        ctx.ntt_dev(bf.data_ptr(), lf, 1, wf, stream=sptr)
+        torch.cuda.synchronize()
+        ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
+        t1 = time.perf_counter()
+        proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
+        extras["fri_prove_2^23_ms"] = round((time.perf_counter() - t1) * 1000.0, 3)
+        extras["fri_layers"] = len(proof)
+
+    ntt_bytes = 64.0 * n                     # read 32 + write 32 B per element per transform
+    achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
+    passes = (log_n + 7) // 8
+    modmuls = (n // 2) * log_n + 2 * n * (passes - 1)   # butterflies + column twiddles (2 products each)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": f"ntt 2^{log_n} = {passes} x ntt_pass_kernel<8>", "ms_per_launch": round(ev_ms, 4)}
+    valu = {"bound": "valu_mad64", "modmuls_per_transform": modmuls,
+            "achieved_mad64_tops": round(modmuls * 136 / (ev_ms / 1000.0) / 1e12, 3),
+            "peak_mad64_tops": MAD64_PEAK_TOPS}
+    valu["frac"] = round(valu["achieved_mad64_tops"] / MAD64_PEAK_TOPS, 4)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle as O2
+        o = O2.Oracle()
+        cores = min(16, os.cpu_count() or 1)
+        threads = 1 << (cores.bit_length() - 1)
+        lc = 21
+        hc = synthetic(1 << lc, 1234)
+        wc = O2.root_of_unity(lc)
+        t2 = time.perf_counter()
+        o.best_fft(hc, wc, lc, cpus=threads)
+        tc = time.perf_counter() - t2
+        cpu = {"value": (1 << lc) / tc, "unit": "field-elems/s", "cores": threads, "kind": "port",
+               "sample": f"one 2^{lc}-point best_fft (oracle C restatement of fft.rs parallel_fft, "
+                         f"{threads} threads), {tc:.2f} s"}
+
+    if rank == 0:
+        line = {"metric": "2^24-pt NTT field-elems/sec", "value": value, "unit": "field-elems/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32x8 (BN254 Fr)",
+                "data": "synthetic (splitmix64 uniform in [0,p), BASELINE.md)",
+                "config": {"workload": f"forward NTT 2^{log_n} BN254 Fr, natural order, HBM-resident",
+                           "global_batch": world, "seq_len": n, "parallelism": f"independent transforms x{world}"},
+                "roofline": roofline, "valu_roofline": valu, "cpu_baseline": cpu}
+        line.update(extras)
+        print(json.dumps(line))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

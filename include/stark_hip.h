@@ -1,0 +1,164 @@
+/*
+ * stark_hip.h -- C ABI of the MI355X (gfx950) FRI-prover hot path.
+ *
+ * Drop-in boundary for the reference's Rust hot path
+ * (InternetMaximalism/stark-pure-rust).  Each entry point names the reference
+ * item it replaces (path:line, relative to the reference repo root).  A Rust
+ * `extern "C"` shim that binds these is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Field elements are BN254 Fr values as 4 little-endian u64 limbs, i.e. the
+ *    32-byte canonical image `Fp::to_bytes_le` produces
+ *    (packages/ff_utils/src/fp.rs:35-44).  Inputs must be < p (every Fp value
+ *    is); outputs are always fully reduced.
+ *  - Host-buffer entry points copy in, compute on the context's GPU, copy out,
+ *    and never retain caller pointers after returning.  Device entry points
+ *    (suffix _dev) take device pointers and a hipStream_t (NULL = the context
+ *    stream) and are asynchronous on that stream.
+ *  - Every call returns a stark_status; 0 = success.  Nothing unwinds.
+ *  - One context per GPU; a context is not shared between threads.
+ */
+#ifndef STARK_HIP_H
+#define STARK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  STARK_OK = 0,
+  STARK_ERR_BAD_LENGTH = 1,   /* len > 2^log_n, or not a power of two where one is required
+                                 (fft.rs:162 assert, merkle_proof_in_place.rs:113 assert) */
+  STARK_ERR_BAD_ROOT = 2,     /* root is not a primitive 2^log_n-th root of unity */
+  STARK_ERR_BAD_ARG = 3,      /* null pointer, index out of range, modulus >= 2^24
+                                 (fri/src/utils.rs:88 assert), ... */
+  STARK_ERR_OOM = 4,          /* device or host allocation failed */
+  STARK_ERR_HIP = 5,          /* a HIP runtime call failed */
+  STARK_ERR_NO_DEVICE = 6,    /* no gfx950 device / bad device ordinal */
+  STARK_ERR_STATE = 7         /* API used out of order (e.g. proofs before update) */
+} stark_status;
+
+typedef struct stark_ctx stark_ctx;
+typedef struct stark_merkle_tree stark_merkle_tree;
+typedef struct stark_fri_proof stark_fri_proof;
+
+/* ---- context ------------------------------------------------------------ */
+/* Replaces commitment::multicore::Worker::new (packages/commitment/src/multicore.rs:43-45):
+ * the unit of parallel execution is one GPU instead of a thread pool. */
+stark_status stark_ctx_create(int device, stark_ctx** out);
+void stark_ctx_destroy(stark_ctx* ctx);
+const char* stark_status_str(stark_status s);
+/* Last HIP error string recorded by the context (for STARK_ERR_HIP). */
+const char* stark_ctx_last_error(const stark_ctx* ctx);
+/* Returns the HIP stream the context launches on (as void* = hipStream_t). */
+void* stark_ctx_stream(stark_ctx* ctx);
+
+/* ---- NTT (packages/fri/src/fft.rs) --------------------------------------- */
+/* best_fft<T>(coefficients: Vec<T>, root_of_unity: &T, log_order_of_root: u32) -> Vec<T>
+ * (fft.rs:327-357).  Zero-pads `len` coefficients to n = 2^log_n and writes the
+ * n evaluations out[i] = sum_j c_j * root^(i*j) to `out` (4*n u64; may alias
+ * `coeffs` when it has room for 4*n u64). */
+stark_status stark_best_fft(stark_ctx* ctx, const uint64_t* coeffs, size_t len, const uint64_t root[4],
+                            uint32_t log_n, uint64_t* out);
+/* inv_best_fft<T>(evaluations, root_of_unity, log_order_of_root) (fft.rs:359-379):
+ * pad, transform with root^-1, scale by n^-1. */
+stark_status stark_inv_best_fft(stark_ctx* ctx, const uint64_t* evals, size_t len, const uint64_t root[4],
+                                uint32_t log_n, uint64_t* out);
+/* serial_fft / parallel_fft / inv_serial_fft / inv_parallel_fft (fft.rs:150, 195, 284, 295):
+ * in place on exactly 2^log_n values (no padding). */
+stark_status stark_fft_in_place(stark_ctx* ctx, uint64_t* values, const uint64_t root[4], uint32_t log_n,
+                                int inverse);
+/* Device-resident batched NTT: `batch` transforms of n = 2^log_n elements,
+ * transform b at d_data + b*4*n u64.  In place.  inverse != 0 => inv_best_fft
+ * semantics.  Asynchronous on `stream` (NULL = context stream). */
+stark_status stark_ntt_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t batch,
+                           const uint64_t root[4], int inverse, void* stream);
+/* expand_root_of_unity<T>(root) -> Vec<T> (fft.rs:5-14): writes
+ * min(order, cap) powers [1, w, w^2, ...] and stores the order in *count.
+ * The order must be a power of two <= 2^28. */
+stark_status stark_expand_root_of_unity(stark_ctx* ctx, const uint64_t root[4], uint64_t* out, size_t cap,
+                                        size_t* count);
+
+/* ---- field-vector kernels (packages/fri/src/poly_utils.rs) --------------- */
+/* multi_inv<T>(values) -> Vec<T> (poly_utils.rs:38-70); zero maps to zero. */
+stark_status stark_multi_inv(stark_ctx* ctx, const uint64_t* values, size_t n, uint64_t* out);
+/* xs.map(|x| eval_poly_at(poly, x)) (poly_utils.rs:93-102 as used at
+ * r1cs-stark/src/prove.rs:216-220): out[i] = sum_k poly[k] * xs[i]^k. */
+stark_status stark_eval_poly_at_multi(stark_ctx* ctx, const uint64_t* poly, size_t deg_plus_1,
+                                      const uint64_t* xs, size_t n, uint64_t* out);
+
+/* ---- Blake2s + index sampler (packages/fri/src/utils.rs) ------------------ */
+/* blake(message) -> Vec<u8> (fri/src/utils.rs:5-10): Blake2s-256, unkeyed. */
+void stark_blake(const uint8_t* msg, size_t len, uint8_t out[32]);
+/* get_pseudorandom_indices(seed, modulus, count, exclude_multiples_of) (fri/src/utils.rs:82-109). */
+stark_status stark_get_pseudorandom_indices(const uint8_t* seed, size_t seed_len, uint32_t modulus,
+                                            size_t count, uint32_t exclude_multiples_of, uint32_t* out);
+
+/* ---- Merkle commitment (packages/commitment/src) --------------------------
+ * MerkleTree<Vec<u8>, BlakeDigest> implemented by MerkleProofInPlace
+ * (merkle_tree.rs:60-73, merkle_proof_in_place.rs:9-50).  The tree lives in
+ * HBM; gen_proofs does not rebuild it (the reference rebuilds on every call,
+ * with identical results). */
+/* MerkleProofInPlace::new (merkle_proof_in_place.rs:16-25) */
+stark_status stark_merkle_new(stark_ctx* ctx, stark_merkle_tree** out);
+void stark_merkle_free(stark_merkle_tree* tree);
+/* update(leaves) (merkle_proof_in_place.rs:37-42) + the hashing of
+ * gen_multi_proofs_multi_core (:106-189): n leaves of leaf_len bytes each,
+ * packed back to back.  n must be a power of two. */
+stark_status stark_merkle_update(stark_merkle_tree* tree, const uint8_t* leaves, size_t n, size_t leaf_len);
+/* Same, leaves already in device memory. */
+stark_status stark_merkle_update_dev(stark_merkle_tree* tree, const uint8_t* d_leaves, size_t n,
+                                     size_t leaf_len, void* stream);
+/* width() (merkle_tree.rs:62) */
+size_t stark_merkle_width(const stark_merkle_tree* tree);
+/* get_root() (merkle_tree.rs:66): *root_len = 32, or 0 before the first
+ * gen_proofs (the reference's H::default() = empty digest, :19). */
+stark_status stark_merkle_get_root(const stark_merkle_tree* tree, uint8_t root[32], size_t* root_len);
+/* gen_proofs(indices) -> Vec<Proof> (merkle_tree.rs:72, merkle_proof_in_place.rs:44-49):
+ * for each of the k indices (caller order, duplicates allowed) writes the leaf
+ * (leaf_len bytes) to leaves_out + i*leaf_len and log2(n) sibling digests
+ * leaf->root to nodes_out + i*log2(n)*32.  Either output may be NULL when
+ * k == 0.  Sets the root returned by get_root. */
+stark_status stark_merkle_gen_proofs(stark_merkle_tree* tree, const size_t* indices, size_t k,
+                                     uint8_t* leaves_out, uint8_t* nodes_out);
+/* verify_multi_branch / Proof::validate (merkle_tree.rs:25-58), host side:
+ * returns STARK_OK when every path hashes to root. */
+stark_status stark_merkle_verify(const uint8_t root[32], const size_t* indices, size_t k,
+                                 const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes, size_t depth);
+
+/* ---- FRI (packages/fri/src/fri.rs) ---------------------------------------- */
+/* prove_low_degree<T, H=BlakeDigest>(values, root_of_unity, max_deg_plus_1,
+ * exclude_multiples_of) -> Vec<FriProof<H>> (fri.rs:46-224).  n = len(values)
+ * must equal the (power-of-two) order of root_of_unity. */
+stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size_t n, const uint64_t root[4],
+                                    size_t max_deg_plus_1, uint32_t exclude_multiples_of,
+                                    stark_fri_proof** out);
+/* Same with values already in device memory (not modified). */
+stark_status stark_prove_low_degree_dev(stark_ctx* ctx, const uint64_t* d_values, size_t n,
+                                        const uint64_t root[4], size_t max_deg_plus_1,
+                                        uint32_t exclude_multiples_of, stark_fri_proof** out);
+void stark_fri_proof_free(stark_fri_proof* proof);
+/* serde_json (compact) encoding of Vec<FriProof<BlakeDigest>> (fri.rs:16-26).
+ * Writes up to cap bytes (NUL-terminated if room) and the full length to *len. */
+stark_status stark_fri_proof_json(const stark_fri_proof* proof, char* buf, size_t cap, size_t* len);
+/* Structured access: number of FriProof entries (Middle... then one Last). */
+size_t stark_fri_proof_num_layers(const stark_fri_proof* proof);
+/* Layer i: *is_last, root2 (Middle), number of column / poly branches, depth of each. */
+stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, int* is_last, uint8_t root2[32],
+                                        size_t* n_column, size_t* column_depth, size_t* n_poly,
+                                        size_t* poly_depth, size_t* n_last);
+
+/* ---- device memory helpers (for callers without their own allocator) ------ */
+stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);
+stark_status stark_dev_free(stark_ctx* ctx, void* d_ptr);
+stark_status stark_memcpy_h2d(stark_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
+stark_status stark_memcpy_d2h(stark_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+stark_status stark_ctx_synchronize(stark_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STARK_HIP_H */

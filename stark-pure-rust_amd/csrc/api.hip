@@ -1,0 +1,217 @@
+// C ABI: contexts, buffers, NTT entry points, Blake2s and the index sampler.
+// Each extern "C" function cites the reference item it replaces in
+// include/stark_hip.h.
+#include <new>
+#include <string.h>
+
+#include "internal.h"
+#include "blake2s.h"
+
+namespace stark {
+
+stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what) {
+  if (ctx) {
+    ctx->last_error = std::string(what) + ": " + hipGetErrorString(e);
+  }
+  return e == hipErrorOutOfMemory ? STARK_ERR_OOM : STARK_ERR_HIP;
+}
+
+stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.ptr) return STARK_OK;
+  if (b.ptr) {
+    hipError_t e = hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipFree");
+  }
+  hipError_t e = hipMalloc(&b.ptr, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    b.ptr = nullptr;
+    return hip_fail(ctx, e, "hipMalloc");
+  }
+  b.bytes = bytes;
+  return STARK_OK;
+}
+
+hipStream_t pick_stream(stark_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+// Host-buffer NTT: copy in (zero-padded), transform on the GPU, copy out.
+static stark_status fft_host(stark_ctx* ctx, const uint64_t* in, size_t len, const uint64_t root[4], uint32_t log_n,
+                             uint64_t* out, bool inverse) {
+  if (!ctx || !root || !out || (len && !in)) return STARK_ERR_BAD_ARG;
+  if (log_n > 28) return STARK_ERR_BAD_LENGTH;
+  const size_t n = (size_t)1 << log_n;
+  if (len > n) return STARK_ERR_BAD_LENGTH;  // fft.rs:162 assert_eq!(values.len(), order)
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  uint64_t use_root[4];
+  memcpy(use_root, root, 32);
+  if (inverse) {  // inv_serial_fft uses root^-1 (fft.rs:288)
+    HostFp w = F.from_canonical(root);
+    F.to_canonical(F.inv(w), use_root);
+  }
+  const Twiddles* tw = nullptr;
+  stark_status st = get_twiddles(ctx, use_root, log_n, &tw);
+  if (st != STARK_OK) return st;
+  st = ensure_buf(ctx, ctx->io, n * sizeof(fe));
+  if (st != STARK_OK) return st;
+  fe* d = (fe*)ctx->io.ptr;
+  if (len) STARK_HIP(ctx, hipMemcpyAsync(d, in, len * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  if (len < n) STARK_HIP(ctx, hipMemsetAsync(d + len, 0, (n - len) * sizeof(fe), ctx->stream));
+  st = ntt_device(ctx, d, log_n, 1, *tw, inverse, ctx->stream);
+  if (st != STARK_OK) return st;
+  STARK_HIP(ctx, hipMemcpyAsync(out, d, n * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+const char* stark_status_str(stark_status s) {
+  switch (s) {
+    case STARK_OK: return "ok";
+    case STARK_ERR_BAD_LENGTH: return "bad length";
+    case STARK_ERR_BAD_ROOT: return "root is not a primitive 2^k-th root of unity";
+    case STARK_ERR_BAD_ARG: return "bad argument";
+    case STARK_ERR_OOM: return "out of memory";
+    case STARK_ERR_HIP: return "HIP runtime error";
+    case STARK_ERR_NO_DEVICE: return "no gfx950 device";
+    case STARK_ERR_STATE: return "bad call order";
+  }
+  return "unknown";
+}
+
+stark_status stark_ctx_create(int device, stark_ctx** out) {
+  if (!out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return STARK_ERR_NO_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return STARK_ERR_NO_DEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return STARK_ERR_NO_DEVICE;
+  stark_ctx* ctx = new (std::nothrow) stark_ctx();
+  if (!ctx) return STARK_ERR_OOM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return STARK_ERR_HIP;
+  }
+  *out = ctx;
+  return STARK_OK;
+}
+
+void stark_ctx_destroy(stark_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->tw)
+    if (kv.second->d_lo) hipFree(kv.second->d_lo);
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2})
+    if (b->ptr) hipFree(b->ptr);
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* stark_ctx_last_error(const stark_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+void* stark_ctx_stream(stark_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+stark_status stark_best_fft(stark_ctx* ctx, const uint64_t* coeffs, size_t len, const uint64_t root[4], uint32_t log_n,
+                            uint64_t* out) {
+  return fft_host(ctx, coeffs, len, root, log_n, out, false);
+}
+
+stark_status stark_inv_best_fft(stark_ctx* ctx, const uint64_t* evals, size_t len, const uint64_t root[4],
+                                uint32_t log_n, uint64_t* out) {
+  return fft_host(ctx, evals, len, root, log_n, out, true);
+}
+
+stark_status stark_fft_in_place(stark_ctx* ctx, uint64_t* values, const uint64_t root[4], uint32_t log_n,
+                                int inverse) {
+  if (log_n > 28) return STARK_ERR_BAD_LENGTH;
+  return fft_host(ctx, values, (size_t)1 << log_n, root, log_n, values, inverse != 0);
+}
+
+stark_status stark_ntt_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t batch, const uint64_t root[4],
+                           int inverse, void* stream) {
+  if (!ctx || !d_data || !root) return STARK_ERR_BAD_ARG;
+  if (log_n > 28) return STARK_ERR_BAD_LENGTH;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  uint64_t use_root[4];
+  memcpy(use_root, root, 32);
+  if (inverse) F.to_canonical(F.inv(F.from_canonical(root)), use_root);
+  const Twiddles* tw = nullptr;
+  stark_status st = get_twiddles(ctx, use_root, log_n, &tw);
+  if (st != STARK_OK) return st;
+  return ntt_device(ctx, (fe*)d_data, log_n, batch, *tw, inverse != 0, pick_stream(ctx, stream));
+}
+
+void stark_blake(const uint8_t* msg, size_t len, uint8_t out[32]) { b2s_host(msg, len, out); }
+
+stark_status stark_get_pseudorandom_indices(const uint8_t* seed, size_t seed_len, uint32_t modulus, size_t count,
+                                            uint32_t exclude_multiples_of, uint32_t* out) {
+  if ((count && !out) || (seed_len && !seed)) return STARK_ERR_BAD_ARG;
+  if (modulus >= (1u << 24)) return STARK_ERR_BAD_ARG;  // fri/src/utils.rs:88
+  // data[len-32..] must exist when the seed is extended (utils.rs:91).
+  if (seed_len < 4 * count && seed_len < 32) return STARK_ERR_BAD_ARG;
+  uint32_t real_mod = modulus;
+  if (exclude_multiples_of != 0) {
+    if (exclude_multiples_of == 1) return STARK_ERR_BAD_ARG;  // division by zero in the reference
+    // The reference computes modulus * (e - 1) in u32 (utils.rs:101); refuse inputs where that overflows.
+    if ((uint64_t)modulus * (exclude_multiples_of - 1) > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+    real_mod = (uint32_t)((uint64_t)modulus * (exclude_multiples_of - 1) / exclude_multiples_of);
+  }
+  if (count && real_mod == 0) return STARK_ERR_BAD_ARG;  // % 0 panics in the reference
+  std::vector<uint8_t> data(seed, seed + seed_len);
+  while (data.size() < 4 * count) {
+    uint8_t d[32];
+    b2s_host(data.data() + data.size() - 32, 32, d);
+    data.insert(data.end(), d, d + 32);
+  }
+  for (size_t i = 0; i < count; ++i) {
+    const uint32_t w = ((uint32_t)data[4 * i] << 24) | ((uint32_t)data[4 * i + 1] << 16) |
+                       ((uint32_t)data[4 * i + 2] << 8) | (uint32_t)data[4 * i + 3];
+    const uint32_t v = w % real_mod;
+    out[i] = exclude_multiples_of ? v + 1 + v / (exclude_multiples_of - 1) : v;
+  }
+  return STARK_OK;
+}
+
+stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr) {
+  if (!ctx || !d_ptr) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipMalloc(d_ptr, bytes ? bytes : 16));
+  return STARK_OK;
+}
+stark_status stark_dev_free(stark_ctx* ctx, void* d_ptr) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipFree(d_ptr));
+  return STARK_OK;
+}
+stark_status stark_memcpy_h2d(stark_ctx* ctx, void* d_dst, const void* h_src, size_t bytes) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+stark_status stark_memcpy_d2h(stark_ctx* ctx, void* h_dst, const void* d_src, size_t bytes) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+stark_status stark_ctx_synchronize(stark_ctx* ctx) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,308 @@
+// FRI prover (prove_low_degree, packages/fri/src/fri.rs:46-224) on gfx950.
+//
+// Per layer, everything large stays in HBM: the Merkle tree of the layer's
+// values, the 4->1 fold, the Merkle tree of the folded column and the
+// proof-path gathers.  The host only runs the transcript (root -> special_x,
+// Blake2s index sampling) and assembles the proof.
+//
+// Fold (fri.rs:141-164 with multi_interp_4 poly_utils.rs:449-511 and
+// eval_quartic :442-446): row i interpolates the cubic through
+// (w^(i + j n/4), v[i + j n/4]), j = 0..3, and evaluates it at special_x.
+// The four x's are x0 * zeta^j with zeta = w^(n/4) (zeta^2 = -1), so with
+// u = special_x / x0 the cubic's value is sum_k d_k u^k where d = the inverse
+// 4-point DFT of the y's:
+//   d0 = (y0+y1+y2+y3)/4         d2 = (y0-y1+y2-y3)/4
+//   d1 = ((y0-y2) - zeta(y1-y3))/4  d3 = ((y0-y2) + zeta(y1-y3))/4
+// It is the same unique cubic, so the column is bit-identical to the
+// reference's, with 7 modular products per row and no batch inverse.
+#include <string.h>
+
+#include <array>
+#include <string>
+
+#include "internal.h"
+#include "blake2s.h"
+
+// Defined in merkle.hip.
+namespace stark {
+stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                          hipStream_t stream);
+stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
+stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
+                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream);
+}  // namespace stark
+
+struct stark_fri_layer {
+  bool last = false;
+  uint8_t root2[32];
+  size_t col_depth = 0, poly_depth = 0;
+  std::vector<size_t> col_idx, poly_idx;
+  std::vector<uint8_t> col_leaves, col_nodes;    // 32 B leaves, depth*32 B paths
+  std::vector<uint8_t> poly_leaves, poly_nodes;
+  std::vector<uint8_t> last_values;              // n * 32 B
+};
+
+struct stark_fri_proof {
+  std::vector<stark_fri_layer> layers;
+};
+
+namespace stark {
+
+__global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
+                                const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, fe s_m, fe zeta_m,
+                                fe inv4_m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q) return;
+  const fe y0 = fe_load(v + i), y1 = fe_load(v + i + q), y2 = fe_load(v + i + 2 * q), y3 = fe_load(v + i + 3 * q);
+  const uint64_t e = i << shift;
+  const fe winv = fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]);  // Montgomery w^-i
+  const fe u_m = fe_mul(s_m, winv);                                         // Montgomery special_x * w^-i
+  const fe s02 = fe_add(y0, y2), s13 = fe_add(y1, y3);
+  const fe e02 = fe_sub(y0, y2);
+  const fe z = fe_mul(fe_sub(y1, y3), zeta_m);
+  const fe d0 = fe_add(s02, s13), d2 = fe_sub(s02, s13);
+  const fe d1 = fe_sub(e02, z), d3 = fe_add(e02, z);
+  fe acc = fe_add(fe_mul(d3, u_m), d2);
+  acc = fe_add(fe_mul(acc, u_m), d1);
+  acc = fe_add(fe_mul(acc, u_m), d0);
+  fe_store(col + i, fe_mul(acc, inv4_m));
+}
+
+static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
+                               size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out) {
+  const FieldHost& F = FieldHost::get();
+  hipStream_t s = ctx->stream;
+  auto proof = std::make_unique<stark_fri_proof>();
+  // Layer sizes and checks up front (the reference panics on these).
+  size_t layers = 0;
+  {
+    size_t m = n, deg = max_deg_plus_1;
+    while (deg > 16) {
+      if (m < 8 || (m & (m - 1))) return STARK_ERR_BAD_LENGTH;
+      if (excl != 0 && (excl == 1 || (uint64_t)(m / 4) * (excl - 1) / excl == 0)) return STARK_ERR_BAD_ARG;
+      if (m / 4 >= (1u << 24)) return STARK_ERR_BAD_ARG;  // get_pseudorandom_indices assert
+      m /= 4;
+      deg /= 4;
+      ++layers;
+    }
+  }
+  const Twiddles* tw = nullptr;
+  uint32_t log_n0 = 0;
+  while (((size_t)1 << log_n0) < n) ++log_n0;
+  if (layers > 0) {
+    // values.len() must equal the order of root (xs = expand_root_of_unity, fri.rs:84).
+    uint64_t inv_root[4];
+    F.to_canonical(F.inv(F.from_canonical(root)), inv_root);
+    stark_status st = get_twiddles(ctx, inv_root, log_n0, &tw);
+    if (st != STARK_OK) return st;
+  }
+  // Column buffers: n/4 + n/16 + ... elements.
+  size_t col_total = 0;
+  {
+    size_t m = n;
+    for (size_t l = 0; l < layers; ++l) {
+      m /= 4;
+      col_total += m;
+    }
+  }
+  DevBuf cols;
+  stark_status st = ensure_buf(ctx, cols, (col_total ? col_total : 1) * sizeof(fe));
+  if (st != STARK_OK) return st;
+  struct Guard {
+    DevBuf* b;
+    ~Guard() {
+      if (b->ptr) hipFree(b->ptr);
+    }
+  } guard{&cols};
+  stark_merkle_tree* trees[2] = {nullptr, nullptr};
+  st = stark_merkle_new(ctx, &trees[0]);
+  if (st == STARK_OK) st = stark_merkle_new(ctx, &trees[1]);
+  struct TreeGuard {
+    stark_merkle_tree** t;
+    ~TreeGuard() {
+      stark_merkle_free(t[0]);
+      stark_merkle_free(t[1]);
+    }
+  } tguard{trees};
+  if (st != STARK_OK) return st;
+
+  const fe* cur = d_values;
+  fe* next = (fe*)cols.ptr;
+  size_t m = n, deg = max_deg_plus_1;
+  int tc = 0;  // trees[tc] holds the tree of `cur`
+  HostFp w = F.from_canonical(root);
+  const HostFp inv4 = F.inv(F.from_u64(4));
+  for (size_t layer = 0; layer < layers; ++layer) {
+    if (layer == 0) {
+      st = merkle_build(ctx, trees[tc], (const uint8_t*)cur, m, 32, s);
+      if (st != STARK_OK) return st;
+    }
+    uint8_t m_root[32];
+    st = merkle_root_d2h(ctx, trees[tc], s, m_root);
+    if (st != STARK_OK) return st;
+    // special_x = T::from_bytes_le(m_root) (fri.rs:135): reduced mod p.
+    const HostFp sx = F.from_bytes_le(m_root, 32);
+    const size_t q = m / 4;
+    const HostFp zeta = F.pow_u64(w, q);  // w^(n/4)
+    const unsigned blocks = (unsigned)((q + 255) / 256);
+    hipLaunchKernelGGL(fri_fold_kernel, dim3(blocks), dim3(256), 0, s, cur, next, (uint64_t)q, (uint32_t)(2 * layer),
+                       tw->d_lo, tw->d_hi, tw->kb, to_dev(sx), to_dev(zeta), to_dev(inv4));
+    STARK_HIP(ctx, hipGetLastError());
+    st = merkle_build(ctx, trees[1 - tc], (const uint8_t*)next, q, 32, s);
+    if (st != STARK_OK) return st;
+    stark_fri_layer L;
+    st = merkle_root_d2h(ctx, trees[1 - tc], s, L.root2);
+    if (st != STARK_OK) return st;
+    // ys = get_pseudorandom_indices(m2_root, column.len(), 40, exclude) (fri.rs:181-189)
+    uint32_t ys[40];
+    st = stark_get_pseudorandom_indices(L.root2, 32, (uint32_t)q, 40, excl, ys);
+    if (st != STARK_OK) return st;
+    L.col_idx.assign(ys, ys + 40);
+    for (int i = 0; i < 40; ++i)
+      for (int j = 0; j < 4; ++j) L.poly_idx.push_back((size_t)ys[i] + q * j);  // fri.rs:193-204
+    L.col_depth = 0;
+    while (((size_t)1 << L.col_depth) < q) ++L.col_depth;
+    L.poly_depth = L.col_depth + 2;
+    L.col_leaves.resize(40 * 32);
+    L.col_nodes.resize(40 * L.col_depth * 32);
+    L.poly_leaves.resize(160 * 32);
+    L.poly_nodes.resize(160 * L.poly_depth * 32);
+    st = merkle_gather(ctx, trees[1 - tc], L.col_idx.data(), 40, L.col_leaves.data(), L.col_nodes.data(), s);
+    if (st != STARK_OK) return st;
+    st = merkle_gather(ctx, trees[tc], L.poly_idx.data(), 160, L.poly_leaves.data(), L.poly_nodes.data(), s);
+    if (st != STARK_OK) return st;
+    proof->layers.push_back(std::move(L));
+    // Recurse on the column with w^4 (fri.rs:215-223); its tree is the one just built.
+    cur = next;
+    next += q;
+    m = q;
+    deg /= 4;
+    w = F.pow_u64(w, 4);
+    tc = 1 - tc;
+  }
+  // Last { last: values.map(to_bytes_le) } (fri.rs:108-110)
+  stark_fri_layer last;
+  last.last = true;
+  last.last_values.resize(m * 32);
+  if (m) STARK_HIP(ctx, hipMemcpyAsync(last.last_values.data(), cur, m * 32, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  proof->layers.push_back(std::move(last));
+  *out = proof.release();
+  return STARK_OK;
+}
+
+static void json_bytes(std::string& o, const uint8_t* p, size_t n) {
+  o.push_back('[');
+  char tmp[8];
+  for (size_t i = 0; i < n; ++i) {
+    int k = snprintf(tmp, sizeof tmp, i ? ",%u" : "%u", (unsigned)p[i]);
+    o.append(tmp, (size_t)k);
+  }
+  o.push_back(']');
+}
+
+static void json_branches(std::string& o, const std::vector<uint8_t>& leaves, const std::vector<uint8_t>& nodes,
+                          size_t k, size_t depth) {
+  o.push_back('[');
+  for (size_t i = 0; i < k; ++i) {
+    if (i) o.push_back(',');
+    o += "{\"leaf\":";
+    json_bytes(o, leaves.data() + 32 * i, 32);
+    o += ",\"nodes\":[";
+    for (size_t d = 0; d < depth; ++d) {
+      if (d) o.push_back(',');
+      json_bytes(o, nodes.data() + (i * depth + d) * 32, 32);
+    }
+    o += "]}";
+  }
+  o.push_back(']');
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+stark_status stark_prove_low_degree_dev(stark_ctx* ctx, const uint64_t* d_values, size_t n, const uint64_t root[4],
+                                        size_t max_deg_plus_1, uint32_t exclude_multiples_of, stark_fri_proof** out) {
+  if (!ctx || !root || !out || (n && !d_values)) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  return prove_impl(ctx, (const fe*)d_values, n, root, max_deg_plus_1, exclude_multiples_of, out);
+}
+
+stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size_t n, const uint64_t root[4],
+                                    size_t max_deg_plus_1, uint32_t exclude_multiples_of, stark_fri_proof** out) {
+  if (!ctx || !root || !out || (n && !values)) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  DevBuf buf;
+  stark_status st = ensure_buf(ctx, buf, (n ? n : 1) * sizeof(fe));
+  if (st != STARK_OK) return st;
+  if (n) {
+    hipError_t e = hipMemcpyAsync(buf.ptr, values, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) {
+      hipFree(buf.ptr);
+      return hip_fail(ctx, e, "hipMemcpyAsync");
+    }
+  }
+  st = prove_impl(ctx, (const fe*)buf.ptr, n, root, max_deg_plus_1, exclude_multiples_of, out);
+  hipStreamSynchronize(ctx->stream);
+  hipFree(buf.ptr);
+  return st;
+}
+
+void stark_fri_proof_free(stark_fri_proof* proof) { delete proof; }
+
+stark_status stark_fri_proof_json(const stark_fri_proof* proof, char* buf, size_t cap, size_t* len) {
+  if (!proof || !len) return STARK_ERR_BAD_ARG;
+  std::string o = "[";
+  for (size_t l = 0; l < proof->layers.size(); ++l) {
+    const stark_fri_layer& L = proof->layers[l];
+    if (l) o.push_back(',');
+    if (L.last) {
+      o += "{\"Last\":{\"last\":[";
+      for (size_t i = 0; i < L.last_values.size() / 32; ++i) {
+        if (i) o.push_back(',');
+        json_bytes(o, L.last_values.data() + 32 * i, 32);
+      }
+      o += "]}}";
+    } else {
+      o += "{\"Middle\":{\"root2\":";
+      json_bytes(o, L.root2, 32);
+      o += ",\"column_branches\":";
+      json_branches(o, L.col_leaves, L.col_nodes, L.col_idx.size(), L.col_depth);
+      o += ",\"poly_branches\":";
+      json_branches(o, L.poly_leaves, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
+      o += "}}";
+    }
+  }
+  o.push_back(']');
+  *len = o.size();
+  if (buf && cap) {
+    const size_t k = o.size() < cap ? o.size() : cap;
+    memcpy(buf, o.data(), k);
+    if (k < cap) buf[k] = 0;
+  }
+  return STARK_OK;
+}
+
+size_t stark_fri_proof_num_layers(const stark_fri_proof* proof) { return proof ? proof->layers.size() : 0; }
+
+stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, int* is_last, uint8_t root2[32],
+                                        size_t* n_column, size_t* column_depth, size_t* n_poly, size_t* poly_depth,
+                                        size_t* n_last) {
+  if (!proof || i >= proof->layers.size()) return STARK_ERR_BAD_ARG;
+  const stark_fri_layer& L = proof->layers[i];
+  if (is_last) *is_last = L.last ? 1 : 0;
+  if (root2) memcpy(root2, L.root2, 32);
+  if (n_column) *n_column = L.col_idx.size();
+  if (column_depth) *column_depth = L.col_depth;
+  if (n_poly) *n_poly = L.poly_idx.size();
+  if (poly_depth) *poly_depth = L.poly_depth;
+  if (n_last) *n_last = L.last_values.size() / 32;
+  return STARK_OK;
+}
+
+}  // extern "C"

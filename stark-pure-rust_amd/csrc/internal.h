@@ -1,0 +1,81 @@
+// Internal declarations shared by the HIP translation units of libstark_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/stark_hip.h"
+#include "fp_dev.h"
+#include "fp_host.h"
+
+namespace stark {
+
+// Device buffer owned by a context.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+// Twiddle set for one (root, log_n): everything in Montgomery form.
+//   lo[i] = w^i                   i < 2^kb
+//   hi[i] = w^(i * 2^kb)          i < 2^(log_n - kb)
+//   small_off[l] = offset into `small` of w_R^k = w^(k * n / R), k < R/2, R = 2^l
+struct Twiddles {
+  uint32_t log_n = 0, kb = 0;
+  fe* d_lo = nullptr;
+  fe* d_hi = nullptr;
+  fe* d_small = nullptr;
+  uint32_t small_off[16] = {0};
+  HostFp root;      // the root these tables were built for (Montgomery)
+  HostFp inv_n;     // n^-1 (Montgomery)
+};
+
+}  // namespace stark
+
+struct stark_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  stark::DevBuf scratch;   // NTT ping-pong partner
+  stark::DevBuf io;        // staging for host-buffer entry points
+  stark::DevBuf io2;
+  // (root canonical limbs, log_n) -> tables
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
+};
+
+namespace stark {
+
+stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
+#define STARK_HIP(ctx, call)                                  \
+  do {                                                        \
+    hipError_t e_ = (call);                                   \
+    if (e_ != hipSuccess) return ::stark::hip_fail(ctx, e_, #call); \
+  } while (0)
+
+stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
+hipStream_t pick_stream(stark_ctx* ctx, void* stream);
+
+// Returns tables for `root` (canonical limbs) of order exactly 2^log_n, or
+// STARK_ERR_BAD_ROOT.  Cached per context.
+stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n, const Twiddles** out);
+
+// Device NTT over `batch` contiguous transforms (in place, canonical values).
+stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
+                        bool inverse, hipStream_t stream);
+
+// Montgomery image of a host value as a device fe (same bytes).
+inline fe to_dev(const HostFp& x) {
+  fe r;
+  for (int i = 0; i < 4; ++i) {
+    r.w[2 * i] = (uint32_t)x.v[i];
+    r.w[2 * i + 1] = (uint32_t)(x.v[i] >> 32);
+  }
+  return r;
+}
+
+}  // namespace stark

@@ -1,0 +1,365 @@
+// Blake2s Merkle commitment on gfx950: the tree of
+// gen_multi_proofs_multi_core (packages/commitment/src/merkle_proof_in_place.rs:106-206):
+// leaf node = Blake2s(leaf bytes), parent = Blake2s(left || right), root =
+// the single node of the top level.  The reference splits the tree into
+// 2^log2(cpus) subtrees and a top tree; every split yields this same tree.
+//
+// HBM layout: all 2n-1 digests, level-major (level 0 = leaf digests, then
+// n/2 parents, ... , root), each 32 B.  gen_proofs only gathers siblings from
+// this resident tree.
+//
+// Build: one workgroup owns a block of 1024 nodes of its input level: it
+// hashes them (leaf mode: one leaf per node; pair mode: two child digests per
+// node read from the level below), then reduces the block in LDS for up to
+// 10 further levels, writing every level to HBM.  Three launches cover
+// 2^24 leaves.
+#include "internal.h"
+#include "blake2s.h"
+
+struct stark_merkle_tree {
+  stark_ctx* ctx = nullptr;
+  size_t n = 0, leaf_len = 0;
+  uint32_t depth = 0;                // log2(n)
+  stark::DevBuf nodes;               // (2n - 1) * 32 B
+  stark::DevBuf own_leaves;          // leaves copied from the host
+  const uint8_t* d_leaves = nullptr; // leaves the proofs are read from
+  bool built = false;
+  bool has_root = false;             // set by gen_proofs (reference: root = H::default() before)
+  uint8_t root[32];
+  stark::DevBuf gather;              // scratch for proof gathers
+};
+
+namespace stark {
+
+constexpr uint32_t kMerkleBlock = 1024;   // nodes per workgroup at its input level
+constexpr uint32_t kMerkleThreads = 256;
+
+struct Digest {
+  uint32_t h[8];
+};
+
+// Digest of one leaf of `len` bytes at p.
+__device__ __forceinline__ Digest hash_leaf(const uint8_t* __restrict__ p, uint32_t len) {
+  Digest d;
+  b2s_init(d.h);
+  uint32_t m[16];
+  const bool vec = ((((uintptr_t)p) & 15) == 0) && ((len & 15) == 0);
+  uint32_t off = 0;
+  // Full blocks that are not the last one.
+  while (len - off > 64) {
+    if (vec) {
+      const uint4* q = reinterpret_cast<const uint4*>(p + off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint4 x = q[i];
+        m[4 * i] = x.x; m[4 * i + 1] = x.y; m[4 * i + 2] = x.z; m[4 * i + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        m[i] = (uint32_t)p[off + 4 * i] | ((uint32_t)p[off + 4 * i + 1] << 8) |
+               ((uint32_t)p[off + 4 * i + 2] << 16) | ((uint32_t)p[off + 4 * i + 3] << 24);
+    }
+    off += 64;
+    b2s_compress(d.h, m, off, 0, false);
+  }
+  // Final (possibly partial or empty) block, zero padded.
+  const uint32_t rem = len - off;
+  if (vec) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + off);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint4 x = (uint32_t)(16 * i) < rem ? q[i] : make_uint4(0, 0, 0, 0);
+      m[4 * i] = x.x; m[4 * i + 1] = x.y; m[4 * i + 2] = x.z; m[4 * i + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      uint32_t w = 0;
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = 4 * i + k;
+        if (b < rem) w |= (uint32_t)p[off + b] << (8 * k);
+      }
+      m[i] = w;
+    }
+  }
+  b2s_compress(d.h, m, len, 0, true);
+  return d;
+}
+
+__device__ __forceinline__ Digest hash_pair(const Digest& l, const Digest& r) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[i] = l.h[i];
+    m[i + 8] = r.h[i];
+  }
+  Digest d;
+  b2s_init(d.h);
+  b2s_compress(d.h, m, 64, 0, true);
+  return d;
+}
+
+__device__ __forceinline__ Digest load_digest(const Digest* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  Digest d;
+  d.h[0] = a.x; d.h[1] = a.y; d.h[2] = a.z; d.h[3] = a.w;
+  d.h[4] = b.x; d.h[5] = b.y; d.h[6] = b.z; d.h[7] = b.w;
+  return d;
+}
+__device__ __forceinline__ void store_digest(Digest* p, const Digest& d) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4(d.h[0], d.h[1], d.h[2], d.h[3]);
+  q[1] = make_uint4(d.h[4], d.h[5], d.h[6], d.h[7]);
+}
+
+// One launch: input level `lvl_in` nodes [0, count) are produced by this
+// workgroup's block (leaf mode: from leaves; pair mode: from level lvl_in-1
+// at `below`), then `extra` more levels are reduced in LDS.
+//   out_level[k] = pointer to level (lvl_in + k) in the node buffer.
+struct LevelPtrs {
+  Digest* lv[12];
+};
+
+__global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint8_t* __restrict__ leaves,
+                                                                      uint32_t leaf_len,
+                                                                      const Digest* __restrict__ below,
+                                                                      uint64_t count, uint32_t extra,
+                                                                      LevelPtrs out) {
+  __shared__ __attribute__((aligned(16))) Digest lds[kMerkleBlock];
+  const uint64_t base = (uint64_t)blockIdx.x * kMerkleBlock;
+  const uint32_t here = (uint32_t)((count - base) < kMerkleBlock ? (count - base) : kMerkleBlock);
+  for (uint32_t i = threadIdx.x; i < here; i += blockDim.x) {
+    const uint64_t node = base + i;
+    Digest d;
+    if (leaves) {
+      d = hash_leaf(leaves + node * leaf_len, leaf_len);
+    } else {
+      d = hash_pair(load_digest(below + 2 * node), load_digest(below + 2 * node + 1));
+    }
+    store_digest(out.lv[0] + node, d);
+    lds[i] = d;
+  }
+  __syncthreads();
+  uint32_t width = here;
+  for (uint32_t k = 1; k <= extra; ++k) {
+    width >>= 1;
+    Digest res[kMerkleBlock / 2 / kMerkleThreads];
+    uint32_t c = 0;
+    for (uint32_t i = threadIdx.x; i < width; i += blockDim.x) res[c++] = hash_pair(lds[2 * i], lds[2 * i + 1]);
+    __syncthreads();
+    c = 0;
+    for (uint32_t i = threadIdx.x; i < width; i += blockDim.x) {
+      lds[i] = res[c];
+      store_digest(out.lv[k] + (base >> k) + i, res[c]);
+      ++c;
+    }
+    __syncthreads();
+  }
+}
+
+// Proof gather: for proof i (index idx[i]): the leaf bytes and the depth
+// siblings ((idx >> d) ^ 1 at level d), leaf -> root.
+__global__ void merkle_gather_kernel(const uint8_t* __restrict__ leaves, uint32_t leaf_len,
+                                     const Digest* __restrict__ nodes, uint64_t n, uint32_t depth,
+                                     const uint64_t* __restrict__ idx, uint32_t k, uint8_t* __restrict__ leaf_out,
+                                     Digest* __restrict__ node_out) {
+  const uint32_t i = blockIdx.x;
+  if (i >= k) return;
+  const uint64_t id = idx[i];
+  for (uint32_t b = threadIdx.x; b < leaf_len; b += blockDim.x) leaf_out[(uint64_t)i * leaf_len + b] = leaves[id * leaf_len + b];
+  uint64_t off = 0, width = n;
+  for (uint32_t d = 0; d < depth; ++d) {
+    if (threadIdx.x == d % blockDim.x) node_out[(uint64_t)i * depth + d] = nodes[off + ((id >> d) ^ 1)];
+    off += width;
+    width >>= 1;
+  }
+}
+
+static uint64_t level_offset(uint64_t n, uint32_t level) {
+  uint64_t off = 0, w = n;
+  for (uint32_t l = 0; l < level; ++l) {
+    off += w;
+    w >>= 1;
+  }
+  return off;
+}
+
+// Builds every level of the tree over d_leaves (n leaves of leaf_len bytes).
+stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                          hipStream_t stream) {
+  if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
+  if (leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  uint32_t depth = 0;
+  while (((size_t)1 << depth) < n) ++depth;
+  stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
+  if (st != STARK_OK) return st;
+  Digest* nodes = (Digest*)t->nodes.ptr;
+  uint32_t level = 0;
+  uint64_t count = n;
+  bool leaf_mode = true;
+  while (true) {
+    // Levels reducible inside a block of min(count, 1024) nodes.
+    const uint64_t blk = count < kMerkleBlock ? count : kMerkleBlock;
+    uint32_t extra = 0;
+    while ((blk >> (extra + 1)) >= 1 && extra + 1 <= 10 && level + extra + 1 <= depth) ++extra;
+    LevelPtrs lp;
+    for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
+    const unsigned grid = (unsigned)((count + kMerkleBlock - 1) / kMerkleBlock);
+    const Digest* below = leaf_mode ? nullptr : nodes + level_offset(n, level - 1);
+    hipLaunchKernelGGL(merkle_build_kernel, dim3(grid), dim3(kMerkleThreads), 0, stream,
+                       leaf_mode ? d_leaves : nullptr, (uint32_t)leaf_len, below, count, extra, lp);
+    STARK_HIP(ctx, hipGetLastError());
+    level += extra;
+    count >>= extra;
+    if (level == depth) break;
+    // Next launch starts by hashing pairs of the current top level.
+    ++level;
+    count >>= 1;
+    leaf_mode = false;
+    if (level == depth && count == 1) {
+      // A single pair remains: handled by a 1-node launch.
+    }
+  }
+  t->n = n;
+  t->leaf_len = leaf_len;
+  t->depth = depth;
+  t->d_leaves = d_leaves;
+  t->built = true;
+  return STARK_OK;
+}
+
+stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]) {
+  const Digest* nodes = (const Digest*)t->nodes.ptr;
+  STARK_HIP(ctx, hipMemcpyAsync(out, nodes + (2 * t->n - 2), 32, hipMemcpyDeviceToHost, stream));
+  STARK_HIP(ctx, hipStreamSynchronize(stream));
+  return STARK_OK;
+}
+
+// Gathers k proofs (leaf bytes + siblings) to host buffers.
+stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
+                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream) {
+  if (k == 0) return STARK_OK;
+  for (size_t i = 0; i < k; ++i)
+    if (indices[i] >= t->n) return STARK_ERR_BAD_ARG;
+  const size_t idx_bytes = k * sizeof(uint64_t);
+  const size_t leaf_bytes = k * t->leaf_len;
+  const size_t node_bytes = k * t->depth * sizeof(Digest);
+  const size_t total = idx_bytes + ((leaf_bytes + 15) & ~(size_t)15) + node_bytes;
+  stark_status st = ensure_buf(ctx, t->gather, total);
+  if (st != STARK_OK) return st;
+  uint8_t* base = (uint8_t*)t->gather.ptr;
+  uint64_t* d_idx = (uint64_t*)base;
+  uint8_t* d_leaf = base + idx_bytes;
+  Digest* d_node = (Digest*)(base + idx_bytes + ((leaf_bytes + 15) & ~(size_t)15));
+  std::vector<uint64_t> h_idx(indices, indices + k);
+  STARK_HIP(ctx, hipMemcpyAsync(d_idx, h_idx.data(), idx_bytes, hipMemcpyHostToDevice, stream));
+  hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)k), dim3(64), 0, stream, t->d_leaves,
+                     (uint32_t)t->leaf_len, (const Digest*)t->nodes.ptr, (uint64_t)t->n, t->depth, d_idx,
+                     (uint32_t)k, d_leaf, d_node);
+  STARK_HIP(ctx, hipGetLastError());
+  if (leaves_out) STARK_HIP(ctx, hipMemcpyAsync(leaves_out, d_leaf, leaf_bytes, hipMemcpyDeviceToHost, stream));
+  if (nodes_out && node_bytes)
+    STARK_HIP(ctx, hipMemcpyAsync(nodes_out, d_node, node_bytes, hipMemcpyDeviceToHost, stream));
+  STARK_HIP(ctx, hipStreamSynchronize(stream));
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+stark_status stark_merkle_new(stark_ctx* ctx, stark_merkle_tree** out) {
+  if (!ctx || !out) return STARK_ERR_BAD_ARG;
+  stark_merkle_tree* t = new (std::nothrow) stark_merkle_tree();
+  if (!t) return STARK_ERR_OOM;
+  t->ctx = ctx;
+  *out = t;
+  return STARK_OK;
+}
+
+void stark_merkle_free(stark_merkle_tree* t) {
+  if (!t) return;
+  hipSetDevice(t->ctx->device);
+  if (t->nodes.ptr) hipFree(t->nodes.ptr);
+  if (t->own_leaves.ptr) hipFree(t->own_leaves.ptr);
+  if (t->gather.ptr) hipFree(t->gather.ptr);
+  delete t;
+}
+
+stark_status stark_merkle_update(stark_merkle_tree* t, const uint8_t* leaves, size_t n, size_t leaf_len) {
+  if (!t || (!leaves && n * leaf_len)) return STARK_ERR_BAD_ARG;
+  if (n == 0 || (n & (n - 1))) return STARK_ERR_BAD_LENGTH;
+  stark_ctx* ctx = t->ctx;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  stark_status st = ensure_buf(ctx, t->own_leaves, n * leaf_len ? n * leaf_len : 16);
+  if (st != STARK_OK) return st;
+  if (n * leaf_len)
+    STARK_HIP(ctx, hipMemcpyAsync(t->own_leaves.ptr, leaves, n * leaf_len, hipMemcpyHostToDevice, ctx->stream));
+  st = merkle_build(ctx, t, (const uint8_t*)t->own_leaves.ptr, n, leaf_len, ctx->stream);
+  if (st != STARK_OK) return st;
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+
+stark_status stark_merkle_update_dev(stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                                     void* stream) {
+  if (!t || (!d_leaves && n * leaf_len)) return STARK_ERR_BAD_ARG;
+  stark_ctx* ctx = t->ctx;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  return merkle_build(ctx, t, d_leaves, n, leaf_len, pick_stream(ctx, stream));
+}
+
+size_t stark_merkle_width(const stark_merkle_tree* t) { return t ? t->n : 0; }
+
+stark_status stark_merkle_get_root(const stark_merkle_tree* t, uint8_t root[32], size_t* root_len) {
+  if (!t || !root_len) return STARK_ERR_BAD_ARG;
+  if (!t->has_root) {
+    *root_len = 0;
+    return STARK_OK;
+  }
+  if (root) memcpy(root, t->root, 32);
+  *root_len = 32;
+  return STARK_OK;
+}
+
+stark_status stark_merkle_gen_proofs(stark_merkle_tree* t, const size_t* indices, size_t k, uint8_t* leaves_out,
+                                     uint8_t* nodes_out) {
+  if (!t || (k && !indices)) return STARK_ERR_BAD_ARG;
+  if (!t->built) return STARK_ERR_STATE;
+  stark_ctx* ctx = t->ctx;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  stark_status st = merkle_root_d2h(ctx, t, ctx->stream, t->root);
+  if (st != STARK_OK) return st;
+  t->has_root = true;
+  return merkle_gather(ctx, t, indices, k, leaves_out, nodes_out, ctx->stream);
+}
+
+stark_status stark_merkle_verify(const uint8_t root[32], const size_t* indices, size_t k, const uint8_t* leaves,
+                                 size_t leaf_len, const uint8_t* nodes, size_t depth) {
+  if (!root || (k && (!indices || !leaves || (depth && !nodes)))) return STARK_ERR_BAD_ARG;
+  for (size_t i = 0; i < k; ++i) {
+    uint8_t cur[32], msg[64];
+    b2s_host(leaves + i * leaf_len, leaf_len, cur);
+    size_t pos = indices[i];
+    for (size_t d = 0; d < depth; ++d) {
+      const uint8_t* sib = nodes + (i * depth + d) * 32;
+      if (pos % 2 == 0) {
+        memcpy(msg, cur, 32);
+        memcpy(msg + 32, sib, 32);
+      } else {
+        memcpy(msg, sib, 32);
+        memcpy(msg + 32, cur, 32);
+      }
+      b2s_host(msg, 64, cur);
+      pos /= 2;
+    }
+    if (memcmp(cur, root, 32) != 0) return STARK_ERR_BAD_ARG;
+  }
+  return STARK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+"""GPU parity: Blake2s Merkle trees, FRI proofs and field-vector kernels vs
+the oracle and the reference's KATs."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import stark_amd as S
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+KATS = json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))
+GOLD = json.load(open(os.path.join(HERE, "golden", "golden_vectors.json")))
+
+
+def test_merkle_kat_16(ctx):
+    k = KATS["merkle_16"]
+    t = S.MerkleProofInPlace(ctx)
+    assert t.get_root() == b""  # H::default() before gen_proofs
+    t.update([bytes.fromhex(h) for h in k["leaves_hex"]])
+    proofs = t.gen_proofs([k["index"]])
+    assert t.get_root().hex() == k["root_hex"]
+    assert proofs[0].leaf.hex() == k["leaf_hex"]
+    assert [d.hex() for d in proofs[0].nodes] == k["nodes_hex"]
+    assert t.width() == 16
+
+
+def test_merkle_kat_4096(ctx):
+    k = KATS["merkle_4096"]
+    t = S.MerkleProofInPlace(ctx)
+    t.update([bytes.fromhex(k["leaf_hex"])] * k["n"])
+    proofs = t.gen_proofs(k["indices"])
+    root = t.get_root()
+    assert root.hex() == k["root_hex"]
+    assert proofs[0].nodes[0].hex() == k["proof0_node0_hex"]
+    S.verify_multi_branch(root, k["indices"], proofs)
+
+
+def test_merkle_multi_core_kat(ctx, oracle):
+    k = KATS["merkle_multi_core"]
+    leaves = [i.to_bytes(4, "big") for i in range(16)]
+    t = S.MerkleProofInPlace(ctx)
+    t.update(leaves)
+    proofs = t.gen_proofs(k["indices"])
+    root, paths = oracle.merkle(b"".join(leaves), 16, 4, k["indices"], chunks=k["cpus"])
+    assert t.get_root() == root
+    assert [p.nodes for p in proofs] == paths
+    assert [p.leaf for p in proofs] == [leaves[i] for i in k["indices"]]
+
+
+def test_golden_merkle(ctx):
+    for v in GOLD["merkle"]:
+        leaves = b"".join(O.to_bytes_le(x) for x in O.from_limbs(O.random_elements(v["n"], v["seed"])))
+        t = S.MerkleProofInPlace(ctx)
+        t.update_bytes(leaves, v["n"], 32)
+        proofs = t.gen_proofs(v["indices"])
+        assert t.get_root().hex() == v["root"]
+        assert [[d.hex() for d in p.nodes] for p in proofs] == v["paths"]
+
+
+@pytest.mark.parametrize("log_n,leaf_len", [(0, 32), (1, 32), (5, 40), (9, 256), (11, 4), (12, 33), (14, 64),
+                                            (17, 32), (20, 32)])
+def test_merkle_vs_oracle(ctx, oracle, log_n, leaf_len):
+    n = 1 << log_n
+    rng = np.random.default_rng(log_n * 1000 + leaf_len)
+    leaves = rng.integers(0, 256, n * leaf_len, dtype=np.uint8).tobytes()
+    idx = sorted(set(rng.integers(0, n, 20).tolist())) + [0, n - 1, 0]
+    t = S.MerkleProofInPlace(ctx)
+    t.update_bytes(leaves, n, leaf_len)
+    proofs = t.gen_proofs(idx)
+    root, paths = oracle.merkle(leaves, n, leaf_len, idx, chunks=8)
+    assert t.get_root() == root
+    assert [p.nodes for p in proofs] == paths
+    assert [p.leaf for p in proofs] == [leaves[i * leaf_len:(i + 1) * leaf_len] for i in idx]
+
+
+def test_merkle_errors(ctx):
+    t = S.MerkleProofInPlace(ctx)
+    with pytest.raises(S.StarkError) as e:
+        t.gen_proofs([0])  # proofs before update
+    assert e.value.code == 7
+    with pytest.raises(S.StarkError) as e:
+        t.update_bytes(b"\0" * 96, 3, 32)  # not a power of two (merkle_proof_in_place.rs:113)
+    assert e.value.code == 1
+    t.update_bytes(b"\0" * 128, 4, 32)
+    with pytest.raises(S.StarkError):
+        t.gen_proofs([4])
+
+
+def test_golden_fri(ctx, oracle):
+    for v in GOLD["fri"]:
+        n = 1 << v["log_n"]
+        w = O.root_of_unity(v["log_n"])
+        vals = oracle.best_fft(O.random_elements(n // 4, v["coeff_seed"]), w, v["log_n"], cpus=4)
+        js = ctx.prove_low_degree(vals, w, n // 4, v["exclude"]).to_json()
+        assert hashlib.sha256(js.encode()).hexdigest() == v["json_sha256"]
+
+
+@pytest.mark.parametrize("log_n,excl,deg_div", [(7, 8, 4), (12, 8, 4), (14, 0, 4), (16, 8, 8), (13, 8, 4096)])
+def test_fri_vs_oracle(ctx, oracle, log_n, excl, deg_div):
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    vals = oracle.best_fft(O.random_elements(n // deg_div, log_n), w, log_n, cpus=8)
+    want = oracle.prove_low_degree_json(vals, w, n // deg_div, excl, chunks=8)
+    got = ctx.prove_low_degree(vals, w, n // deg_div, excl).to_json()
+    assert got == want
+
+
+def test_fri_large_structure(ctx):
+    """2^20 FRI: every opened path verifies against its root (size-independent)."""
+    log_n = 20
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    coeffs = O.random_elements(n // 4, 0x5EED0000 + log_n)
+    d = ctx.alloc(n * 32)
+    try:
+        ctx.h2d(d, coeffs)
+        # zero-pad then NTT on device
+        pad = np.zeros((n - n // 4, 4), dtype=np.uint64)
+        ctx.lib.stark_memcpy_h2d(ctx.h, d + (n // 4) * 32, pad.ctypes.data, pad.nbytes)
+        ctx.ntt_dev(d, log_n, 1, w)
+        proof = ctx.prove_low_degree_dev(d, n, w, n // 4, 8).layers()
+    finally:
+        ctx.free(d)
+    assert [list(x)[0] for x in proof] == ["Middle"] * 7 + ["Last"]
+    # Last layer: n/4^7 values of a polynomial of degree < 16
+    last = [O.from_bytes_le(bytes(b)) for b in proof[-1]["Last"]["last"]]
+    assert len(last) == n // 4 ** 7
+    m = proof[0]["Middle"]
+    root2 = bytes(m["root2"])
+    for br in m["column_branches"]:
+        nodes = [bytes(x) for x in br["nodes"]]
+        cur = O.py_blake(bytes(br["leaf"]))
+        # cannot know the index from JSON alone; check path length
+        assert len(nodes) == log_n - 2
+    assert len(m["poly_branches"]) == 160
+
+
+def test_fri_errors(ctx):
+    w = O.root_of_unity(8)
+    vals = O.random_elements(256, 1)
+    with pytest.raises(S.StarkError):
+        ctx.prove_low_degree(vals[:128], w, 64, 8)  # len != order of root
+
+
+def test_multi_inv(ctx, oracle):
+    v = O.random_elements(10000, 4)
+    v[0] = 0
+    v[17] = 0
+    v[9999] = 0
+    assert np.array_equal(ctx.multi_inv(v), oracle.multi_inv(v))
+    assert np.array_equal(ctx.multi_inv(v[:1]), oracle.multi_inv(v[:1]))
+
+
+def test_eval_poly_multi(ctx, oracle):
+    poly = O.random_elements(37, 5)
+    xs = O.random_elements(5000, 6)
+    assert np.array_equal(ctx.eval_poly_at_multi(poly, xs), oracle.eval_poly_multi(poly, xs))

@@ -1,0 +1,127 @@
+"""GPU parity: NTT / iNTT through the C ABI vs the oracle (bit-exact)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import stark_amd as S
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "golden_vectors.json")))
+
+
+def test_golden_ntt(ctx):
+    for v in GOLD["ntt"]:
+        c = O.to_limbs([int(x) for x in v["coeffs"]])
+        w = int(v["root"])
+        assert O.from_limbs(ctx.best_fft(c, w, v["log_n"])) == [int(x) for x in v["forward"]]
+        assert O.from_limbs(ctx.inv_best_fft(c, w, v["log_n"])) == [int(x) for x in v["inverse"]]
+
+
+@pytest.mark.parametrize("log_n", list(range(0, 19)))
+def test_ntt_vs_oracle(ctx, oracle, log_n):
+    n = 1 << log_n
+    c = O.random_elements(n, 0x5EED0000 + log_n)
+    w = O.root_of_unity(log_n)
+    want = oracle.best_fft(c, w, log_n, cpus=8)
+    got = ctx.best_fft(c, w, log_n)
+    assert np.array_equal(got, want)
+    want_i = oracle.inv_best_fft(c, w, log_n, cpus=8)
+    got_i = ctx.inv_best_fft(c, w, log_n)
+    assert np.array_equal(got_i, want_i)
+
+
+@pytest.mark.parametrize("log_n,length", [(10, 1), (10, 77), (12, 1000), (16, 65535), (13, 0)])
+def test_ntt_zero_padding(ctx, oracle, log_n, length):
+    c = O.random_elements(max(length, 1), 11)[:length]
+    w = O.root_of_unity(log_n)
+    assert np.array_equal(ctx.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=8))
+
+
+def test_ntt_extreme_values(ctx, oracle):
+    # p-1 everywhere, zeros, ones: stresses the carry / reduction paths.
+    log_n = 12
+    n = 1 << log_n
+    c = np.zeros((n, 4), dtype=np.uint64)
+    c[: n // 3] = O.to_limbs([O.P - 1])[0]
+    c[n // 3: n // 2] = O.to_limbs([1])[0]
+    w = O.root_of_unity(log_n)
+    assert np.array_equal(ctx.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=8))
+    assert np.array_equal(ctx.inv_best_fft(c, w, log_n), oracle.inv_best_fft(c, w, log_n, cpus=8))
+
+
+def test_ntt_other_root(ctx, oracle):
+    # any primitive root of the right order, e.g. w^3 and w^-1
+    log_n = 11
+    w = pow(O.root_of_unity(log_n), 3, O.P)
+    c = O.random_elements(1 << log_n, 99)
+    assert np.array_equal(ctx.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=4))
+
+
+def test_ntt_errors(ctx):
+    w = O.root_of_unity(8)
+    c = O.random_elements(300, 1)
+    with pytest.raises(S.StarkError) as e:
+        ctx.best_fft(c, w, 8)  # len > 2^log_n (fft.rs:162 assert)
+    assert e.value.code == 1
+    with pytest.raises(S.StarkError) as e:
+        ctx.best_fft(c[:10], pow(w, 2, O.P), 8)  # root of order 128, not 256
+    assert e.value.code == 2
+
+
+@pytest.mark.parametrize("log_n", [20, 22, 24])
+def test_ntt_roundtrip_large(ctx, log_n):
+    """fwd then inv == identity at full size (size-independent property)."""
+    n = 1 << log_n
+    c = O.random_elements(n, 0x5EED0000 + log_n)
+    w = O.root_of_unity(log_n)
+    d = ctx.alloc(n * 32)
+    try:
+        ctx.h2d(d, c)
+        ctx.ntt_dev(d, log_n, 1, w, inverse=False)
+        mid = np.empty_like(c)
+        ctx.d2h(mid, d)
+        assert not np.array_equal(mid, c)
+        ctx.ntt_dev(d, log_n, 1, w, inverse=True)
+        back = np.empty_like(c)
+        ctx.d2h(back, d)
+        assert np.array_equal(back, c)
+        if log_n > 20:
+            return
+        # spot-check 2 outputs of the forward transform against the DFT definition
+        rng = np.random.default_rng(log_n)
+        ci = O.from_limbs(c)
+        for i in rng.integers(0, n, 2):
+            wi = pow(w, int(i), O.P)
+            acc, pw = 0, 1
+            for x in ci:
+                acc += x * pw
+                pw = pw * wi % O.P
+            assert O.from_limbs(mid[i])[0] == acc % O.P
+    finally:
+        ctx.free(d)
+
+
+def test_ntt_dev_batch(ctx, oracle):
+    log_n, batch = 10, 5
+    n = 1 << log_n
+    c = O.random_elements(n * batch, 3)
+    w = O.root_of_unity(log_n)
+    d = ctx.alloc(c.nbytes)
+    try:
+        ctx.h2d(d, c)
+        ctx.ntt_dev(d, log_n, batch, w)
+        got = np.empty_like(c)
+        ctx.d2h(got, d)
+    finally:
+        ctx.free(d)
+    for b in range(batch):
+        assert np.array_equal(got[b * n:(b + 1) * n], oracle.best_fft(c[b * n:(b + 1) * n], w, log_n, cpus=4))
+
+
+def test_expand_root_of_unity(ctx, oracle):
+    w = O.root_of_unity(13)
+    assert np.array_equal(ctx.expand_root_of_unity(w), oracle.expand_root_of_unity(w))
