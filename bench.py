@@ -68,8 +68,10 @@ def main():
         dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
     ctx = S.Context(local)
-    stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
+    # All kernels go to the library's own stream; torch sees it as an external
+    # stream so its HIP events bracket exactly those launches.
+    sptr = ctx.stream
+    stream = torch.cuda.ExternalStream(sptr)
 
     log_n = args.log_n
     n = 1 << log_n
@@ -77,6 +79,7 @@ def main():
     w = O.root_of_unity(log_n)
     host = synthetic(n, 0x5EED0000 + log_n + 7919 * rank)
     buf = torch.from_numpy(host.view(np.int64)).to(f"cuda:{local}")
+    torch.cuda.synchronize()
     dptr = buf.data_ptr()
 
     def step():
@@ -108,12 +111,14 @@ def main():
         w20 = O.root_of_unity(20)
         h20 = synthetic(n20, 0x5EED0000 + 20)
         b20 = torch.from_numpy(h20.view(np.int64)).to(f"cuda:{local}")
+        torch.cuda.synchronize()
 
         def pair():
             ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=False, stream=sptr)
             ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=True, stream=sptr)
         pair()
         pair_ms = timed_events(pair, stream, 10)
+        stream.synchronize()
         ok = bool(np.array_equal(b20.cpu().numpy().view(np.uint64).reshape(-1, 4), h20))
         extras["ntt_2^20_fwd_inv_ms"] = round(pair_ms, 4)
         extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
@@ -136,8 +141,9 @@ def main():
         hf = np.zeros((nf, 4), dtype=np.uint64)
         hf[: nf // 4] = coef
         bf = torch.from_numpy(hf.view(np.int64)).to(f"cuda:{local}")
-        ctx.ntt_dev(bf.data_ptr(), lf, 1, wf, stream=sptr)
         torch.cuda.synchronize()
+        ctx.ntt_dev(bf.data_ptr(), lf, 1, wf, stream=sptr)
+        stream.synchronize()
         ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
         t1 = time.perf_counter()
         proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)

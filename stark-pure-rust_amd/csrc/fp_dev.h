@@ -92,32 +92,50 @@ __device__ __forceinline__ fe fe_neg(const fe& a) {
   return fe_sub(z, a);
 }
 
-// Montgomery product a*b*2^-256 mod p.  CIOS with the "no final carry word"
-// shortcut, valid because p's top limb 0x30644e72 < 2^31 - 1: the running
-// sum t stays below 2p < 2^256 after every outer step.
+// acc(64) + carry word c += a * b: one v_mad_u64_u32 whose carry-out is
+// counted into c by v_addc_co_u32 (gfx950: ~5 + ~2 cycles per wave64).
+__device__ __forceinline__ void fe_mac(uint64_t& acc, uint32_t& c, uint32_t a, uint32_t b) {
+  uint64_t cy;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
+      "v_addc_co_u32 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cy), "+v"(c)
+      : "v"(a), "v"(b));
+}
+
+// Montgomery product a*b*2^-256 mod p, product scanning with the reduction
+// interleaved per column (FIPS order): 64 a*b + 64 m*p word products, each a
+// single mad_u64_u32 into a 96-bit column accumulator; no partial-product
+// arrays, no carry-propagation chains.  Inputs < p, output < p.
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
-  uint32_t t[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t bi = b.w[i];
-    uint64_t A = (uint64_t)a.w[0] * bi + t[0];
-    t[0] = (uint32_t)A;
-    const uint32_t m = t[0] * STARK_PINV32;
-    uint64_t C = (uint64_t)m * STARK_P0 + t[0];
-#pragma unroll
-    for (int j = 1; j < 8; j++) {
-      A = (uint64_t)a.w[j] * bi + t[j] + (A >> 32);
-      t[j] = (uint32_t)A;
-      C = (uint64_t)m * p_limb(j) + t[j] + (C >> 32);
-      t[j - 1] = (uint32_t)C;
-    }
-    t[7] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
-  }
+  uint32_t m[8];
   fe r;
+  uint64_t acc = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.w[i] = t[i];
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int j = 0; j < k; ++j) {
+      fe_mac(acc, c, a.w[j], b.w[k - j]);
+      fe_mac(acc, c, m[j], p_limb(k - j));
+    }
+    fe_mac(acc, c, a.w[k], b.w[0]);
+    m[k] = (uint32_t)acc * STARK_PINV32;
+    fe_mac(acc, c, m[k], STARK_P0);  // clears the low word
+    acc = (acc >> 32) | ((uint64_t)c << 32);
+    c = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; ++k) {
+#pragma unroll
+    for (int j = k - 7; j < 8; ++j) {
+      fe_mac(acc, c, a.w[j], b.w[k - j]);
+      fe_mac(acc, c, m[j], p_limb(k - j));
+    }
+    r.w[k - 8] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)c << 32);
+    c = 0;
+  }
+  r.w[7] = (uint32_t)acc;  // result < 2p < 2^255
   fe_reduce_once(r);
   return r;
 }
