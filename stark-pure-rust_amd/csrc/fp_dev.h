@@ -37,59 +37,103 @@ __device__ __forceinline__ uint32_t p_limb(int i) {
   }
 }
 
-// r = t - p if t >= p (t < 2p on entry).
+// p's limbs as loop-invariant VGPR operands: gfx950's VOP2/VOP3 carry chains
+// cannot take a literal or a second SGPR next to the carry (constant-bus
+// limit 1), so the modulus lives in VGPRs that the compiler hoists.
+struct PLimbs {
+  uint32_t l[8];
+};
+__device__ __forceinline__ PLimbs p_vgprs() {
+  PLimbs q;
+  q.l[0] = STARK_P0; q.l[1] = STARK_P1; q.l[2] = STARK_P2; q.l[3] = STARK_P3;
+  q.l[4] = STARK_P4; q.l[5] = STARK_P5; q.l[6] = STARK_P6; q.l[7] = STARK_P7;
+  return q;
+}
+
+// t <- t - p if t >= p (t < 2p on entry): one borrow chain + 8 selects.
 __device__ __forceinline__ void fe_reduce_once(fe& t) {
-  uint32_t d[8];
-  uint64_t borrow = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t x = (uint64_t)t.w[i] - p_limb(i) - borrow;
-    d[i] = (uint32_t)x;
-    borrow = (x >> 32) & 1;
-  }
-  const bool keep = borrow != 0;  // t < p
-#pragma unroll
-  for (int i = 0; i < 8; i++) t.w[i] = keep ? t.w[i] : d[i];
+  const PLimbs q = p_vgprs();
+  uint32_t d0, d1, d2, d3, d4, d5, d6, d7;
+  asm("v_sub_co_u32 %8, vcc, %0, %16\n\t"
+      "v_subb_co_u32 %9, vcc, %1, %17, vcc\n\t"
+      "v_subb_co_u32 %10, vcc, %2, %18, vcc\n\t"
+      "v_subb_co_u32 %11, vcc, %3, %19, vcc\n\t"
+      "v_subb_co_u32 %12, vcc, %4, %20, vcc\n\t"
+      "v_subb_co_u32 %13, vcc, %5, %21, vcc\n\t"
+      "v_subb_co_u32 %14, vcc, %6, %22, vcc\n\t"
+      "v_subb_co_u32 %15, vcc, %7, %23, vcc\n\t"
+      "v_cndmask_b32 %0, %8, %0, vcc\n\t"
+      "v_cndmask_b32 %1, %9, %1, vcc\n\t"
+      "v_cndmask_b32 %2, %10, %2, vcc\n\t"
+      "v_cndmask_b32 %3, %11, %3, vcc\n\t"
+      "v_cndmask_b32 %4, %12, %4, vcc\n\t"
+      "v_cndmask_b32 %5, %13, %5, vcc\n\t"
+      "v_cndmask_b32 %6, %14, %6, vcc\n\t"
+      "v_cndmask_b32 %7, %15, %7, vcc"
+      : "+v"(t.w[0]), "+v"(t.w[1]), "+v"(t.w[2]), "+v"(t.w[3]), "+v"(t.w[4]), "+v"(t.w[5]), "+v"(t.w[6]),
+        "+v"(t.w[7]), "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(d4), "=&v"(d5), "=&v"(d6), "=&v"(d7)
+      : "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7])
+      : "vcc");
 }
 
 __device__ __forceinline__ fe fe_add(const fe& a, const fe& b) {
-  fe r;
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c += (uint64_t)a.w[i] + b.w[i];
-    r.w[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  fe r = a;
+  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
+      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
+      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
+      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
+      "v_addc_co_u32 %7, vcc, %7, %15, vcc"
+      : "+v"(r.w[0]), "+v"(r.w[1]), "+v"(r.w[2]), "+v"(r.w[3]), "+v"(r.w[4]), "+v"(r.w[5]), "+v"(r.w[6]),
+        "+v"(r.w[7])
+      : "v"(b.w[0]), "v"(b.w[1]), "v"(b.w[2]), "v"(b.w[3]), "v"(b.w[4]), "v"(b.w[5]), "v"(b.w[6]), "v"(b.w[7])
+      : "vcc");
   fe_reduce_once(r);  // a + b < 2p < 2^255: no carry out of limb 7
   return r;
 }
 
 __device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
-  fe r;
-  uint64_t borrow = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t x = (uint64_t)a.w[i] - b.w[i] - borrow;
-    r.w[i] = (uint32_t)x;
-    borrow = (x >> 32) & 1;
-  }
-  const uint32_t mask = 0u - (uint32_t)borrow;
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c += (uint64_t)r.w[i] + (p_limb(i) & mask);
-    r.w[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  fe r = a;
+  uint64_t borrow;
+  asm("v_sub_co_u32 %0, vcc, %0, %9\n\t"
+      "v_subb_co_u32 %1, vcc, %1, %10, vcc\n\t"
+      "v_subb_co_u32 %2, vcc, %2, %11, vcc\n\t"
+      "v_subb_co_u32 %3, vcc, %3, %12, vcc\n\t"
+      "v_subb_co_u32 %4, vcc, %4, %13, vcc\n\t"
+      "v_subb_co_u32 %5, vcc, %5, %14, vcc\n\t"
+      "v_subb_co_u32 %6, vcc, %6, %15, vcc\n\t"
+      "v_subb_co_u32 %7, %8, %7, %16, vcc"
+      : "+v"(r.w[0]), "+v"(r.w[1]), "+v"(r.w[2]), "+v"(r.w[3]), "+v"(r.w[4]), "+v"(r.w[5]), "+v"(r.w[6]),
+        "+v"(r.w[7]), "=s"(borrow)
+      : "v"(b.w[0]), "v"(b.w[1]), "v"(b.w[2]), "v"(b.w[3]), "v"(b.w[4]), "v"(b.w[5]), "v"(b.w[6]), "v"(b.w[7])
+      : "vcc");
+  // r += p where the subtraction borrowed.
+  const PLimbs q = p_vgprs();
+  uint32_t e0, e1, e2, e3, e4, e5, e6, e7;
+  asm("v_add_co_u32 %8, vcc, %0, %17\n\t"
+      "v_addc_co_u32 %9, vcc, %1, %18, vcc\n\t"
+      "v_addc_co_u32 %10, vcc, %2, %19, vcc\n\t"
+      "v_addc_co_u32 %11, vcc, %3, %20, vcc\n\t"
+      "v_addc_co_u32 %12, vcc, %4, %21, vcc\n\t"
+      "v_addc_co_u32 %13, vcc, %5, %22, vcc\n\t"
+      "v_addc_co_u32 %14, vcc, %6, %23, vcc\n\t"
+      "v_addc_co_u32 %15, vcc, %7, %24, vcc\n\t"
+      "v_cndmask_b32_e64 %0, %0, %8, %16\n\t"
+      "v_cndmask_b32_e64 %1, %1, %9, %16\n\t"
+      "v_cndmask_b32_e64 %2, %2, %10, %16\n\t"
+      "v_cndmask_b32_e64 %3, %3, %11, %16\n\t"
+      "v_cndmask_b32_e64 %4, %4, %12, %16\n\t"
+      "v_cndmask_b32_e64 %5, %5, %13, %16\n\t"
+      "v_cndmask_b32_e64 %6, %6, %14, %16\n\t"
+      "v_cndmask_b32_e64 %7, %7, %15, %16"
+      : "+v"(r.w[0]), "+v"(r.w[1]), "+v"(r.w[2]), "+v"(r.w[3]), "+v"(r.w[4]), "+v"(r.w[5]), "+v"(r.w[6]),
+        "+v"(r.w[7]), "=&v"(e0), "=&v"(e1), "=&v"(e2), "=&v"(e3), "=&v"(e4), "=&v"(e5), "=&v"(e6), "=&v"(e7)
+      : "s"(borrow), "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]),
+        "v"(q.l[7])
+      : "vcc");
   return r;
-}
-
-__device__ __forceinline__ fe fe_neg(const fe& a) {
-  fe z;
-#pragma unroll
-  for (int i = 0; i < 8; i++) z.w[i] = 0;
-  return fe_sub(z, a);
 }
 
 // acc(64) + carry word c += a * b: one v_mad_u64_u32 whose carry-out is

@@ -128,7 +128,7 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
 
   const fe* cur = d_values;
   fe* next = (fe*)cols.ptr;
-  size_t m = n, deg = max_deg_plus_1;
+  size_t m = n;
   int tc = 0;  // trees[tc] holds the tree of `cur`
   HostFp w = F.from_canonical(root);
   const HostFp inv4 = F.inv(F.from_u64(4));
@@ -176,7 +176,6 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
     cur = next;
     next += q;
     m = q;
-    deg /= 4;
     w = F.pow_u64(w, 4);
     tc = 1 - tc;
   }

@@ -9,7 +9,7 @@
 #include <tuple>
 #include <vector>
 
-#include "../../include/stark_hip.h"
+#include "stark_hip.h"
 #include "fp_dev.h"
 #include "fp_host.h"
 
@@ -30,6 +30,8 @@ struct Twiddles {
   fe* d_lo = nullptr;
   fe* d_hi = nullptr;
   fe* d_small = nullptr;
+  fe* d_t16 = nullptr;   // t16[i] = w^(i n / 2^l16), l16 = min(16, log_n)
+  uint32_t l16 = 0;
   uint32_t small_off[16] = {0};
   HostFp root;      // the root these tables were built for (Montgomery)
   HostFp inv_n;     // n^-1 (Montgomery)

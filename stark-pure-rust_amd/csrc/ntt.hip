@@ -18,81 +18,191 @@
 
 namespace stark {
 
-template <int LOG_R>
-__global__ __launch_bounds__(256) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
-                                                       uint32_t log_n, uint32_t log_ns, uint32_t log_b,
-                                                       const fe* __restrict__ tw_lo, const fe* __restrict__ tw_hi,
-                                                       uint32_t kb, const fe* __restrict__ small, fe scale,
-                                                       int do_scale) {
+// Twiddle of column exponent e (< n): direct table when the pass's
+// w_{Ns R} powers fit the 2^16-entry table, else the two-level lo * hi form.
+struct ColTw {
+  const fe* t16;    // t16[i] = w^(i * n / 2^l16), i < 2^l16
+  const fe* lo;     // lo[i]  = w^i,                i < 2^kb
+  const fe* hi;     // hi[i]  = w^(i 2^kb),         i < 2^(log_n - kb)
+  uint32_t l16, kb;
+};
+
+// One Stockham pass (see the file comment), persistent: each workgroup walks
+// tiles (B adjacent columns x R points) with stride gridDim.x and prefetches
+// the next tile's 4 elements per thread into registers while it computes the
+// current one, so HBM traffic overlaps the modular arithmetic.
+// T = B*R/4 threads, each owning exactly 4 elements in every phase.
+template <int LOG_R, bool PERSIST>
+__global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
+                                                          uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
+                                                          const fe* __restrict__ small, fe scale, int do_scale,
+                                                          uint32_t log_tiles, uint32_t total_tiles) {
   constexpr uint32_t R = 1u << LOG_R;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
+  fe* sm = lds;          // R/2 small roots w_R^k
+  fe* X = lds + R / 2;   // [R][B] data image
   const uint32_t B = 1u << log_b;
-  const uint32_t E = B << LOG_R;
-  const uint32_t T = blockDim.x;
-  const size_t boff = (size_t)blockIdx.y << log_n;
-  in += boff;
-  out += boff;
-  const size_t j0 = (size_t)blockIdx.x << log_b;
-  const uint32_t log_cols = log_n - LOG_R;  // n / R columns
+  const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
+  const uint32_t tid = threadIdx.x;
+  const bool active = tid < nthr;
+  const uint32_t log_cols = log_n - LOG_R;
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
-  const uint32_t tw_shift = log_n - log_ns - LOG_R;  // exponent unit n / (Ns R)
-  const uint64_t lo_mask = ((uint64_t)1 << kb) - 1;
+  const uint32_t tile_mask = (1u << log_tiles) - 1;
 
-  // Load + column twiddle, scattered into the bit-reversed LDS image [r][b].
-  for (uint32_t e = threadIdx.x; e < E; e += T) {
-    const uint32_t b = e & (B - 1), r = e >> log_b;
-    const size_t j = j0 + b;
-    fe v = fe_load(in + j + ((size_t)r << log_cols));
-    if (log_ns != 0 && r != 0) {
-      const uint64_t ex = ((uint64_t)(j & ns_mask) * r) << tw_shift;
-      const fe t = fe_mul(tw_lo[ex & lo_mask], tw_hi[ex >> kb]);
-      v = fe_mul(v, t);
-    }
-    const uint32_t rr = __builtin_bitreverse32(r) >> (32 - LOG_R);
-    lds[(rr << log_b) + b] = v;
+  for (uint32_t k = tid; k < R / 2; k += blockDim.x) sm[k] = small[k];
+
+  // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row).
+  uint32_t eb[4], er[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t e = tid + (uint32_t)t * nthr;
+    eb[t] = e & (B - 1);
+    er[t] = e >> log_b;
   }
-  __syncthreads();
+  const uint32_t b = tid & (B - 1);
+  const uint32_t q = tid >> log_b;  // radix-4 group within the column
 
-  // R-point radix-2 DIT, in place in LDS.
-#pragma unroll 1
-  for (int s = 0; s < LOG_R; ++s) {
-    const uint32_t m = 1u << s;
-    for (uint32_t g = threadIdx.x; g < E / 2; g += T) {
-      const uint32_t b = g & (B - 1), q = g >> log_b;
-      const uint32_t jj = q & (m - 1);
-      const uint32_t pa = ((q >> s) << (s + 1)) + jj;
-      fe* xa = &lds[(pa << log_b) + b];
-      fe* xb = &lds[((pa + m) << log_b) + b];
-      fe a = *xa, c = *xb;
-      if (s != 0) c = fe_mul(c, small[jj << (LOG_R - 1 - s)]);
-      *xa = fe_add(a, c);
-      *xb = fe_sub(a, c);
+  uint32_t tile = blockIdx.x;
+  fe v[4];
+  if (active && tile < total_tiles) {
+    const fe* src = in + ((size_t)(tile >> log_tiles) << log_n) + ((size_t)(tile & tile_mask) << log_b);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = fe_load(src + eb[t] + ((size_t)er[t] << log_cols));
+  }
+
+  for (; tile < total_tiles; tile += gridDim.x) {
+    const size_t boff = (size_t)(tile >> log_tiles) << log_n;
+    const size_t j0 = (size_t)(tile & tile_mask) << log_b;
+
+    // ---- column twiddle, scatter into the bit-reversed LDS image ----
+    if (active) {
+      if (log_ns != 0) {
+        const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
+        fe tw[4];
+        if (lnr <= ct.l16) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
+            tw[t] = ct.t16[k << (ct.l16 - lnr)];
+          }
+        } else {
+          const uint32_t unit = log_n - lnr;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) << unit;
+            tw[t] = fe_mul(ct.lo[ex & (((uint64_t)1 << ct.kb) - 1)], ct.hi[ex >> ct.kb]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = fe_mul(v[t], tw[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+        X[(rr << log_b) + eb[t]] = v[t];
+      }
     }
     __syncthreads();
-  }
 
-  // Store: out[(j / Ns) Ns R + (j mod Ns) + r Ns].
-  if (((size_t)1 << log_ns) >= B) {
-    for (uint32_t e = threadIdx.x; e < E; e += T) {
-      const uint32_t b = e & (B - 1), r = e >> log_b;
-      const size_t j = j0 + b;
-      const size_t dst = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)r << log_ns);
-      fe v = lds[(r << log_b) + b];
-      if (do_scale) v = fe_mul(v, scale);
-      fe_store(out + dst, v);
+    // ---- prefetch the next tile while this one is transformed ----
+    const uint32_t nt = tile + gridDim.x;
+    if (PERSIST && active && nt < total_tiles) {
+      const fe* src = in + ((size_t)(nt >> log_tiles) << log_n) + ((size_t)(nt & tile_mask) << log_b);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = fe_load(src + eb[t] + ((size_t)er[t] << log_cols));
     }
-  } else {
-    // Ns < B: the workgroup's output is the contiguous run [j0 R, (j0 + B) R).
-    for (uint32_t o = threadIdx.x; o < E; o += T) {
-      const uint32_t q = o >> (log_ns + LOG_R);
-      const uint32_t rem = o & ((1u << (log_ns + LOG_R)) - 1);
-      const uint32_t r = rem >> log_ns;
-      const uint32_t b = (q << log_ns) + (rem & (uint32_t)ns_mask);
-      fe v = lds[(r << log_b) + b];
-      if (do_scale) v = fe_mul(v, scale);
-      fe_store(out + (j0 << LOG_R) + o, v);
+
+    // ---- R-point DIT over the bit-reversed image ----
+    int s = 0;
+    if (LOG_R & 1) {
+      if (active) {  // radix-2 stage 0: twiddles are all 1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t g = q * 2 + h;
+          fe* xa = &X[((2 * g) << log_b) + b];
+          fe* xb = &X[((2 * g + 1) << log_b) + b];
+          const fe a = *xa, c = *xb;
+          *xa = fe_add(a, c);
+          *xb = fe_sub(a, c);
+        }
+      }
+      __syncthreads();
+      s = 1;
     }
+#pragma unroll 1
+    for (; s < LOG_R; s += 2) {
+      if (active) {
+        const uint32_t m = 1u << s;
+        const uint32_t jj = q & (m - 1);
+        const uint32_t base = ((q >> s) << (s + 2)) + jj;
+        fe x0 = X[(base << log_b) + b];
+        fe x1 = X[((base + m) << log_b) + b];
+        fe x2 = X[((base + 2 * m) << log_b) + b];
+        fe x3 = X[((base + 3 * m) << log_b) + b];
+        if (s != 0) {
+          const fe ta = sm[jj << (LOG_R - 1 - s)];  // w_{2m}^jj
+          x1 = fe_mul(x1, ta);
+          x3 = fe_mul(x3, ta);
+        }
+        const fe y0 = fe_add(x0, x1), y1 = fe_sub(x0, x1);
+        fe y2 = fe_add(x2, x3), y3 = fe_sub(x2, x3);
+        const fe tc = sm[(jj + m) << (LOG_R - 2 - s)];  // w_{4m}^(jj+m)
+        if (s != 0) {
+          const fe tb = sm[jj << (LOG_R - 2 - s)];  // w_{4m}^jj
+          y2 = fe_mul(y2, tb);
+        }
+        y3 = fe_mul(y3, tc);
+        X[(base << log_b) + b] = fe_add(y0, y2);
+        X[((base + 2 * m) << log_b) + b] = fe_sub(y0, y2);
+        X[((base + m) << log_b) + b] = fe_add(y1, y3);
+        X[((base + 3 * m) << log_b) + b] = fe_sub(y1, y3);
+      }
+      __syncthreads();
+    }
+
+    // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
+    if (active) {
+      fe* dst = out + boff;
+      if (((size_t)1 << log_ns) >= B) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const size_t j = j0 + eb[t];
+          const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
+          fe val = X[(er[t] << log_b) + eb[t]];
+          if (do_scale) val = fe_mul(val, scale);
+          fe_store(dst + o, val);
+        }
+      } else {
+        // Ns < B: the tile's output is the contiguous run [j0 R, (j0 + B) R).
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t o = tid + (uint32_t)t * nthr;
+          const uint32_t qq = o >> (log_ns + LOG_R);
+          const uint32_t rem = o & ((1u << (log_ns + LOG_R)) - 1);
+          const uint32_t r = rem >> log_ns;
+          const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
+          fe val = X[(r << log_b) + bb];
+          if (do_scale) val = fe_mul(val, scale);
+          fe_store(dst + (j0 << LOG_R) + o, val);
+        }
+      }
+    }
+    if (!PERSIST) break;
+    __syncthreads();  // X is rewritten by the next tile
   }
+}
+
+// n = 2 (best_fft with log_order_of_root = 1): out = (a + b, a - b) [* 1/2].
+__global__ void ntt2_kernel(fe* d, fe scale, int do_scale) {
+  const size_t off = (size_t)blockIdx.x * 2;
+  const fe a = fe_load(d + off), c = fe_load(d + off + 1);
+  fe x = fe_add(a, c), y = fe_sub(a, c);
+  if (do_scale) {
+    x = fe_mul(x, scale);
+    y = fe_mul(y, scale);
+  }
+  fe_store(d + off, x);
+  fe_store(d + off + 1, y);
 }
 
 namespace {
@@ -103,6 +213,12 @@ struct PassPlan {
 };
 
 constexpr uint32_t kMaxLogR = 8;
+// Workgroups of a persistent pass: 256 CUs x 2 resident 256-thread groups.
+constexpr uint64_t kPersistentGrid = 256 * 2;
+#ifndef STARK_NTT_PERSISTENT
+#define STARK_NTT_PERSISTENT 0
+#endif
+constexpr bool kPersistent = STARK_NTT_PERSISTENT != 0;
 
 PassPlan plan_passes(uint32_t log_n) {
   PassPlan p;
@@ -112,28 +228,27 @@ PassPlan plan_passes(uint32_t log_n) {
   return p;
 }
 
-// Columns per workgroup (log2): >= 4 columns (128-B runs) when possible,
-// enough elements to give 256 butterflies, never more than n / R columns.
+// Columns per workgroup (log2): 1024 elements (256 threads x 4) when the
+// transform has that many columns, so every global access is a run of
+// B*32 >= 128 contiguous bytes for R <= 256.
 uint32_t choose_log_b(uint32_t log_n, uint32_t log_r) {
-  uint32_t lb = 2;
-  while (log_r + lb < 9) ++lb;
+  uint32_t lb = log_r >= 10 ? 0 : 10 - log_r;
   if (lb > log_n - log_r) lb = log_n - log_r;
   return lb;
 }
 
-typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, const fe*, const fe*, uint32_t, const fe*,
-                        fe, int);
+typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, fe, int, uint32_t,
+                        uint32_t);
 
-pass_fn pass_kernel(uint32_t log_r) {
+pass_fn pass_kernel(uint32_t log_r, bool persist) {
   switch (log_r) {
-    case 1: return ntt_pass_kernel<1>;
-    case 2: return ntt_pass_kernel<2>;
-    case 3: return ntt_pass_kernel<3>;
-    case 4: return ntt_pass_kernel<4>;
-    case 5: return ntt_pass_kernel<5>;
-    case 6: return ntt_pass_kernel<6>;
-    case 7: return ntt_pass_kernel<7>;
-    case 8: return ntt_pass_kernel<8>;
+    case 2: return persist ? ntt_pass_kernel<2, true> : ntt_pass_kernel<2, false>;
+    case 3: return persist ? ntt_pass_kernel<3, true> : ntt_pass_kernel<3, false>;
+    case 4: return persist ? ntt_pass_kernel<4, true> : ntt_pass_kernel<4, false>;
+    case 5: return persist ? ntt_pass_kernel<5, true> : ntt_pass_kernel<5, false>;
+    case 6: return persist ? ntt_pass_kernel<6, true> : ntt_pass_kernel<6, false>;
+    case 7: return persist ? ntt_pass_kernel<7, true> : ntt_pass_kernel<7, false>;
+    case 8: return persist ? ntt_pass_kernel<8, true> : ntt_pass_kernel<8, false>;
     default: return nullptr;
   }
 }
@@ -189,15 +304,29 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     }
   }
   if (h_small.empty()) h_small.push_back(to_dev(F.one()));
-  const size_t bytes = (n_lo + n_hi + h_small.size()) * sizeof(fe);
+  // t16[i] = w^(i n / 2^l16): the w_{Ns R} powers of every pass with Ns R <= 2^16.
+  tw->l16 = log_n < 16 ? log_n : 16;
+  const size_t n16 = (size_t)1 << tw->l16;
+  std::vector<fe> h_t16(n16);
+  {
+    const HostFp w16 = F.pow_u64(w, (uint64_t)1 << (log_n - tw->l16));
+    HostFp a = F.one();
+    for (size_t i = 0; i < n16; ++i) {
+      h_t16[i] = to_dev(a);
+      a = F.mul(a, w16);
+    }
+  }
+  const size_t bytes = (n_lo + n_hi + h_small.size() + n16) * sizeof(fe);
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return STARK_ERR_OOM;
   tw->d_lo = (fe*)d;
   tw->d_hi = tw->d_lo + n_lo;
   tw->d_small = tw->d_hi + n_hi;
+  tw->d_t16 = tw->d_small + h_small.size();
   STARK_HIP(ctx, hipMemcpy(tw->d_lo, h_lo.data(), n_lo * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi, h_hi.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_small, h_small.data(), h_small.size() * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_t16, h_t16.data(), n16 * sizeof(fe), hipMemcpyHostToDevice));
   *out = tw.get();
   ctx->tw.emplace(key, std::move(tw));
   return STARK_OK;
@@ -206,10 +335,15 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
                         bool inverse, hipStream_t stream) {
   if (batch == 0) return STARK_OK;
-  if (batch > 65535) return STARK_ERR_BAD_ARG;
+  if (((uint64_t)batch << log_n) > ((uint64_t)1 << 34)) return STARK_ERR_BAD_ARG;
   const size_t n = (size_t)1 << log_n;
   const fe scale = to_dev(tw.inv_n);
   if (log_n == 0) return STARK_OK;  // 1-point DFT is the identity (n^-1 = 1)
+  if (log_n == 1) {
+    hipLaunchKernelGGL(ntt2_kernel, dim3(batch), dim3(1), 0, stream, d_data, scale, inverse ? 1 : 0);
+    STARK_HIP(ctx, hipGetLastError());
+    return STARK_OK;
+  }
   const PassPlan plan = plan_passes(log_n);
   stark_status st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
   if (st != STARK_OK) return st;
@@ -224,10 +358,16 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
     fe* dst = last ? d_data : (cur == d_data ? scratch : d_data);
     const uint32_t lb = choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
-    const uint32_t threads = elems / 2 < 256 ? (elems / 2 < 64 ? 64 : elems / 2) : 256;
-    dim3 grid((unsigned)(n >> (lr + lb)), batch);
-    hipLaunchKernelGGL(pass_kernel(lr), grid, dim3(threads), elems * sizeof(fe), stream, cur, dst, log_n, log_ns,
-                       lb, tw.d_lo, tw.d_hi, tw.kb, tw.d_small + tw.small_off[lr], scale, (inverse && last) ? 1 : 0);
+    const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
+    const size_t lds = ((size_t)elems + (1u << (lr - 1))) * sizeof(fe);
+    const uint32_t log_tiles = log_n - lr - lb;
+    const uint64_t total = (uint64_t)batch << log_tiles;
+    const bool persist = kPersistent && total > kPersistentGrid;
+    const unsigned grid = (unsigned)(persist ? kPersistentGrid : total);
+    ColTw ct{tw.d_t16, tw.d_lo, tw.d_hi, tw.l16, tw.kb};
+    hipLaunchKernelGGL(pass_kernel(lr, persist), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
+                       tw.d_small + tw.small_off[lr], scale, (inverse && last) ? 1 : 0, log_tiles,
+                       (uint32_t)total);
     STARK_HIP(ctx, hipGetLastError());
     cur = dst;
     log_ns += lr;

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Builds an experimental variant of libstark_hip.so: copies csrc/ to a temp
+# dir, applies a python transform to ntt.hip, compiles.  Timing-only builds;
+# never shipped.   usage: build_variant.sh <out.so> <python-expr on s> [extra hipcc flags]
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$1; EXPR=$2; shift 2
+TMP=$(mktemp -d)
+cp "$ROOT"/stark-pure-rust_amd/csrc/* "$TMP"/
+python3 - "$TMP/ntt.hip" "$EXPR" <<'PY'
+import sys
+p, expr = sys.argv[1], sys.argv[2]
+s = open(p).read()
+s = eval(expr)
+open(p, 'w').write(s)
+PY
+for f in api ntt merkle field_ops fri; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -I"$ROOT/include" "$@" -c "$TMP/$f.hip" -o "$TMP/$f.o" &
+done
+wait
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o "$OUT" "$TMP"/*.o
+rm -rf "$TMP"
