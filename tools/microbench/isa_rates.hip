@@ -99,6 +99,75 @@ __global__ void k_pk_fma32(uint64_t* out, uint32_t s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)(a0.x + a1.x + a2.y + a3.x + a4.x + a5.x + a6.x + a7.x);
 }
 
+
+__global__ void k_addc3(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  for (int i = 0; i < ITERS; i++) {
+    asm volatile("v_addc_co_u32 %0, s[40:41], %0, 0, s[40:41]\n\tv_addc_co_u32 %1, s[42:43], %1, 0, s[42:43]\n\t"
+                 "v_addc_co_u32 %2, s[44:45], %2, 0, s[44:45]\n\tv_addc_co_u32 %3, s[46:47], %3, 0, s[46:47]\n\t"
+                 "v_addc_co_u32 %4, s[48:49], %4, 0, s[48:49]\n\tv_addc_co_u32 %5, s[50:51], %5, 0, s[50:51]\n\t"
+                 "v_addc_co_u32 %6, s[52:53], %6, 0, s[52:53]\n\tv_addc_co_u32 %7, s[54:55], %7, 0, s[54:55]"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+                 :: "s40","s41","s42","s43","s44","s45","s46","s47","s48","s49","s50","s51","s52","s53","s54","s55");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_addco3(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1;
+  for (int i = 0; i < ITERS; i++) {
+    asm volatile("v_add_co_u32 %0, s[40:41], %0, %8\n\tv_add_co_u32 %1, s[42:43], %1, %8\n\t"
+                 "v_add_co_u32 %2, s[44:45], %2, %8\n\tv_add_co_u32 %3, s[46:47], %3, %8\n\t"
+                 "v_add_co_u32 %4, s[48:49], %4, %8\n\tv_add_co_u32 %5, s[50:51], %5, %8\n\t"
+                 "v_add_co_u32 %6, s[52:53], %6, %8\n\tv_add_co_u32 %7, s[54:55], %7, %8"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(y)
+                 : "s40","s41","s42","s43","s44","s45","s46","s47","s48","s49","s50","s51","s52","s53","s54","s55");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_addc2vcc(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1;
+  for (int i = 0; i < ITERS; i++) {
+    asm volatile("v_add_co_u32 %0, vcc, %0, %8\n\tv_addc_co_u32 %1, vcc, %1, %8, vcc\n\t"
+                 "v_addc_co_u32 %2, vcc, %2, %8, vcc\n\tv_addc_co_u32 %3, vcc, %3, %8, vcc\n\t"
+                 "v_addc_co_u32 %4, vcc, %4, %8, vcc\n\tv_addc_co_u32 %5, vcc, %5, %8, vcc\n\t"
+                 "v_addc_co_u32 %6, vcc, %6, %8, vcc\n\tv_addc_co_u32 %7, vcc, %7, %8, vcc"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(y) : "vcc");
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_alignbit(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_alignbit_b32 %0, %1, %0, 29" : "+v"(a##k) : "v"(y));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_cndmask(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(a##k) : "v"(y) : "s40", "s41");
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_mad_nodep(uint64_t* out, uint32_t s) {
+  uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t x = s + threadIdx.x, y = s * 3 + 1;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0\n\tv_addc_co_u32 %3, s[40:41], %3, 0, s[40:41]" : "+v"(a##k) : "v"(x), "v"(y), "v"(x) : "s40", "s41");
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 typedef void (*kfn)(uint64_t*, uint32_t);
 static void run(const char* name, kfn k, uint64_t* buf) {
   const int blocks = 256 * 4, threads = 1024;  // 16 waves per CU = 4 per SIMD
@@ -124,5 +193,10 @@ int main() {
   run("v_fma_f64", k_fma64, buf);
   run("v_mad_u32_u24", k_mad_u32_u24, buf);
   run("v_pk_fma_f32", k_pk_fma32, buf);
+  run("v_addc VOP3 sgpr", k_addc3, buf);
+  run("v_add_co VOP3 sgpr", k_addco3, buf);
+  run("add_co+addc vcc chain", k_addc2vcc, buf);
+  run("v_alignbit_b32", k_alignbit, buf);
+  run("v_cndmask_e64", k_cndmask, buf);
   return 0;
 }
