@@ -27,8 +27,12 @@ import torch.distributed as dist  # noqa: E402
 import stark_amd as S  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-MAD64_PEAK_TOPS = 19.66        # v_mad_u64_u32: quarter rate x 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+# VALU bound of the modular product: every Montgomery product issues 128
+# v_mad_u64_u32 + 128 carry ops, all half-rate on gfx950 (4 cycles per wave64,
+# tools/microbench/isa_lat.hip): 1024 SIMDs x 2.4 GHz x 64 lanes / (256 x 4).
+MODMUL_PEAK = 1024 * 2.4e9 * 64 / (256 * 4)
 LOG_N = 24
+PROFILE = os.path.join(ROOT, "profiles", "r01_summary.json")
 
 
 def parse():
@@ -150,17 +154,38 @@ def main():
         extras["fri_prove_2^23_ms"] = round((time.perf_counter() - t1) * 1000.0, 3)
         extras["fri_layers"] = len(proof)
 
-    ntt_bytes = 64.0 * n                     # read 32 + write 32 B per element per transform
+    # Roofline of the dominant kernel, ntt_pass_kernel: one 2^24 transform is
+    # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element
+    # per transform (read 32 + write 32) x n / transform time (HIP events).
+    ntt_bytes = 64.0 * n
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     passes = (log_n + 7) // 8
-    modmuls = (n // 2) * log_n + 2 * n * (passes - 1)   # butterflies + column twiddles (2 products each)
+    traffic = None
+    try:
+        prof = json.load(open(PROFILE))
+        rec = prof["pmc_bytes_per_launch"].get("stark::ntt_pass_kernel<8, false>")
+        if rec and log_n == 24:
+            traffic = passes * rec["hbm_bytes"]   # PMC bytes of one transform (per-launch x passes)
+    except (OSError, KeyError, ValueError):
+        pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": f"ntt 2^{log_n} = {passes} x ntt_pass_kernel<8>", "ms_per_launch": round(ev_ms, 4)}
-    valu = {"bound": "valu_mad64", "modmuls_per_transform": modmuls,
-            "achieved_mad64_tops": round(modmuls * 136 / (ev_ms / 1000.0) / 1e12, 3),
-            "peak_mad64_tops": MAD64_PEAK_TOPS}
-    valu["frac"] = round(valu["achieved_mad64_tops"] / MAD64_PEAK_TOPS, 4)
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": f"ntt_pass_kernel<8> x {passes} launches per 2^{log_n} transform",
+                "ms_per_transform": round(ev_ms, 4)}
+    # modular products per transform: radix-4 steps (3 per group of 4, 1 in the
+    # first step) + column twiddles (1 per element in table passes, 2 in two-level passes)
+    lr = [log_n // passes + (1 if i < log_n % passes else 0) for i in range(passes)]
+    modmuls = 0
+    ns = 0
+    for r in lr:
+        steps = r // 2
+        modmuls += n * (steps - (0 if r % 2 else 1)) + n // 4 * (0 if r % 2 else 1)
+        if ns:
+            modmuls += n * (1 if ns + r <= 16 else 2)
+        ns += r
+    valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
+            "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
+    valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -168,7 +193,7 @@ def main():
         o = O2.Oracle()
         cores = min(16, os.cpu_count() or 1)
         threads = 1 << (cores.bit_length() - 1)
-        lc = 21
+        lc = log_n  # the same workload as the GPU step (one 2^24 transform, ~3 s on 16 threads)
         hc = synthetic(1 << lc, 1234)
         wc = O2.root_of_unity(lc)
         t2 = time.perf_counter()

@@ -1,0 +1,52 @@
+"""Summarises rocprofv3 CSV output (kernel stats + PMC passes) into a small
+JSON committed under profiles/.  FETCH_SIZE is doubled for wide coalesced
+streaming reads on gfx950 and WRITE_SIZE taken as is
+(/opt/skills/guides/MI355X_MICROARCH.md, section HBM); both are reported in
+KiB by rocprofv3 and converted to bytes here.
+
+usage: profile_summary.py <stats_dir> <fetch_dir> <write_dir> <out.json>
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def load(pattern):
+    files = glob.glob(pattern)
+    return list(csv.DictReader(open(files[0]))) if files else []
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def main():
+    stats_dir, fetch_dir, write_dir, out = sys.argv[1:5]
+    summary = {"kernels": {}, "pmc_bytes_per_launch": {}}
+    for r in load(f"{stats_dir}/*kernel_stats.csv"):
+        summary["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                                "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
+                                                "pct": float(r["Percentage"])}
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in (fetch_dir, write_dir):
+        for r in load(f"{d}/*counter_collection.csv"):
+            per[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, cs in per.items():
+        rec = {}
+        if "FETCH_SIZE" in cs:
+            v = cs["FETCH_SIZE"]
+            rec["fetch_bytes_corrected"] = 2 * 1024 * sum(v) / len(v)
+        if "WRITE_SIZE" in cs:
+            v = cs["WRITE_SIZE"]
+            rec["write_bytes"] = 1024 * sum(v) / len(v)
+        if rec:
+            rec["hbm_bytes"] = rec.get("fetch_bytes_corrected", 0) + rec.get("write_bytes", 0)
+            summary["pmc_bytes_per_launch"][k] = rec
+    json.dump(summary, open(out, "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
