@@ -1,14 +1,17 @@
 """Benchmark of the FRI-prover hot path on MI355X (BASELINE.json metric:
 "2^24-pt NTT field-elems/sec + Merkle leaves/sec; end-to-end proof wall-clock").
 
-A step is one 2^24-point forward NTT over BN254 Fr on HBM-resident synthetic
-data (BASELINE.md generator).  `value` = NTT field elements per second over all
-ranks.  The same JSON line also carries the Merkle leaves/s (2^24 32-B leaves),
-the 2^20 forward+inverse pair (config 2) and an FRI prove wall-clock.
+A step is one forward NTT over BN254 Fr on HBM-resident synthetic data
+(BASELINE.md generator) with 2^24 points per GPU.  `value` = field elements of
+the transform per second.  The N=1 line also carries the Merkle leaves/s (2^24
+32-B leaves), the 2^20 forward+inverse pair (config 2) and an FRI prove
+wall-clock.
 
-N > 1 GPUs: one process per GPU (torch.distributed.run), each rank transforms
-its own 2^24-point input (independent columns shard with no collective), so
-scaling is weak; timing is barrier-bracketed and the max over ranks is used.
+N > 1 GPUs: one process per GPU (torch.distributed.run, backend "nccl" = RCCL);
+the GPUs jointly transform ONE 2^(24+log2 N)-point vector, block-sharded, with
+the four-step algorithm whose three exchanges are RCCL all-to-alls over xGMI
+(stark_amd/distributed.py).  Per-GPU work is fixed, so scaling is weak; timing
+is barrier-bracketed and the max over ranks is used.
 """
 import argparse
 import json
@@ -68,26 +71,36 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo", init_method="env://")
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device(f"cuda:{local}"))
     ctx = S.Context(local)
-    # All kernels go to the library's own stream; torch sees it as an external
-    # stream so its HIP events bracket exactly those launches.
-    sptr = ctx.stream
-    stream = torch.cuda.ExternalStream(sptr)
+    # Every library launch and every RCCL collective goes to this stream, so
+    # the HIP events below bracket exactly the timed work.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
 
-    log_n = args.log_n
+    log_n = args.log_n                      # per-GPU shard: 2^log_n elements
     n = 1 << log_n
+    log_total = log_n + (world.bit_length() - 1)
     import oracle as O
+    w_total = O.root_of_unity(log_total)
     w = O.root_of_unity(log_n)
-    host = synthetic(n, 0x5EED0000 + log_n + 7919 * rank)
+    host = synthetic(n, 0x5EED0000 + log_total + 7919 * rank)
     buf = torch.from_numpy(host.view(np.int64)).to(f"cuda:{local}")
     torch.cuda.synchronize()
     dptr = buf.data_ptr()
+    if world > 1:
+        from stark_amd.distributed import GpuOps, four_step_ntt
+        ops = GpuOps(ctx)
+        state = {"x": buf}
 
-    def step():
-        ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr)
+        def step():
+            state["x"] = four_step_ntt(state["x"], log_total, w_total, ops)
+    else:
+        def step():
+            ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr)
 
     for _ in range(args.warmup):
         step()
@@ -101,15 +114,15 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t[0])
+    elapsed = float(t.cpu()[0])
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * n * args.steps / elapsed
 
     extras = {}
-    if not args.no_extras:
+    if not args.no_extras and world == 1:
         # config 2: 2^20 forward + inverse pair, bit-exact round trip checked
         n20 = 1 << 20
         w20 = O.root_of_unity(20)
@@ -127,6 +140,7 @@ def main():
         extras["ntt_2^20_fwd_inv_ms"] = round(pair_ms, 4)
         extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
         # inverse 2^24 throughput
+        ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr)   # warm: builds the w^-1 tables
         inv_ms = timed_events(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream, 5)
         extras["intt_2^24_elems_per_s"] = n / (inv_ms / 1000.0)
         # Merkle: 2^24 leaves of 32 B (canonical Fp, the FRI / L-tree leaves)
@@ -208,8 +222,10 @@ def main():
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32x8 (BN254 Fr)",
                 "data": "synthetic (splitmix64 uniform in [0,p), BASELINE.md)",
-                "config": {"workload": f"forward NTT 2^{log_n} BN254 Fr, natural order, HBM-resident",
-                           "global_batch": world, "seq_len": n, "parallelism": f"independent transforms x{world}"},
+                "config": {"workload": f"forward NTT 2^{log_total} BN254 Fr, natural order, HBM-resident"
+                                       + (f", four-step over {world} GPUs (RCCL all-to-all)" if world > 1 else ""),
+                           "global_batch": 1, "seq_len": n * world, "shard_per_gpu": n,
+                           "parallelism": f"four-step NTT x{world} (block shards)" if world > 1 else "single GPU"},
                 "roofline": roofline, "valu_roofline": valu, "cpu_baseline": cpu}
         line.update(extras)
         print(json.dumps(line))

@@ -151,6 +151,17 @@ stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, 
                                         size_t* n_column, size_t* column_depth, size_t* n_poly,
                                         size_t* poly_depth, size_t* n_last);
 
+/* ---- multi-GPU four-step NTT building blocks (no reference counterpart;
+ * the reference is single-process).  The exchanges are RCCL
+ * all-to-alls issued by the caller; see stark-pure-rust_amd/stark_amd/distributed.py. */
+/* dst[c][r] = src[r][c] for `batch` row-major rows x cols matrices of elements. */
+stark_status stark_transpose_dev(stark_ctx* ctx, const uint64_t* d_src, uint64_t* d_dst, size_t rows, size_t cols,
+                                 uint32_t batch, void* stream);
+/* d_data[i][j] *= root^((row_base + i) * (col_base + j)) for a rows x cols matrix;
+ * root must be a primitive 2^log_order-th root of unity. */
+stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, size_t cols, uint64_t row_base,
+                                 uint64_t col_base, const uint64_t root[4], uint32_t log_order, void* stream);
+
 /* ---- device memory helpers (for callers without their own allocator) ------ */
 stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);
 stark_status stark_dev_free(stark_ctx* ctx, void* d_ptr);

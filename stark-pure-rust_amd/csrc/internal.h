@@ -31,6 +31,8 @@ struct Twiddles {
   fe* d_hi = nullptr;
   fe* d_small = nullptr;
   fe* d_t16 = nullptr;   // t16[i] = w^(i n / 2^l16), l16 = min(16, log_n)
+  fe* d_hi_s = nullptr;  // hi[i] * n^-1   (last pass of an inverse transform)
+  fe* d_t16_s = nullptr; // t16[i] * n^-1
   uint32_t l16 = 0;
   uint32_t small_off[16] = {0};
   HostFp root;      // the root these tables were built for (Montgomery)

@@ -316,17 +316,38 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
       a = F.mul(a, w16);
     }
   }
-  const size_t bytes = (n_lo + n_hi + h_small.size() + n16) * sizeof(fe);
+  // Copies scaled by n^-1: the inverse's last pass multiplies every element by
+  // a column twiddle anyway, so folding n^-1 into it makes the scale free.
+  std::vector<fe> h_hi_s(n_hi), h_t16_s(n16);
+  {
+    HostFp a = F.one();
+    const HostFp step_hi = F.pow_u64(w, (uint64_t)1 << tw->kb);
+    for (size_t i = 0; i < n_hi; ++i) {
+      h_hi_s[i] = to_dev(F.mul(a, tw->inv_n));
+      a = F.mul(a, step_hi);
+    }
+    const HostFp w16 = F.pow_u64(w, (uint64_t)1 << (log_n - tw->l16));
+    a = F.one();
+    for (size_t i = 0; i < n16; ++i) {
+      h_t16_s[i] = to_dev(F.mul(a, tw->inv_n));
+      a = F.mul(a, w16);
+    }
+  }
+  const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 2 * n16) * sizeof(fe);
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return STARK_ERR_OOM;
   tw->d_lo = (fe*)d;
   tw->d_hi = tw->d_lo + n_lo;
   tw->d_small = tw->d_hi + n_hi;
   tw->d_t16 = tw->d_small + h_small.size();
+  tw->d_hi_s = tw->d_t16 + n16;
+  tw->d_t16_s = tw->d_hi_s + n_hi;
   STARK_HIP(ctx, hipMemcpy(tw->d_lo, h_lo.data(), n_lo * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi, h_hi.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_small, h_small.data(), h_small.size() * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_t16, h_t16.data(), n16 * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_hi_s, h_hi_s.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_t16_s, h_t16_s.data(), n16 * sizeof(fe), hipMemcpyHostToDevice));
   *out = tw.get();
   ctx->tw.emplace(key, std::move(tw));
   return STARK_OK;
@@ -364,9 +385,12 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
     const uint64_t total = (uint64_t)batch << log_tiles;
     const bool persist = kPersistent && total > kPersistentGrid;
     const unsigned grid = (unsigned)(persist ? kPersistentGrid : total);
-    ColTw ct{tw.d_t16, tw.d_lo, tw.d_hi, tw.l16, tw.kb};
+    // Inverse: n^-1 rides on the last pass's column twiddles (scaled tables)
+    // when that pass has them (log_ns > 0), else it is an explicit product.
+    const bool fold = inverse && last && log_ns > 0;
+    ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, tw.l16, tw.kb};
     hipLaunchKernelGGL(pass_kernel(lr, persist), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
-                       tw.d_small + tw.small_off[lr], scale, (inverse && last) ? 1 : 0, log_tiles,
+                       tw.d_small + tw.small_off[lr], scale, (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total);
     STARK_HIP(ctx, hipGetLastError());
     cur = dst;

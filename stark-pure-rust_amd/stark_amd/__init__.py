@@ -78,6 +78,9 @@ _SIGNATURES = {
     "stark_fri_proof_num_layers": ([_vp], ctypes.c_size_t),
     "stark_fri_proof_layer_info": ([_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), _u8p, _szp, _szp, _szp,
                                     _szp, _szp], ctypes.c_int),
+    "stark_transpose_dev": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32, _vp], ctypes.c_int),
+    "stark_twiddle2d_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _u64p,
+                             ctypes.c_uint32, _vp], ctypes.c_int),
     "stark_dev_alloc": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_dev_free": ([_vp, _vp], ctypes.c_int),
     "stark_memcpy_h2d": ([_vp, _vp, _vp, ctypes.c_size_t], ctypes.c_int),
@@ -193,6 +196,15 @@ class Context:
         r = _limbs(root)
         self.check(self.lib.stark_ntt_dev(self.h, d_ptr, log_n, batch, _p64(r), 1 if inverse else 0, stream or None),
                    "ntt_dev")
+
+    def transpose_dev(self, d_src: int, d_dst: int, rows: int, cols: int, batch: int = 1, stream: int = 0) -> None:
+        self.check(self.lib.stark_transpose_dev(self.h, d_src, d_dst, rows, cols, batch, stream or None), "transpose")
+
+    def twiddle2d_dev(self, d_ptr: int, rows: int, cols: int, row_base: int, col_base: int, root, log_order: int,
+                      stream: int = 0) -> None:
+        r = _limbs(root)
+        self.check(self.lib.stark_twiddle2d_dev(self.h, d_ptr, rows, cols, row_base, col_base, _p64(r), log_order,
+                                                stream or None), "twiddle2d")
 
     def expand_root_of_unity(self, root_of_unity) -> np.ndarray:
         """fft.rs:5-14."""

@@ -1,0 +1,104 @@
+"""Multi-GPU four-step NTT: one transform of n = G * M elements sharded over
+G ranks (one process per GPU), block distribution in and out:
+
+    rank r holds x[r M : (r+1) M]  ->  rank r holds X[r M : (r+1) M]
+
+with X[k] = sum_j x[j] w^(j k) exactly as best_fft (packages/fri/src/fft.rs:327-357).
+The reference is single-process; this module is the
+MI355X-native way to scale the hot path across the xGMI-connected GPUs of one
+node.  Derivation (j = g M + m, k = h M + q1 + G q2, t = q2 + (M/G) h):
+
+    S[m][q1] = sum_g x[g M + m] wG^(g q1)                (G-point DFTs, wG = w^M)
+    T[q1][m] = S[m][q1] w^(m q1)                          (four-step twiddle)
+    X[h M + q1 + G q2] = sum_m T[q1][m] wM^(m t)          (M-point DFTs, wM = w^G)
+
+Three all-to-alls (RCCL over xGMI with backend "nccl"; each moves (G-1)/G of
+the shard, 1/G of it per peer link) and three local transposes; all local
+arithmetic runs in libstark_hip.  `ops` abstracts the local steps so the same
+orchestration is tested on CPU with gloo (tests/test_distributed_cpu.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import P
+
+
+def _exchange(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """all_to_all_single of equal chunks; gloo needs host tensors."""
+    if dist.get_backend(group) == "gloo" and inp.is_cuda:
+        o = torch.empty_like(out, device="cpu")
+        dist.all_to_all_single(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, group=group)
+
+
+def four_step_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = False, group=None) -> torch.Tensor:
+    """Distributed forward (or inverse, inv_best_fft semantics) NTT.
+
+    x: this rank's block, shape (M, 4) int64 (canonical u64 limbs), M = n / G.
+    Returns a new (M, 4) tensor with this rank's block of the result.
+    """
+    G = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    n = 1 << log_n
+    M = n // G
+    if M * G != n or M % G != 0 or x.shape[0] != M:
+        raise ValueError(f"four_step_ntt: need M = n/G divisible by G (n=2^{log_n}, G={G}, block={x.shape[0]})")
+    log_m = M.bit_length() - 1
+    log_g = G.bit_length() - 1
+    w = root % P
+    if G == 1:
+        y = x.clone()
+        ops.ntt(y, log_n, 1, w, inverse)
+        return y
+    w_tw = pow(w, P - 2, P) if inverse else w   # the twiddle uses w^-1 for the inverse
+    c = M // G
+    # 1) all-to-all: chunk q of every block goes to rank q -> R1[g][ml] = x_g[r c + ml]
+    r1 = torch.empty_like(x)
+    _exchange(r1, x, group)
+    # 2) G-point DFTs over g for each ml
+    t1 = torch.empty_like(x)
+    ops.transpose(r1, t1, G, c)                      # (G, c) -> (c, G)
+    ops.ntt(t1, log_g, c, pow(w, M, P), inverse)     # batch c of G-point transforms, root w^M
+    # 3) twiddle w^(m q1), m = r c + ml
+    ops.twiddle2d(t1, c, G, r * c, 0, w_tw, log_n)
+    # 4) all-to-all: row q1 to rank q1 -> R2 = T[r][m], m in [0, M) in order
+    u = torch.empty_like(x)
+    ops.transpose(t1, u, c, G)                       # (c, G) -> (G, c)
+    r2 = torch.empty_like(x)
+    _exchange(r2, u, group)
+    # 5) M-point DFT over m, root w^G
+    ops.ntt(r2, log_m, 1, pow(w, G, P), inverse)
+    # 6) all-to-all: t-chunk h to rank h -> R3[q1][q2] = X[r M + q1 + G q2]
+    r3 = torch.empty_like(x)
+    _exchange(r3, r2, group)
+    # 7) natural order: out[q2 G + q1] = R3[q1][q2]
+    out = torch.empty_like(x)
+    ops.transpose(r3, out, G, c)
+    return out
+
+
+class GpuOps:
+    """Local steps on this rank's GPU through libstark_hip (kernels on the
+    torch current stream, so they order with the RCCL collectives)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def ntt(self, t: torch.Tensor, log_len: int, batch: int, root: int, inverse: bool) -> None:
+        self.ctx.ntt_dev(t.data_ptr(), log_len, batch, root, inverse=inverse, stream=self._stream())
+
+    def transpose(self, src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int) -> None:
+        self.ctx.transpose_dev(src.data_ptr(), dst.data_ptr(), rows, cols, 1, stream=self._stream())
+
+    def twiddle2d(self, t: torch.Tensor, rows: int, cols: int, row_base: int, col_base: int, root: int,
+                  log_order: int) -> None:
+        self.ctx.twiddle2d_dev(t.data_ptr(), rows, cols, row_base, col_base, root, log_order,
+                               stream=self._stream())

@@ -1,0 +1,89 @@
+"""GPU: the four-step multi-GPU NTT with libstark_hip local steps.  On the
+one-GPU test box both ranks share GPU 0 and exchange through gloo; the 8-GPU
+bench uses the same code with RCCL ("nccl")."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, log_n, inverse, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stark_amd as S
+    from stark_amd.distributed import GpuOps, four_step_ntt
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = S.Context(0)
+    n = 1 << log_n
+    M = n // world
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    x = torch.from_numpy(full[rank * M:(rank + 1) * M].copy().view(np.int64)).cuda()
+    y = four_step_ntt(x, log_n, O.root_of_unity(log_n), GpuOps(ctx), inverse=inverse)
+    torch.cuda.synchronize()
+    out_q.put((rank, y.cpu().numpy().view(np.uint64).copy()))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n,inverse", [(2, 12, False), (2, 17, True), (4, 16, False)])
+def test_four_step_ntt_gpu(world, log_n, inverse):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    got = np.concatenate([parts[r] for r in range(world)])
+    o = O.Oracle()
+    n = 1 << log_n
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    w = O.root_of_unity(log_n)
+    want = o.inv_best_fft(full, w, log_n, cpus=8) if inverse else o.best_fft(full, w, log_n, cpus=8)
+    assert np.array_equal(got, want)
+
+
+def test_transpose_and_twiddle(ctx):
+    rows, cols = 37, 70
+    a = O.random_elements(rows * cols, 3)
+    d = ctx.alloc(a.nbytes)
+    e = ctx.alloc(a.nbytes)
+    try:
+        ctx.h2d(d, a)
+        ctx.transpose_dev(d, e, rows, cols)
+        t = np.empty_like(a)
+        ctx.d2h(t, e)
+        assert np.array_equal(t.reshape(cols, rows, 4), a.reshape(rows, cols, 4).transpose(1, 0, 2))
+        w = O.root_of_unity(12)
+        ctx.twiddle2d_dev(d, rows, cols, 5, 9, w, 12)
+        g = np.empty_like(a)
+        ctx.d2h(g, d)
+        vals = O.from_limbs(a)
+        want = [v * pow(w, ((5 + i // cols) * (9 + i % cols)) % 4096, O.P) % O.P for i, v in enumerate(vals)]
+        assert O.from_limbs(g) == want
+    finally:
+        ctx.free(d)
+        ctx.free(e)
