@@ -38,12 +38,16 @@ typedef enum {
   STARK_ERR_OOM = 4,          /* device or host allocation failed */
   STARK_ERR_HIP = 5,          /* a HIP runtime call failed */
   STARK_ERR_NO_DEVICE = 6,    /* no gfx950 device / bad device ordinal */
-  STARK_ERR_STATE = 7         /* API used out of order (e.g. proofs before update) */
+  STARK_ERR_STATE = 7,        /* API used out of order (e.g. proofs before update) */
+  STARK_ERR_CHECK = 8         /* the witness does not satisfy the R1CS: a divisibility assert of
+                                 r1cs-stark/src/utils.rs:379-418 (D1-D3) or :477-524 (B2, B3) */
 } stark_status;
 
 typedef struct stark_ctx stark_ctx;
 typedef struct stark_merkle_tree stark_merkle_tree;
 typedef struct stark_fri_proof stark_fri_proof;
+typedef struct stark_r1cs_proof stark_r1cs_proof;
+typedef struct stark_r1cs_trace stark_r1cs_trace;
 
 /* ---- context ------------------------------------------------------------ */
 /* Replaces commitment::multicore::Worker::new (packages/commitment/src/multicore.rs:43-45):
@@ -150,6 +154,44 @@ size_t stark_fri_proof_num_layers(const stark_fri_proof* proof);
 stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, int* is_last, uint8_t root2[32],
                                         size_t* n_column, size_t* column_depth, size_t* n_poly,
                                         size_t* poly_depth, size_t* n_last);
+
+/* ---- R1CS STARK prover (packages/r1cs-stark) -------------------------------- */
+/* mk_r1cs_proof<Fp, BlakeDigest>(witness_trace, computational_trace, public_wires,
+ * public_first_indices, permuted_indices, coefficients, flag0, flag1, flag2,
+ * n_constraints, n_wires) -> StarkProof (prove.rs:14-378), resident on the GPU.
+ * Step vectors have original_steps elements (canonical u64[4] each);
+ * public_first_indices holds n_public_first (wire k, trace position w) pairs.
+ * Returns STARK_ERR_CHECK where the reference's D/B asserts would panic. */
+stark_status stark_mk_r1cs_proof(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
+                                 size_t original_steps, const uint64_t* public_wires, size_t n_public,
+                                 const size_t* public_first_indices, size_t n_public_first,
+                                 const size_t* permuted_indices, const uint64_t* coefficients,
+                                 const uint64_t* flag0, const uint64_t* flag1, const uint64_t* flag2,
+                                 size_t n_constraints, size_t n_wires, stark_r1cs_proof** out);
+/* serde_json::to_string(&StarkProof<BlakeDigest>) (utils.rs:122-130, run.rs:549). */
+stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, size_t cap, size_t* len);
+stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_root[32], uint8_t l_root[32],
+                                    uint8_t a_root[32]);
+void stark_r1cs_proof_free(stark_r1cs_proof* proof);
+
+/* R1CS front end (host): read_r1cs (circom2bellman_core/src/reader.rs:4-89) +
+ * read_witness (r1cs-stark/src/reader.rs:7-42) + the trace construction of
+ * prove_with_witness (run.rs:310-437: calc_coefficients_and_witness :109-281,
+ * calc_flags :283-308, permuted indices :388-401, public_first_indices :411-419).
+ * STARK_ERR_BAD_ARG on a malformed file, a prime other than BN254 r
+ * (run.rs:344-350) or witness[0] != 1 (run.rs:358). */
+stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns, size_t wtns_len,
+                                    stark_r1cs_trace** out);
+stark_status stark_r1cs_trace_dims(const stark_r1cs_trace* trace, size_t* original_steps, size_t* n_public,
+                                   size_t* n_public_first, size_t* n_constraints, size_t* n_wires);
+/* Copies the mk_r1cs_proof arguments out (any pointer may be NULL). */
+stark_status stark_r1cs_trace_export(const stark_r1cs_trace* trace, uint64_t* witness_trace,
+                                     uint64_t* computational_trace, uint64_t* coefficients, uint64_t* flag0,
+                                     uint64_t* flag1, uint64_t* flag2, size_t* permuted_indices,
+                                     uint64_t* public_wires, size_t* public_first_indices);
+void stark_r1cs_trace_free(stark_r1cs_trace* trace);
+/* prove_with_witness (run.rs:310-452) = stark_mk_r1cs_proof on a built trace. */
+stark_status stark_prove_r1cs_trace(stark_ctx* ctx, const stark_r1cs_trace* trace, stark_r1cs_proof** out);
 
 /* ---- multi-GPU four-step NTT building blocks (no reference counterpart;
  * the reference is single-process).  The exchanges are RCCL

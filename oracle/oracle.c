@@ -28,8 +28,9 @@
 #include <stdio.h>
 #include <pthread.h>
 
+#include "oracle_internal.h"
+
 typedef unsigned __int128 u128;
-typedef struct { uint64_t v[4]; } fp; /* Montgomery form, R = 2^256 */
 
 /* BN254 scalar field r (ff_utils/src/fp.rs:9), little-endian u64 limbs. */
 static const uint64_t P[4] = {0x43e1f593f0000001ull, 0x2833e84879b97091ull,
@@ -89,7 +90,7 @@ fp fp_mul(fp a, fp b) {
 int fp_eq(fp a, fp b) { return memcmp(a.v, b.v, 32) == 0; }
 int fp_is_zero(fp a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
 
-static void init(void) {
+void or_init(void) {
   if (g_init) return;
   uint64_t x = 1; /* Newton iteration for p^{-1} mod 2^64 */
   for (int i = 0; i < 7; i++) x *= 2 - P[0] * x;
@@ -257,50 +258,50 @@ void or_inv_best_fft_mont(fp* values, size_t len, fp root, uint32_t log_n, uint3
 /* Canonical-limb entry points used by the Python tests / bench.       */
 /* Elements cross this boundary as canonical LE u64[4] (= to_bytes_le).*/
 /* ------------------------------------------------------------------ */
-static fp* load(const uint64_t* c, size_t len, size_t cap) {
+fp* or_load(const uint64_t* c, size_t len, size_t cap) {
   fp* v = (fp*)malloc(sizeof(fp) * (cap ? cap : 1));
   for (size_t i = 0; i < len; i++) v[i] = fp_from_canon(c + 4 * i);
   return v;
 }
-static void store(const fp* v, uint64_t* c, size_t len) {
+void or_store(const fp* v, uint64_t* c, size_t len) {
   for (size_t i = 0; i < len; i++) fp_to_canon(v[i], c + 4 * i);
 }
 
 /* out must hold 4*2^log_n u64.  Returns 0 on success, -1 on bad length. */
 int oracle_best_fft(const uint64_t* in, size_t len, const uint64_t root[4], uint32_t log_n,
                     uint32_t cpus, uint64_t* out) {
-  init();
+  or_init();
   size_t n = (size_t)1 << log_n;
   if (len > n) return -1;
-  fp* v = load(in, len, n);
+  fp* v = or_load(in, len, n);
   or_best_fft_mont(v, len, fp_from_canon(root), log_n, cpus);
-  store(v, out, n); free(v);
+  or_store(v, out, n); free(v);
   return 0;
 }
 int oracle_inv_best_fft(const uint64_t* in, size_t len, const uint64_t root[4], uint32_t log_n,
                         uint32_t cpus, uint64_t* out) {
-  init();
+  or_init();
   size_t n = (size_t)1 << log_n;
   if (len > n) return -1;
-  fp* v = load(in, len, n);
+  fp* v = or_load(in, len, n);
   or_inv_best_fft_mont(v, len, fp_from_canon(root), log_n, cpus);
-  store(v, out, n); free(v);
+  or_store(v, out, n); free(v);
   return 0;
 }
 /* Returns the number of powers; writes min(count, cap) of them. */
 size_t oracle_expand_root_of_unity(const uint64_t root[4], uint64_t* out, size_t cap) {
-  init();
+  or_init();
   size_t cnt = or_expand_root_of_unity(fp_from_canon(root), NULL, 0);
   if (out) {
     fp* v = (fp*)malloc(sizeof(fp) * cnt);
     or_expand_root_of_unity(fp_from_canon(root), v, cnt);
-    store(v, out, cnt < cap ? cnt : cap); free(v);
+    or_store(v, out, cnt < cap ? cnt : cap); free(v);
   }
   return cnt;
 }
 /* 7^((p-1)/2^log_n): the NTT root the prover builds (r1cs-stark/src/prove.rs:71-82). */
 void oracle_root_of_unity(uint32_t log_n, uint64_t out[4]) {
-  init();
+  or_init();
   uint64_t e[4]; memcpy(e, P, 32); e[0] -= 1; /* p - 1 */
   for (uint32_t i = 0; i < log_n; i++) { /* shift right by log_n */
     e[0] = (e[0] >> 1) | (e[1] << 63); e[1] = (e[1] >> 1) | (e[2] << 63);
@@ -310,17 +311,17 @@ void oracle_root_of_unity(uint32_t log_n, uint64_t out[4]) {
   fp_to_canon(g, out);
 }
 void oracle_fp_mul(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]) {
-  init(); fp_to_canon(fp_mul(fp_from_canon(a), fp_from_canon(b)), out);
+  or_init(); fp_to_canon(fp_mul(fp_from_canon(a), fp_from_canon(b)), out);
 }
 void oracle_fp_inv(const uint64_t a[4], uint64_t out[4]) {
-  init(); fp_to_canon(fp_inv(fp_from_canon(a)), out);
+  or_init(); fp_to_canon(fp_inv(fp_from_canon(a)), out);
 }
 void oracle_fp_pow(const uint64_t a[4], uint64_t e, uint64_t out[4]) {
-  init(); fp_to_canon(fp_pow(fp_from_canon(a), e), out);
+  or_init(); fp_to_canon(fp_pow(fp_from_canon(a), e), out);
 }
 /* from_bytes_le (ff_utils/src/fp.rs:74-76): LE integer of up to 32 bytes mod p. */
 void oracle_from_bytes_le(const uint8_t* b, size_t len, uint64_t out[4]) {
-  init();
+  or_init();
   uint64_t c[4] = {0, 0, 0, 0};
   for (size_t i = 0; i < len && i < 32; i++) c[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
   fp_to_canon(fp_from_canon(c), out);
@@ -344,9 +345,9 @@ void or_multi_inv(const fp* values, fp* outputs, size_t n) {
   free(partials);
 }
 void oracle_multi_inv(const uint64_t* in, size_t n, uint64_t* out) {
-  init();
-  fp* v = load(in, n, n); fp* o = (fp*)malloc(sizeof(fp) * (n ? n : 1));
-  or_multi_inv(v, o, n); store(o, out, n); free(v); free(o);
+  or_init();
+  fp* v = or_load(in, n, n); fp* o = (fp*)malloc(sizeof(fp) * (n ? n : 1));
+  or_multi_inv(v, o, n); or_store(o, out, n); free(v); free(o);
 }
 
 /* eval_poly_at, poly_utils.rs:93-102 (Horner-free power accumulation). */
@@ -357,8 +358,8 @@ fp or_eval_poly_at(const fp* poly, size_t deg1, fp x) {
 }
 void oracle_eval_poly_multi(const uint64_t* poly, size_t deg1, const uint64_t* xs, size_t n,
                             uint64_t* out) {
-  init();
-  fp* p = load(poly, deg1, deg1);
+  or_init();
+  fp* p = or_load(poly, deg1, deg1);
   for (size_t i = 0; i < n; i++) fp_to_canon(or_eval_poly_at(p, deg1, fp_from_canon(xs + 4 * i)), out + 4 * i);
   free(p);
 }
@@ -575,19 +576,18 @@ int oracle_merkle_proofs(const uint8_t* leaves, size_t n, size_t leaf_len, const
 /* compact encoding of Vec<FriProof<BlakeDigest>> (fri.rs:16-26,        */
 /* commitment/src/merkle_tree.rs:14-18, blake.rs:8).                    */
 /* ------------------------------------------------------------------ */
-typedef struct { char* s; size_t len, cap; } sbuf;
-static void sb_put(sbuf* b, const char* s, size_t n) {
+void sb_put(sbuf* b, const char* s, size_t n) {
   if (b->len + n + 1 > b->cap) { b->cap = (b->len + n + 1) * 2; b->s = (char*)realloc(b->s, b->cap); }
   memcpy(b->s + b->len, s, n); b->len += n; b->s[b->len] = 0;
 }
-static void sb_str(sbuf* b, const char* s) { sb_put(b, s, strlen(s)); }
-static void sb_bytes(sbuf* b, const uint8_t* p, size_t n) {
+void sb_str(sbuf* b, const char* s) { sb_put(b, s, strlen(s)); }
+void sb_bytes(sbuf* b, const uint8_t* p, size_t n) {
   char tmp[8];
   sb_str(b, "[");
   for (size_t i = 0; i < n; i++) { int k = snprintf(tmp, sizeof tmp, i ? ",%u" : "%u", p[i]); sb_put(b, tmp, (size_t)k); }
   sb_str(b, "]");
 }
-static void sb_proofs(sbuf* b, const uint8_t* leaves, size_t leaf_len, const size_t* idx, size_t k,
+void sb_proofs(sbuf* b, const uint8_t* leaves, size_t leaf_len, const size_t* idx, size_t k,
                       const uint8_t* nodes, size_t logn) {
   sb_str(b, "[");
   for (size_t i = 0; i < k; i++) {
@@ -600,7 +600,7 @@ static void sb_proofs(sbuf* b, const uint8_t* leaves, size_t leaf_len, const siz
   sb_str(b, "]");
 }
 
-static void fri_rec(sbuf* b, int first, fp* values, size_t nvals, fp root, size_t maxdeg,
+void fri_rec(sbuf* b, int first, fp* values, size_t nvals, fp root, size_t maxdeg,
                     uint32_t excl, size_t chunks) {
   /* xs = expand_root_of_unity(root) (fri.rs:84) */
   size_t nxs = or_expand_root_of_unity(root, NULL, 0);
@@ -662,8 +662,8 @@ static void fri_rec(sbuf* b, int first, fp* values, size_t nvals, fp root, size_
 /* Returns a malloc'd NUL-terminated JSON string (free with oracle_free). */
 char* oracle_prove_low_degree_json(const uint64_t* values, size_t n, const uint64_t root[4],
                                    size_t max_deg_plus_1, uint32_t exclude, size_t chunks) {
-  init();
-  fp* v = load(values, n, n);
+  or_init();
+  fp* v = or_load(values, n, n);
   sbuf b = {0, 0, 0};
   sb_str(&b, "[");
   fri_rec(&b, 1, v, n, fp_from_canon(root), max_deg_plus_1, exclude, chunks);

@@ -81,6 +81,7 @@ const char* stark_status_str(stark_status s) {
     case STARK_ERR_HIP: return "HIP runtime error";
     case STARK_ERR_NO_DEVICE: return "no gfx950 device";
     case STARK_ERR_STATE: return "bad call order";
+    case STARK_ERR_CHECK: return "constraint check failed";
   }
   return "unknown";
 }

@@ -190,7 +190,7 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
   return STARK_OK;
 }
 
-static void json_bytes(std::string& o, const uint8_t* p, size_t n) {
+void json_bytes(std::string& o, const uint8_t* p, size_t n) {
   o.push_back('[');
   char tmp[8];
   for (size_t i = 0; i < n; ++i) {
@@ -200,13 +200,14 @@ static void json_bytes(std::string& o, const uint8_t* p, size_t n) {
   o.push_back(']');
 }
 
-static void json_branches(std::string& o, const std::vector<uint8_t>& leaves, const std::vector<uint8_t>& nodes,
-                          size_t k, size_t depth) {
+// serde_json of Vec<Proof<Vec<u8>, BlakeDigest>> (commitment/src/merkle_tree.rs:14-18).
+void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
+                   const std::vector<uint8_t>& nodes, size_t k, size_t depth) {
   o.push_back('[');
   for (size_t i = 0; i < k; ++i) {
     if (i) o.push_back(',');
     o += "{\"leaf\":";
-    json_bytes(o, leaves.data() + 32 * i, 32);
+    json_bytes(o, leaves.data() + leaf_len * i, leaf_len);
     o += ",\"nodes\":[";
     for (size_t d = 0; d < depth; ++d) {
       if (d) o.push_back(',');
@@ -271,9 +272,9 @@ stark_status stark_fri_proof_json(const stark_fri_proof* proof, char* buf, size_
       o += "{\"Middle\":{\"root2\":";
       json_bytes(o, L.root2, 32);
       o += ",\"column_branches\":";
-      json_branches(o, L.col_leaves, L.col_nodes, L.col_idx.size(), L.col_depth);
+      json_branches(o, L.col_leaves, 32, L.col_nodes, L.col_idx.size(), L.col_depth);
       o += ",\"poly_branches\":";
-      json_branches(o, L.poly_leaves, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
+      json_branches(o, L.poly_leaves, 32, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
       o += "}}";
     }
   }

@@ -1,0 +1,762 @@
+// mk_r1cs_proof (packages/r1cs-stark/src/prove.rs:14-378) resident on one
+// gfx950 GPU.
+//
+// Everything of size `steps` or `precision` lives in HBM from upload to
+// proof; the host runs only the transcript (a_root -> r, m_root -> k,
+// l_root -> positions, the FRI layer roots) and serialises the proof.
+//
+//   upload 6 step columns + permuted indices
+//   index/accumulator kernel      IDX, PIDX, 40-B accumulator leaves
+//   acc Merkle tree               -> a_root -> r (host, utils.rs:272-290)
+//   batched iNTT(steps, g1) x 8 -> zero-pad -> batched NTT(precision, g2) x 8
+//   A column: a_vals kernel, two product scans, multi_inv, iNTT/NTT
+//   zb kernel + multi_inv         inverse Zb2 / Zb3 (0 -> 0)
+//   constraint kernel             Q1..Q3 -> D1..D3, B2, B3 (with the
+//                                 reference's divisibility asserts) written as
+//                                 the 256-B main-tree rows P|A|S|D1|D2|D3|B2|B3
+//   main Merkle tree (256-B leaves) -> m_root -> k (host, prove.rs:274-283)
+//   linear-combination kernel     L, then its Merkle tree -> l_root
+//   proof gathers + prove_low_degree on the resident L.
+//
+// Values are canonical in HBM; constants are Montgomery images so that
+// fe_mul(data, const) is the canonical product (see fp_dev.h).
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "blake2s.h"
+
+namespace stark {
+stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                          hipStream_t stream);
+stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
+stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
+                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream);
+stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
+void json_bytes(std::string& o, const uint8_t* p, size_t n);
+void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
+                   const std::vector<uint8_t>& nodes, size_t k, size_t depth);
+}  // namespace stark
+
+struct stark_r1cs_proof {
+  uint8_t m_root[32], l_root[32], a_root[32];
+  std::string json;
+};
+
+namespace stark {
+
+static inline fe fe_zero_host() {
+  fe r;
+  for (int i = 0; i < 8; ++i) r.w[i] = 0;
+  return r;
+}
+
+constexpr int kExtensionFactor = 8;     // utils.rs:135
+constexpr int kLogExtensionFactor = 3;  // utils.rs:134
+constexpr int kSpotChecks = 80;         // utils.rs:136
+constexpr uint32_t kScanBlock = 1024;   // elements per workgroup in the product scan
+
+// Montgomery image of R (montmul(x, r2) = Montgomery image of x) and of 1.
+struct Mont {
+  fe r2, one, unit;  // unit = canonical 1 (montmul(x_m, unit) = canonical x)
+};
+
+static Mont mont() {
+  const FieldHost& F = FieldHost::get();
+  Mont m;
+  HostFp one = F.one();
+  m.r2 = to_dev(F.from_canonical(one.v));
+  m.one = to_dev(one);
+  m.unit = fe_zero_host();
+  m.unit.w[0] = 1;
+  return m;
+}
+
+__device__ __forceinline__ fe fe_from_u64(uint64_t v) {
+  fe r = fe_zero();
+  r.w[0] = (uint32_t)v;
+  r.w[1] = (uint32_t)(v >> 32);
+  return r;
+}
+
+// Montgomery image of g^i from the two-level tables of g.
+__device__ __forceinline__ fe pow_tab(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint64_t i) {
+  return fe_mul(lo[i & (((uint64_t)1 << kb) - 1)], hi[i >> kb]);
+}
+
+// IDX / PIDX step columns (prove.rs:160-167 with the identity tail of
+// prove.rs:55-56) and the accumulator leaves u64 LE index || to_bytes_le(w)
+// (utils.rs:254-263).
+__global__ void r1cs_index_kernel(const uint64_t* __restrict__ perm, uint64_t os, uint64_t steps,
+                                  const fe* __restrict__ w, fe* __restrict__ idx, fe* __restrict__ pidx,
+                                  uint64_t* __restrict__ acc_leaves) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= steps) return;
+  const uint64_t p = i < os ? perm[i] : i;
+  fe_store(idx + i, fe_from_u64(i));
+  fe_store(pidx + i, fe_from_u64(p));
+  const fe x = fe_load(w + i);
+  uint64_t* leaf = acc_leaves + 5 * i;
+  leaf[0] = p;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) leaf[1 + k] = (uint64_t)x.w[2 * k] | ((uint64_t)x.w[2 * k + 1] << 32);
+}
+
+// dst[c][i] = i < steps ? src[c][i] : 0 (best_fft's zero padding, fft.rs:327-357).
+__global__ void r1cs_pad_kernel(const fe* __restrict__ src, fe* __restrict__ dst, uint32_t log_steps,
+                                uint32_t log_prec, uint64_t total) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const uint64_t c = g >> log_prec, i = g & (((uint64_t)1 << log_prec) - 1);
+  fe v = fe_zero();
+  if ((i >> log_steps) == 0) v = fe_load(src + (c << log_steps) + i);
+  fe_store(dst + g, v);
+}
+
+// val_nmr / val_dnm of calc_a_mini_evaluations (utils.rs:317-318), written as
+// Montgomery images for the product scans.
+__global__ void r1cs_a_vals_kernel(const fe* __restrict__ ext_idx, const fe* __restrict__ ext_pidx,
+                                   const fe* __restrict__ w, uint64_t steps, fe r0, fe r1_m, fe r2_m, fe mr2,
+                                   fe* __restrict__ nmr_m, fe* __restrict__ dnm_m) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= steps) return;
+  const fe rw = fe_mul(fe_load(w + j), r2_m);
+  const fe vn = fe_add(fe_add(r0, fe_mul(fe_load(ext_idx + j * kExtensionFactor), r1_m)), rw);
+  const fe vd = fe_add(fe_add(r0, fe_mul(fe_load(ext_pidx + j * kExtensionFactor), r1_m)), rw);
+  fe_store(nmr_m + j, fe_mul(vn, mr2));
+  fe_store(dnm_m + j, fe_mul(vd, mr2));
+}
+
+// Inclusive product scan, phase 1: each workgroup scans kScanBlock Montgomery
+// values in place (4 per thread, then a 256-entry scan of the thread
+// products in LDS) and writes the block product to tot[blockIdx].
+__global__ __launch_bounds__(256) void scan_block_kernel(fe* __restrict__ v, uint64_t n, fe* __restrict__ tot,
+                                                         fe one_m) {
+  __shared__ fe part[256];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + 4 * threadIdx.x;
+  fe x[4];
+  fe acc = one_m;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[k] = base + k < n ? fe_load(v + base + k) : one_m;
+    acc = fe_mul(acc, x[k]);
+    x[k] = acc;
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  // Hillis-Steele over the 256 thread products.
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    fe t = part[threadIdx.x];
+    if (threadIdx.x >= off) t = fe_mul(part[threadIdx.x - off], t);
+    __syncthreads();
+    part[threadIdx.x] = t;
+    __syncthreads();
+  }
+  const fe pre = threadIdx.x ? part[threadIdx.x - 1] : one_m;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + k < n) fe_store(v + base + k, threadIdx.x ? fe_mul(pre, x[k]) : x[k]);
+  if (threadIdx.x == 255) tot[blockIdx.x] = part[255];
+}
+
+// Phase 2: exclusive scan of the block products (one workgroup; each thread
+// owns a contiguous run).
+__global__ __launch_bounds__(256) void scan_tot_kernel(fe* __restrict__ tot, uint32_t nb, fe one_m) {
+  __shared__ fe part[256];
+  const uint32_t per = (nb + 255) / 256;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+  fe acc = one_m;
+  for (uint32_t i = lo; i < hi; ++i) acc = fe_mul(acc, tot[i]);
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fe run = one_m;
+    for (int t = 0; t < 256; ++t) {
+      const fe p = part[t];
+      part[t] = run;
+      run = fe_mul(run, p);
+    }
+  }
+  __syncthreads();
+  acc = part[threadIdx.x];
+  for (uint32_t i = lo; i < hi; ++i) {
+    const fe t = tot[i];
+    tot[i] = acc;
+    acc = fe_mul(acc, t);
+  }
+}
+
+// Phase 3: block b (> 0) times the product of blocks before it; also emits
+// the canonical value into `canon` when given.
+__global__ void scan_apply_kernel(fe* __restrict__ v, uint64_t n, const fe* __restrict__ tot, fe unit,
+                                  fe* __restrict__ canon) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x = fe_load(v + i);
+  const uint64_t b = i / kScanBlock;
+  if (b) x = fe_mul(x, tot[b]);
+  fe_store(v + i, x);
+  if (canon) fe_store(canon + i, fe_mul(x, unit));
+}
+
+// a_mini[j] = acc_nmr[j] * inv(acc_dnm[j]) (utils.rs:331-336); nmr Montgomery, inv canonical.
+__global__ void r1cs_a_mini_kernel(const fe* __restrict__ nmr_m, const fe* __restrict__ inv_dnm, uint64_t steps,
+                                   fe* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= steps) return;
+  fe_store(out + j, fe_mul(fe_load(nmr_m + j), fe_load(inv_dnm + j)));
+}
+
+// Zb2(x) = prod_k (x - x_k) (utils.rs:438-455) and Zb3(x) = x - x_last
+// (utils.rs:466-474), canonical, for the batch inverse.
+__global__ void r1cs_zb_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint64_t prec,
+                               const fe* __restrict__ xpub_m, uint32_t npub, fe xlast_m, fe unit, fe one_m,
+                               fe* __restrict__ zb2, fe* __restrict__ zb3) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= prec) return;
+  const fe x_m = pow_tab(lo, hi, kb, i);
+  fe acc = one_m;
+  for (uint32_t k = 0; k < npub; ++k) acc = fe_mul(acc, fe_sub(x_m, xpub_m[k]));
+  fe_store(zb2 + i, fe_mul(acc, unit));
+  fe_store(zb3 + i, fe_mul(fe_sub(x_m, xlast_m), unit));
+}
+
+struct ConstraintArgs {
+  const fe* cols;        // K F0 F1 F2 S P IDX PIDX A, precision each
+  const fe* inv_zb;      // inv Zb2 (precision) then inv Zb3 (precision)
+  const fe* interp2;     // canonical coefficients, low degree first
+  const fe* interp3;
+  const fe* lo;          // g2 tables
+  const fe* hi;
+  fe* rows;              // precision x 8 elements
+  int* err;
+  uint64_t prec;
+  uint64_t shift1, shift2;  // original_steps/3*skips, original_steps/3*2*skips (mod precision)
+  uint32_t log_prec, kb, n2, n3;
+  fe r0, r1_m, r2_m, mr2;
+  fe invz_m[8];          // Montgomery inv(w8^t - 1), 0 for t = 0 (multi_inv of Z, prove.rs:203)
+};
+
+// Q1/Q2/Q3 (utils.rs:181-248, 344-376) -> D1..D3 (utils.rs:379-418), I2/I3
+// evaluations (prove.rs:216-220), B2/B3 (utils.rs:477-524); one main-tree row
+// (prove.rs:235-258) per thread.
+__global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.prec) return;
+  const uint64_t n = a.prec, mask = n - 1;
+  const fe* K = a.cols;
+  const fe* F0 = K + n;
+  const fe* F1 = F0 + n;
+  const fe* F2 = F1 + n;
+  const fe* S = F2 + n;
+  const fe* Pc = S + n;
+  const fe* IDX = Pc + n;
+  const fe* PIDX = IDX + n;
+  const fe* A = PIDX + n;
+  const uint64_t prev = (i + n - kExtensionFactor) & mask;
+  const fe p = fe_load(Pc + i), s = fe_load(S + i), av = fe_load(A + i);
+  const fe p_prev = fe_load(Pc + prev), a_prev = fe_load(A + prev);
+  const fe p2 = fe_load(Pc + ((i + a.shift1) & mask)), p3 = fe_load(Pc + ((i + a.shift2) & mask));
+  // Data x data products: one operand to Montgomery form first.
+  const fe s_m = fe_mul(s, a.mr2);
+  const fe q1 = fe_mul(fe_mul(fe_load(F0 + i), a.mr2),
+                       fe_sub(fe_sub(p, fe_mul(fe_mul(fe_load(F1 + i), a.mr2), p_prev)), fe_mul(fe_load(K + i), s_m)));
+  const fe q2 = fe_mul(fe_mul(fe_load(F2 + i), a.mr2), fe_sub(p3, fe_mul(fe_mul(p, a.mr2), p2)));
+  const fe rs = fe_mul(s, a.r2_m);
+  const fe nmr = fe_add(fe_add(a.r0, fe_mul(fe_load(IDX + i), a.r1_m)), rs);
+  const fe dnm = fe_add(fe_add(a.r0, fe_mul(fe_load(PIDX + i), a.r1_m)), rs);
+  const fe q3 = fe_sub(fe_mul(fe_mul(av, a.mr2), dnm), fe_mul(fe_mul(a_prev, a.mr2), nmr));
+  const uint32_t t = (uint32_t)(i & 7);
+  fe iz = a.invz_m[0];
+#pragma unroll
+  for (uint32_t k = 1; k < 8; ++k)
+    if (t == k) iz = a.invz_m[k];
+  if (t == 0 && !(fe_is_zero(q1) && fe_is_zero(q2) && fe_is_zero(q3))) atomicOr(a.err, 1);
+  const fe d1 = fe_mul(q1, iz), d2 = fe_mul(q2, iz), d3 = fe_mul(q3, iz);
+  // I2 / I3 at x = g2^i (Horner; the interpolants are canonical).
+  const fe x_m = pow_tab(a.lo, a.hi, a.kb, i);
+  fe i2 = fe_zero();
+  for (uint32_t k = a.n2; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
+  fe i3 = fe_zero();
+  for (uint32_t k = a.n3; k-- > 0;) i3 = fe_add(fe_mul(i3, x_m), a.interp3[k]);
+  const fe izb2 = fe_load(a.inv_zb + i), izb3 = fe_load(a.inv_zb + n + i);
+  const fe e2 = fe_sub(s, i2), e3 = fe_sub(av, i3);
+  if (fe_is_zero(izb2) && !fe_is_zero(e2)) atomicOr(a.err, 2);
+  if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
+  const fe b2 = fe_mul(fe_mul(e2, a.mr2), izb2), b3 = fe_mul(fe_mul(e3, a.mr2), izb3);
+  fe* row = a.rows + 8 * i;
+  fe_store(row + 0, p);
+  fe_store(row + 1, av);
+  fe_store(row + 2, s);
+  fe_store(row + 3, d1);
+  fe_store(row + 4, d2);
+  fe_store(row + 5, d3);
+  fe_store(row + 6, b2);
+  fe_store(row + 7, b3);
+}
+
+struct LincombArgs {
+  const fe* rows;
+  fe* out;
+  uint64_t prec;
+  fe k_m[11];
+  fe xs_m[8];  // (g2^steps)^t, t = i mod 8 (prove.rs:287-291)
+};
+
+// L = k0 D1 + k1 D2 + k2 D3 + k3 P + k4 P x^steps + k5 B2 + k6 B2 x^steps +
+//     k7 B3 + k8 B3 x^steps + k9 A + k10 S (prove.rs:293-322).
+__global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.prec) return;
+  const fe* row = a.rows + 8 * i;
+  const fe p = fe_load(row + 0), av = fe_load(row + 1), s = fe_load(row + 2), d1 = fe_load(row + 3),
+           d2 = fe_load(row + 4), d3 = fe_load(row + 5), b2 = fe_load(row + 6), b3 = fe_load(row + 7);
+  const uint32_t t = (uint32_t)(i & 7);
+  fe xs = a.xs_m[0];
+#pragma unroll
+  for (uint32_t k = 1; k < 8; ++k)
+    if (t == k) xs = a.xs_m[k];
+  fe acc = fe_mul(d1, a.k_m[0]);
+  acc = fe_add(acc, fe_mul(d2, a.k_m[1]));
+  acc = fe_add(acc, fe_mul(d3, a.k_m[2]));
+  acc = fe_add(acc, fe_mul(p, a.k_m[3]));
+  acc = fe_add(acc, fe_mul(fe_mul(p, a.k_m[4]), xs));
+  acc = fe_add(acc, fe_mul(b2, a.k_m[5]));
+  acc = fe_add(acc, fe_mul(fe_mul(b2, a.k_m[6]), xs));
+  acc = fe_add(acc, fe_mul(b3, a.k_m[7]));
+  acc = fe_add(acc, fe_mul(fe_mul(b3, a.k_m[8]), xs));
+  acc = fe_add(acc, fe_mul(av, a.k_m[9]));
+  acc = fe_add(acc, fe_mul(s, a.k_m[10]));
+  fe_store(a.out + i, acc);
+}
+
+// ---- host helpers -----------------------------------------------------------
+
+// log2_ceil, utils.rs:14-23.
+static uint32_t log2_ceil_ref(size_t v) {
+  uint32_t l = 1;
+  while (v > 1) {
+    v /= 2;
+    ++l;
+  }
+  return l;
+}
+
+static HostFp host_fe(const uint64_t* c) { return FieldHost::get().from_canonical(c); }
+
+// lagrange_interp (fri/src/poly_utils.rs:409-439): the unique interpolant,
+// n coefficients, Montgomery on the host.
+static std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys) {
+  const FieldHost& F = FieldHost::get();
+  const size_t n = xs.size();
+  std::vector<HostFp> root(1, F.one());
+  for (size_t i = 0; i < n; ++i) {  // prod (X - x_i), low degree first
+    std::vector<HostFp> nxt(root.size() + 1, F.zero());
+    for (size_t j = 0; j < root.size(); ++j) {
+      nxt[j + 1] = F.add(nxt[j + 1], root[j]);
+      nxt[j] = F.sub(nxt[j], F.mul(root[j], xs[i]));
+    }
+    root.swap(nxt);
+  }
+  std::vector<HostFp> b(n, F.zero()), num(n), den(n);
+  std::vector<std::vector<HostFp>> nums(n);
+  for (size_t i = 0; i < n; ++i) {
+    HostFp carry = F.zero();
+    for (size_t d = n; d >= 1; --d) {  // root / (X - x_i), synthetic division
+      carry = d == n ? root[d] : F.add(root[d], F.mul(carry, xs[i]));
+      num[d - 1] = carry;
+    }
+    HostFp y = F.zero();
+    for (size_t d = n; d-- > 0;) y = F.add(F.mul(y, xs[i]), num[d]);
+    den[i] = y;
+    nums[i] = num;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const HostFp s = F.mul(ys[i], F.inv(den[i]));
+    for (size_t j = 0; j < n; ++j) b[j] = F.add(b[j], F.mul(nums[i][j], s));
+  }
+  return b;
+}
+
+// Owned device allocations of one proof.
+struct Arena {
+  std::vector<void*> ptrs;
+  ~Arena() {
+    for (void* p : ptrs) hipFree(p);
+  }
+  template <class T>
+  stark_status get(stark_ctx* ctx, size_t count, T** out) {
+    void* p = nullptr;
+    const hipError_t e = hipMalloc(&p, (count ? count : 1) * sizeof(T));
+    if (e != hipSuccess) {
+      ctx->last_error = std::string("hipMalloc: ") + hipGetErrorString(e);
+      return STARK_ERR_OOM;
+    }
+    ptrs.push_back(p);
+    *out = (T*)p;
+    return STARK_OK;
+  }
+};
+
+#define STARK_TRY(expr)                 \
+  do {                                  \
+    stark_status st_ = (expr);          \
+    if (st_ != STARK_OK) return st_;    \
+  } while (0)
+
+static unsigned blocks_for(uint64_t n, unsigned t = 256) { return (unsigned)((n + t - 1) / t); }
+
+// In-place inclusive product scan of n Montgomery values; canonical copy to `canon` if non-null.
+static stark_status product_scan(stark_ctx* ctx, fe* v, uint64_t n, fe* tot, fe* canon, const Mont& mc,
+                                 hipStream_t s) {
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+  hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(256), 0, s, v, n, tot, mc.one);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(256), 0, s, tot, nb, mc.one);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, v, n, (const fe*)tot, mc.unit, canon);
+  STARK_HIP(ctx, hipGetLastError());
+  return STARK_OK;
+}
+
+// LDE of `batch` step columns (in place in `coef`, destroyed) into `out`
+// (batch x precision): inv_best_fft(., g1) then best_fft(., g2) (prove.rs:100-101).
+static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint32_t log_steps, uint32_t log_prec,
+                        const Twiddles& tw_g1_inv, const Twiddles& tw_g2, hipStream_t s) {
+  STARK_TRY(ntt_device(ctx, coef, log_steps, batch, tw_g1_inv, true, s));
+  const uint64_t total = (uint64_t)batch << log_prec;
+  hipLaunchKernelGGL(r1cs_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, s, (const fe*)coef, out, log_steps,
+                     log_prec, total);
+  STARK_HIP(ctx, hipGetLastError());
+  return ntt_device(ctx, out, log_prec, batch, tw_g2, false, s);
+}
+
+struct TreeGuard {
+  stark_merkle_tree* t = nullptr;
+  ~TreeGuard() { stark_merkle_free(t); }
+};
+
+static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
+                               size_t os, const uint64_t* public_wires, size_t n_public,
+                               const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
+                               const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
+                               const uint64_t* flag2, size_t n_constraints, size_t n_wires, stark_r1cs_proof** out) {
+  const FieldHost& F = FieldHost::get();
+  hipStream_t s = ctx->stream;
+  // prove.rs:30-53
+  if (os > 3 * n_constraints * n_wires || os % 3 != 0) return STARK_ERR_BAD_ARG;
+  if (os < 5) return STARK_ERR_BAD_LENGTH;  // the reference's steps/log_steps disagree below 8 steps
+  const uint32_t log_steps = log2_ceil_ref(os - 1);
+  const uint32_t log_prec = log_steps + kLogExtensionFactor;
+  if (log_prec > 28) return STARK_ERR_BAD_LENGTH;
+  const uint64_t steps = (uint64_t)1 << log_steps, prec = (uint64_t)1 << log_prec;
+  const uint64_t skips = prec / steps;
+  for (size_t i = 0; i < n_pfi; ++i)
+    if (public_first_indices[2 * i] >= n_public || public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
+
+  // Roots (prove.rs:71-94): g2 = 7^((p-1)/precision), g1 = g2^8.
+  uint64_t pm1[4];
+  {
+    const uint64_t* p = FieldHost::kP;
+    memcpy(pm1, p, 32);
+    pm1[0] -= 1;
+    for (uint32_t k = 0; k < log_prec; ++k)
+      for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
+  }
+  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
+  const HostFp g1 = F.pow_u64(g2, skips);
+  uint64_t g2c[4], g1ic[4];
+  F.to_canonical(g2, g2c);
+  F.to_canonical(F.inv(g1), g1ic);
+  const Twiddles* tw2 = nullptr;
+  const Twiddles* tw1i = nullptr;
+  STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
+  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
+  const Mont mc = mont();
+
+  Arena ar;
+  fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
+  uint64_t* perm;
+  uint64_t* acc_leaves;
+  int* d_err;
+  const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
+  STARK_TRY(ar.get(ctx, 8 * steps, &raw));  // K F0 F1 F2 S P IDX PIDX (then A's slot reuses K's)
+  STARK_TRY(ar.get(ctx, steps, &wcopy));
+  STARK_TRY(ar.get(ctx, steps, &perm));
+  STARK_TRY(ar.get(ctx, 5 * steps, &acc_leaves));
+  STARK_TRY(ar.get(ctx, 9 * prec, &cols));
+  STARK_TRY(ar.get(ctx, steps, &nmr));
+  STARK_TRY(ar.get(ctx, steps, &dnm));
+  STARK_TRY(ar.get(ctx, 2 * (size_t)nb, &tot));
+  STARK_TRY(ar.get(ctx, steps, &dnm_c));
+  STARK_TRY(ar.get(ctx, steps, &inv_dnm));
+  STARK_TRY(ar.get(ctx, 2 * prec, &zb));
+  STARK_TRY(ar.get(ctx, 2 * prec, &inv_zb));
+  STARK_TRY(ar.get(ctx, 2 * n_pfi + 2, &consts));
+  STARK_TRY(ar.get(ctx, 8 * prec, &rows));
+  STARK_TRY(ar.get(ctx, prec, &lvals));
+  STARK_TRY(ar.get(ctx, 1, &d_err));
+
+  // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).
+  const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
+  for (int c = 0; c < 6; ++c) {
+    STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyHostToDevice, s));
+    if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
+  }
+  static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
+  STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
+  STARK_HIP(ctx, hipMemsetAsync(d_err, 0, sizeof(int), s));
+  hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
+  STARK_HIP(ctx, hipGetLastError());
+
+  auto proof = std::make_unique<stark_r1cs_proof>();
+  // Accumulator tree -> a_root (utils.rs:250-270) -> r (utils.rs:272-290).
+  TreeGuard acc_tree, m_tree, l_tree;
+  STARK_TRY(stark_merkle_new(ctx, &acc_tree.t));
+  STARK_TRY(stark_merkle_new(ctx, &m_tree.t));
+  STARK_TRY(stark_merkle_new(ctx, &l_tree.t));
+  STARK_TRY(merkle_build(ctx, acc_tree.t, (const uint8_t*)acc_leaves, steps, 40, s));
+  // The eight LDEs overlap with the host's wait for a_root below.
+  STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
+  STARK_TRY(merkle_root_d2h(ctx, acc_tree.t, s, proof->a_root));
+  HostFp r[3];
+  {
+    uint32_t rnd[24];
+    STARK_TRY(stark_get_pseudorandom_indices(proof->a_root, 32, (uint32_t)prec, 24, 0, rnd));
+    for (int c = 0; c < 3; ++c) {
+      uint8_t be[32];
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t v = rnd[8 * c + i];
+        be[4 * i] = (uint8_t)(v >> 24);
+        be[4 * i + 1] = (uint8_t)(v >> 16);
+        be[4 * i + 2] = (uint8_t)(v >> 8);
+        be[4 * i + 3] = (uint8_t)v;
+      }
+      r[c] = F.from_bytes_le(be, 32);
+    }
+  }
+  uint64_t r0c[4];
+  F.to_canonical(r[0], r0c);
+  fe r0_canon;
+  for (int k = 0; k < 4; ++k) {
+    r0_canon.w[2 * k] = (uint32_t)r0c[k];
+    r0_canon.w[2 * k + 1] = (uint32_t)(r0c[k] >> 32);
+  }
+  // A (utils.rs:293-339, prove.rs:183-184).
+  fe* ext_idx = cols + 6 * prec;
+  fe* ext_pidx = cols + 7 * prec;
+  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
+                     (const fe*)ext_pidx, (const fe*)wcopy, steps, r0_canon, to_dev(r[1]), to_dev(r[2]), mc.r2, nmr,
+                     dnm);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
+  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
+  STARK_TRY(multi_inv_device(ctx, dnm_c, inv_dnm, steps, s));
+  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
+                     (const fe*)inv_dnm, steps, raw);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(lde(ctx, raw, 1, cols + 8 * prec, log_steps, log_prec, *tw1i, *tw2, s));
+
+  // Interpolants and boundary points (utils.rs:421-474), host side (#pub points).
+  const HostFp x_last = F.pow_u64(g2, prec - skips);
+  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
+  for (size_t i = 0; i < n_pfi; ++i) {
+    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
+    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
+  }
+  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
+  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
+  {
+    std::vector<fe> h(2 * n_pfi + 2);
+    for (size_t i = 0; i < n_pfi; ++i) {
+      h[i] = to_dev(xv[i]);  // Montgomery x_k for Zb2
+      uint64_t c[4];
+      F.to_canonical(interp2[i], c);
+      for (int k = 0; k < 4; ++k) {
+        h[n_pfi + i].w[2 * k] = (uint32_t)c[k];
+        h[n_pfi + i].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+      }
+    }
+    uint64_t c[4];
+    F.to_canonical(interp3[0], c);
+    for (int k = 0; k < 4; ++k) {
+      h[2 * n_pfi].w[2 * k] = (uint32_t)c[k];
+      h[2 * n_pfi].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+    }
+    STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+    STARK_HIP(ctx, hipStreamSynchronize(s));  // h is a stack buffer
+  }
+  hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
+                     (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one, zb, zb + prec);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * prec, s));
+
+  // Constraint kernel.
+  ConstraintArgs ca;
+  ca.cols = cols;
+  ca.inv_zb = inv_zb;
+  ca.interp2 = consts + n_pfi;
+  ca.interp3 = consts + 2 * n_pfi;
+  ca.lo = tw2->d_lo;
+  ca.hi = tw2->d_hi;
+  ca.rows = rows;
+  ca.err = d_err;
+  ca.prec = prec;
+  ca.shift1 = (os / 3 * skips) % prec;
+  ca.shift2 = (os / 3 * 2 * skips) % prec;
+  ca.log_prec = log_prec;
+  ca.kb = tw2->kb;
+  ca.n2 = (uint32_t)n_pfi;
+  ca.n3 = 1;
+  ca.r0 = r0_canon;
+  ca.r1_m = to_dev(r[1]);
+  ca.r2_m = to_dev(r[2]);
+  ca.mr2 = mc.r2;
+  {
+    // Z(g2^i) = (g2^steps)^(i mod 8) - 1; inverse with 0 -> 0 (prove.rs:128-129, 203).
+    const HostFp w8 = F.pow_u64(g2, steps);
+    HostFp wt = F.one();
+    for (int t = 0; t < 8; ++t) {
+      const HostFp z = F.sub(wt, F.one());
+      ca.invz_m[t] = FieldHost::eq(z, F.zero()) ? fe_zero_host() : to_dev(F.inv(z));
+      wt = F.mul(wt, w8);
+    }
+  }
+  hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
+  STARK_HIP(ctx, hipGetLastError());
+  // Main tree over the 256-B rows (prove.rs:261-264).
+  STARK_TRY(merkle_build(ctx, m_tree.t, (const uint8_t*)rows, prec, 256, s));
+  STARK_TRY(merkle_root_d2h(ctx, m_tree.t, s, proof->m_root));
+  int h_err = 0;
+  STARK_HIP(ctx, hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  if (h_err) {
+    ctx->last_error = (h_err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
+                                  : "invalid B: boundary value mismatch (utils.rs:477-524)";
+    return STARK_ERR_CHECK;
+  }
+  // k (prove.rs:274-283): k_i = BE integer of Blake2s(m_root || i) mod p.
+  LincombArgs la;
+  la.rows = rows;
+  la.out = lvals;
+  la.prec = prec;
+  la.k_m[0] = to_dev(F.one());
+  for (int i = 1; i < 11; ++i) {
+    uint8_t msg[33], h[32], le[32];
+    memcpy(msg, proof->m_root, 32);
+    msg[32] = (uint8_t)i;
+    b2s_host(msg, 33, h);
+    for (int b = 0; b < 32; ++b) le[b] = h[31 - b];
+    la.k_m[i] = to_dev(F.from_bytes_le(le, 32));
+  }
+  {
+    const HostFp w8 = F.pow_u64(g2, steps);
+    HostFp wt = F.one();
+    for (int t = 0; t < 8; ++t) {
+      la.xs_m[t] = to_dev(wt);
+      wt = F.mul(wt, w8);
+    }
+  }
+  hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(merkle_build(ctx, l_tree.t, (const uint8_t*)lvals, prec, 32, s));
+  STARK_TRY(merkle_root_d2h(ctx, l_tree.t, s, proof->l_root));
+
+  // Spot checks (prove.rs:337-362).
+  uint32_t pos32[kSpotChecks];
+  STARK_TRY(stark_get_pseudorandom_indices(proof->l_root, 32, (uint32_t)prec, kSpotChecks, (uint32_t)skips, pos32));
+  std::vector<size_t> positions(kSpotChecks), aug(4 * kSpotChecks);
+  for (int i = 0; i < kSpotChecks; ++i) {
+    const size_t j = pos32[i];
+    positions[i] = j;
+    aug[4 * i] = j;
+    aug[4 * i + 1] = (j + prec - skips) % prec;
+    aug[4 * i + 2] = (j + os / 3 * skips) % prec;
+    aug[4 * i + 3] = (j + os / 3 * 2 * skips) % prec;
+  }
+  std::vector<uint8_t> l_leaves(32 * kSpotChecks), l_nodes(32 * kSpotChecks * log_prec);
+  std::vector<uint8_t> m_leaves(256 * 4 * kSpotChecks), m_nodes(32 * 4 * kSpotChecks * log_prec);
+  STARK_TRY(merkle_gather(ctx, l_tree.t, positions.data(), kSpotChecks, l_leaves.data(), l_nodes.data(), s));
+  STARK_TRY(merkle_gather(ctx, m_tree.t, aug.data(), 4 * kSpotChecks, m_leaves.data(), m_nodes.data(), s));
+
+  // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367).
+  stark_fri_proof* fri = nullptr;
+  STARK_TRY(stark_prove_low_degree_dev(ctx, (const uint64_t*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri));
+  size_t fri_len = 0;
+  stark_status st = stark_fri_proof_json(fri, nullptr, 0, &fri_len);
+  std::string fri_json(fri_len, '\0');
+  if (st == STARK_OK) st = stark_fri_proof_json(fri, &fri_json[0], fri_len, &fri_len);
+  stark_fri_proof_free(fri);
+  if (st != STARK_OK) return st;
+
+  // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
+  std::string& o = proof->json;
+  o.reserve(fri_len + 4 * kSpotChecks * (256 * 4 + log_prec * 32 * 4) + kSpotChecks * (log_prec + 1) * 32 * 4);
+  o += "{\"m_root\":";
+  json_bytes(o, proof->m_root, 32);
+  o += ",\"l_root\":";
+  json_bytes(o, proof->l_root, 32);
+  o += ",\"a_root\":";
+  json_bytes(o, proof->a_root, 32);
+  o += ",\"main_branches\":";
+  json_branches(o, m_leaves, 256, m_nodes, 4 * kSpotChecks, log_prec);
+  o += ",\"linear_comb_branches\":";
+  json_branches(o, l_leaves, 32, l_nodes, kSpotChecks, log_prec);
+  o += ",\"fri_proof\":";
+  o += fri_json;
+  o += "}";
+  *out = proof.release();
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+stark_status stark_mk_r1cs_proof(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
+                                 size_t original_steps, const uint64_t* public_wires, size_t n_public,
+                                 const size_t* public_first_indices, size_t n_public_first,
+                                 const size_t* permuted_indices, const uint64_t* coefficients, const uint64_t* flag0,
+                                 const uint64_t* flag1, const uint64_t* flag2, size_t n_constraints, size_t n_wires,
+                                 stark_r1cs_proof** out) {
+  if (!ctx || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  if (original_steps && (!witness_trace || !computational_trace || !permuted_indices || !coefficients || !flag0 ||
+                         !flag1 || !flag2))
+    return STARK_ERR_BAD_ARG;
+  if ((n_public && !public_wires) || (n_public_first && !public_first_indices)) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const stark_status st = prove_r1cs(ctx, witness_trace, computational_trace, original_steps, public_wires, n_public,
+                                     public_first_indices, n_public_first, permuted_indices, coefficients, flag0,
+                                     flag1, flag2, n_constraints, n_wires, out);
+  hipStreamSynchronize(ctx->stream);
+  return st;
+}
+
+stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, size_t cap, size_t* len) {
+  if (!proof || !len) return STARK_ERR_BAD_ARG;
+  *len = proof->json.size();
+  if (buf && cap) {
+    const size_t k = proof->json.size() < cap ? proof->json.size() : cap;
+    memcpy(buf, proof->json.data(), k);
+    if (k < cap) buf[k] = 0;
+  }
+  return STARK_OK;
+}
+
+stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_root[32], uint8_t l_root[32],
+                                    uint8_t a_root[32]) {
+  if (!proof) return STARK_ERR_BAD_ARG;
+  if (m_root) memcpy(m_root, proof->m_root, 32);
+  if (l_root) memcpy(l_root, proof->l_root, 32);
+  if (a_root) memcpy(a_root, proof->a_root, 32);
+  return STARK_OK;
+}
+
+void stark_r1cs_proof_free(stark_r1cs_proof* proof) { delete proof; }
+
+}  // extern "C"

@@ -30,7 +30,7 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "
 P = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
 STATUS = {0: "ok", 1: "bad length", 2: "bad root", 3: "bad argument", 4: "out of memory", 5: "HIP error",
-          6: "no gfx950 device", 7: "bad call order"}
+          6: "no gfx950 device", 7: "bad call order", 8: "constraint check failed"}
 
 
 class StarkError(RuntimeError):
@@ -78,6 +78,17 @@ _SIGNATURES = {
     "stark_fri_proof_num_layers": ([_vp], ctypes.c_size_t),
     "stark_fri_proof_layer_info": ([_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), _u8p, _szp, _szp, _szp,
                                     _szp, _szp], ctypes.c_int),
+    "stark_mk_r1cs_proof": ([_vp, _u64p, _u64p, ctypes.c_size_t, _u64p, ctypes.c_size_t, _szp, ctypes.c_size_t,
+                             _szp, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_size_t,
+                             ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_r1cs_proof_json": ([_vp, ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
+    "stark_r1cs_proof_roots": ([_vp, _u8p, _u8p, _u8p], ctypes.c_int),
+    "stark_r1cs_proof_free": ([_vp], None),
+    "stark_r1cs_trace_build": ([_u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_r1cs_trace_dims": ([_vp, _szp, _szp, _szp, _szp, _szp], ctypes.c_int),
+    "stark_r1cs_trace_export": ([_vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _szp, _u64p, _szp], ctypes.c_int),
+    "stark_r1cs_trace_free": ([_vp], None),
+    "stark_prove_r1cs_trace": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_transpose_dev": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32, _vp], ctypes.c_int),
     "stark_twiddle2d_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _u64p,
                              ctypes.c_uint32, _vp], ctypes.c_int),
@@ -156,7 +167,7 @@ class Context:
 
     def check(self, rc: int, where: str):
         if rc != 0:
-            detail = self.lib.stark_ctx_last_error(self.h).decode() if rc == 5 else ""
+            detail = self.lib.stark_ctx_last_error(self.h).decode() if rc in (5, 8) else ""
             raise StarkError(rc, where, detail)
 
     @property

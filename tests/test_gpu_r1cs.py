@@ -1,0 +1,92 @@
+"""mk_r1cs_proof on the GPU (stark_mk_r1cs_proof / stark_prove_r1cs_trace)
+against the CPU oracle, byte for byte, on the reference's own R1CS fixtures.
+
+Bar: the StarkProof JSON is identical to oracle/r1cs.c's (the restatement of
+prove.rs:14-378), its digest equals the committed golden digest, and the
+restated verifier (verify.rs:13-258) accepts it.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import r1cs as R
+from oracle import to_limbs
+from stark_verify import verify_r1cs_proof
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIX = os.path.join(HERE, "golden", "r1cs")
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "r1cs_proofs.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+def _read(name, ext):
+    with open(os.path.join(FIX, f"{name}.{ext}"), "rb") as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("name", list(GOLDEN))
+def test_prove_with_witness_matches_oracle(ctx, oracle, name):
+    from stark_amd.r1cs import prove_with_witness
+    proof = prove_with_witness(ctx, _read(name, "r1cs"), _read(name, "wtns"))
+    s = proof.to_json()
+    assert hashlib.sha256(s.encode()).hexdigest() == GOLDEN[name]["json_sha256"]
+    tr = R.build_trace(*R.load_fixture(FIX, name))
+    if name in ("compute", "poseidon3_test"):
+        assert s == R.mk_r1cs_proof_json(oracle, tr)
+    roots = proof.roots()
+    assert roots["m_root"].hex() == GOLDEN[name]["m_root"]
+    assert roots["a_root"].hex() == GOLDEN[name]["a_root"]
+    assert verify_r1cs_proof(oracle, s, tr.public_wires, tr.public_first_indices, tr.permuted_indices,
+                             tr.coefficients, tr.flag0, tr.flag1, tr.flag2, tr.n_constraints, tr.n_wires)
+
+
+def test_mk_r1cs_proof_from_python_trace(ctx, oracle):
+    """The prove.rs-level entry point fed with the Python-built trace."""
+    from stark_amd.r1cs import mk_r1cs_proof
+    tr = R.build_trace(*R.load_fixture(FIX, "poseidon3_test"))
+    p = mk_r1cs_proof(ctx, to_limbs(tr.witness_trace), to_limbs(tr.computational_trace), to_limbs(tr.public_wires),
+                      tr.public_first_indices, tr.permuted_indices, to_limbs(tr.coefficients), to_limbs(tr.flag0),
+                      to_limbs(tr.flag1), to_limbs(tr.flag2), tr.n_constraints, tr.n_wires)
+    assert hashlib.sha256(p.to_json().encode()).hexdigest() == GOLDEN["poseidon3_test"]["json_sha256"]
+
+
+def test_unsatisfied_witness_is_rejected(ctx):
+    """The reference panics in calc_d1_polynomial (utils.rs:379-390); the library returns STARK_ERR_CHECK."""
+    from stark_amd import StarkError
+    from stark_amd.r1cs import mk_r1cs_proof
+    tr = R.build_trace(*R.load_fixture(FIX, "compute"))
+    ct = list(tr.computational_trace)
+    ct[3] = (ct[3] + 1) % R.P
+    with pytest.raises(StarkError) as e:
+        mk_r1cs_proof(ctx, to_limbs(tr.witness_trace), to_limbs(ct), to_limbs(tr.public_wires),
+                      tr.public_first_indices, tr.permuted_indices, to_limbs(tr.coefficients), to_limbs(tr.flag0),
+                      to_limbs(tr.flag1), to_limbs(tr.flag2), tr.n_constraints, tr.n_wires)
+    assert e.value.code == 8
+
+
+def test_bad_public_wire_is_rejected(ctx):
+    """A public wire that disagrees with the trace breaks B2 (utils.rs:477-499)."""
+    from stark_amd import StarkError
+    from stark_amd.r1cs import mk_r1cs_proof
+    tr = R.build_trace(*R.load_fixture(FIX, "compute"))
+    pw = list(tr.public_wires)
+    pw[1] = (pw[1] + 1) % R.P
+    with pytest.raises(StarkError) as e:
+        mk_r1cs_proof(ctx, to_limbs(tr.witness_trace), to_limbs(tr.computational_trace), to_limbs(pw),
+                      tr.public_first_indices, tr.permuted_indices, to_limbs(tr.coefficients), to_limbs(tr.flag0),
+                      to_limbs(tr.flag1), to_limbs(tr.flag2), tr.n_constraints, tr.n_wires)
+    assert e.value.code == 8
+
+
+def test_repeated_proofs_identical(ctx):
+    """No state leaks between proofs on one context (cached twiddles, scratch buffers)."""
+    from stark_amd.r1cs import prove_with_witness
+    a = prove_with_witness(ctx, _read("compute", "r1cs"), _read("compute", "wtns")).to_json()
+    b = prove_with_witness(ctx, _read("pedersen_test", "r1cs"), _read("pedersen_test", "wtns")).to_json()
+    c = prove_with_witness(ctx, _read("compute", "r1cs"), _read("compute", "wtns")).to_json()
+    assert a == c
+    assert hashlib.sha256(b.encode()).hexdigest() == GOLDEN["pedersen_test"]["json_sha256"]
