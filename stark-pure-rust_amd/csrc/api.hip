@@ -33,6 +33,15 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   return STARK_OK;
 }
 
+stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out) {
+  if (!ctx->trees[slot]) {
+    stark_status st = stark_merkle_new(ctx, &ctx->trees[slot]);
+    if (st != STARK_OK) return st;
+  }
+  *out = ctx->trees[slot];
+  return STARK_OK;
+}
+
 hipStream_t pick_stream(stark_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
 
 // Host-buffer NTT: copy in (zero-padded), transform on the GPU, copy out.
@@ -111,7 +120,11 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->tw)
     if (kv.second->d_lo) hipFree(kv.second->d_lo);
-  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2})
+  for (stark_merkle_tree*& t : ctx->trees) {
+    stark_merkle_free(t);
+    t = nullptr;
+  }
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);
   delete ctx;

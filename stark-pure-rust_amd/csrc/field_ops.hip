@@ -31,7 +31,9 @@ __device__ fe fe_inv_mont(const fe& x, const fe& one_m) {
 }
 
 // Phase 1: chunk c of kInvChunk elements -> prefix products (Montgomery,
-// zeros skipped) into pref, chunk product into tot[c].
+// zeros skipped) into pref, chunk product into tot[c].  MONT_IN: the input
+// already holds Montgomery images (the chunk products of a lower level).
+template <bool MONT_IN>
 __global__ void inv_prefix_kernel(const fe* __restrict__ v, uint64_t n, fe* __restrict__ pref, fe* __restrict__ tot,
                                   MontConsts mc) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -42,7 +44,7 @@ __global__ void inv_prefix_kernel(const fe* __restrict__ v, uint64_t n, fe* __re
   for (uint64_t i = lo; i < hi; ++i) {
     pref[i] = acc;  // product of the non-zero elements before i (exclusive)
     const fe x = fe_load(v + i);
-    if (!fe_is_zero(x)) acc = fe_mul(acc, fe_mul(x, mc.r2));
+    if (!fe_is_zero(x)) acc = fe_mul(acc, MONT_IN ? x : fe_mul(x, mc.r2));
   }
   tot[c] = acc;
 }
@@ -54,7 +56,10 @@ __global__ void inv_chunk_kernel(fe* __restrict__ tot, uint64_t chunks, MontCons
   tot[c] = fe_inv_mont(tot[c], mc.one);
 }
 
-// Phase 3: walk each chunk backwards (poly_utils.rs:55-67 order).
+// Phase 3: walk each chunk backwards (poly_utils.rs:55-67 order).  `tot`
+// holds the Montgomery inverse of each chunk product.  Output canonical, or
+// Montgomery when MONT_IN.
+template <bool MONT_IN>
 __global__ void inv_back_kernel(const fe* __restrict__ v, uint64_t n, const fe* __restrict__ pref,
                                 const fe* __restrict__ tot, fe* __restrict__ out, MontConsts mc) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -62,17 +67,16 @@ __global__ void inv_back_kernel(const fe* __restrict__ v, uint64_t n, const fe* 
   if (lo >= n) return;
   const uint64_t hi = lo + kInvChunk < n ? lo + kInvChunk : n;
   fe inv = tot[c];  // Montgomery
+  fe unit = fe_zero();
+  unit.w[0] = 1;
   for (uint64_t i = hi; i-- > lo;) {
     const fe x = fe_load(v + i);
     if (fe_is_zero(x)) {
       fe_store(out + i, fe_zero());
     } else {
-      // canonical(pref * inv) = montmul(montmul(pref, inv), 1): pref, inv Montgomery.
-      fe unit = fe_zero();
-      unit.w[0] = 1;
-      fe_store(out + i, fe_mul(fe_mul(pref[i], inv), unit));
-      inv = fe_mul(inv, x);  // Montgomery * canonical -> Montgomery of inv * x / R ... fixed below
-      inv = fe_mul(inv, mc.r2);
+      const fe r = fe_mul(pref[i], inv);  // Montgomery x^-1
+      fe_store(out + i, MONT_IN ? r : fe_mul(r, unit));
+      inv = fe_mul(inv, MONT_IN ? x : fe_mul(x, mc.r2));
     }
   }
 }
@@ -111,18 +115,37 @@ MontConsts mont_consts() {
   return mc;
 }
 
+// Batch inverse (0 -> 0).  Chunk products of kInvChunk elements; when there
+// are many chunks their inverses come from a second batch-inverse level, so
+// only n / kInvChunk^2 Fermat inversions run.
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s) {
   if (n == 0) return STARK_OK;
-  const uint64_t chunks = (n + kInvChunk - 1) / kInvChunk;
-  stark_status st = ensure_buf(ctx, ctx->io2, (n + chunks) * sizeof(fe));
+  const uint64_t c1 = (n + kInvChunk - 1) / kInvChunk;
+  const uint64_t c2 = (c1 + kInvChunk - 1) / kInvChunk;
+  const bool two = c1 > 4096;
+  stark_status st = ensure_buf(ctx, ctx->io2, (n + c1 + (two ? 2 * c1 + c2 : 0)) * sizeof(fe));
   if (st != STARK_OK) return st;
-  fe* pref = (fe*)ctx->io2.ptr;
-  fe* tot = pref + n;
+  fe* pref1 = (fe*)ctx->io2.ptr;
+  fe* tot1 = pref1 + n;
   const MontConsts mc = mont_consts();
-  const unsigned blocks = (unsigned)((chunks + 255) / 256);
-  hipLaunchKernelGGL(inv_prefix_kernel, dim3(blocks), dim3(256), 0, s, d_in, n, pref, tot, mc);
-  hipLaunchKernelGGL(inv_chunk_kernel, dim3(blocks), dim3(256), 0, s, tot, chunks, mc);
-  hipLaunchKernelGGL(inv_back_kernel, dim3(blocks), dim3(256), 0, s, d_in, n, pref, tot, d_out, mc);
+  const unsigned b1 = (unsigned)((c1 + 255) / 256);
+  hipLaunchKernelGGL(inv_prefix_kernel<false>, dim3(b1), dim3(256), 0, s, d_in, n, pref1, tot1, mc);
+  const fe* tot1_inv = tot1;
+  if (two) {
+    fe* pref2 = tot1 + c1;
+    fe* tot2 = pref2 + c1;
+    fe* inv1 = tot2 + c2;
+    const unsigned b2 = (unsigned)((c2 + 255) / 256);
+    hipLaunchKernelGGL(inv_prefix_kernel<true>, dim3(b2), dim3(256), 0, s, (const fe*)tot1, c1, pref2, tot2, mc);
+    hipLaunchKernelGGL(inv_chunk_kernel, dim3(b2), dim3(256), 0, s, tot2, c2, mc);
+    hipLaunchKernelGGL(inv_back_kernel<true>, dim3(b2), dim3(256), 0, s, (const fe*)tot1, c1, (const fe*)pref2,
+                       (const fe*)tot2, inv1, mc);
+    tot1_inv = inv1;
+  } else {
+    hipLaunchKernelGGL(inv_chunk_kernel, dim3(b1), dim3(256), 0, s, tot1, c1, mc);
+  }
+  hipLaunchKernelGGL(inv_back_kernel<false>, dim3(b1), dim3(256), 0, s, d_in, n, (const fe*)pref1, tot1_inv, d_out,
+                     mc);
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
 }

@@ -129,6 +129,13 @@ class FieldHost {
   static bool eq(const HostFp& a, const HostFp& b) { return memcmp(a.v, b.v, 32) == 0; }
   // from_bytes_le (ff_utils/src/fp.rs:74-76): little-endian integer of up to
   // 32 bytes, reduced mod p (ff from_str semantics).  Returns Montgomery.
+  // The same value in canonical form (no Montgomery conversion).
+  HostFp reduce_bytes_le(const uint8_t* b, size_t len) const {
+    HostFp a{{0, 0, 0, 0}};
+    for (size_t i = 0; i < len && i < 32; ++i) a.v[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
+    while (ge_p(a.v)) sub_p_in_place(a.v);
+    return a;
+  }
   HostFp from_bytes_le(const uint8_t* b, size_t len) const {
     uint64_t c[4] = {0, 0, 0, 0};
     for (size_t i = 0; i < len && i < 32; ++i) c[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));

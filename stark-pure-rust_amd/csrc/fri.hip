@@ -105,29 +105,15 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
       col_total += m;
     }
   }
-  DevBuf cols;
-  stark_status st = ensure_buf(ctx, cols, (col_total ? col_total : 1) * sizeof(fe));
+  stark_status st = ensure_buf(ctx, ctx->fri_cols, (col_total ? col_total : 1) * sizeof(fe));
   if (st != STARK_OK) return st;
-  struct Guard {
-    DevBuf* b;
-    ~Guard() {
-      if (b->ptr) hipFree(b->ptr);
-    }
-  } guard{&cols};
   stark_merkle_tree* trees[2] = {nullptr, nullptr};
-  st = stark_merkle_new(ctx, &trees[0]);
-  if (st == STARK_OK) st = stark_merkle_new(ctx, &trees[1]);
-  struct TreeGuard {
-    stark_merkle_tree** t;
-    ~TreeGuard() {
-      stark_merkle_free(t[0]);
-      stark_merkle_free(t[1]);
-    }
-  } tguard{trees};
+  st = ctx_tree(ctx, 0, &trees[0]);
+  if (st == STARK_OK) st = ctx_tree(ctx, 1, &trees[1]);
   if (st != STARK_OK) return st;
 
   const fe* cur = d_values;
-  fe* next = (fe*)cols.ptr;
+  fe* next = (fe*)ctx->fri_cols.ptr;
   size_t m = n;
   int tc = 0;  // trees[tc] holds the tree of `cur`
   HostFp w = F.from_canonical(root);
@@ -190,14 +176,29 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
   return STARK_OK;
 }
 
-void json_bytes(std::string& o, const uint8_t* p, size_t n) {
-  o.push_back('[');
-  char tmp[8];
-  for (size_t i = 0; i < n; ++i) {
-    int k = snprintf(tmp, sizeof tmp, i ? ",%u" : "%u", (unsigned)p[i]);
-    o.append(tmp, (size_t)k);
+// "[b0,b1,...]" for a byte string (serde_json of Vec<u8>), table driven.
+struct ByteText {
+  char s[256][4];
+  uint8_t len[256];
+  ByteText() {
+    for (int i = 0; i < 256; ++i) len[i] = (uint8_t)snprintf(s[i], sizeof s[i], "%d", i);
   }
-  o.push_back(']');
+};
+
+void json_bytes(std::string& o, const uint8_t* p, size_t n) {
+  static const ByteText T;
+  const size_t at = o.size();
+  o.resize(at + 2 + 4 * n);  // upper bound: 3 digits + comma per byte
+  char* w = &o[at];
+  *w++ = '[';
+  for (size_t i = 0; i < n; ++i) {
+    if (i) *w++ = ',';
+    const uint8_t b = p[i];
+    memcpy(w, T.s[b], 4);
+    w += T.len[b];
+  }
+  *w++ = ']';
+  o.resize((size_t)(w - &o[0]));
 }
 
 // serde_json of Vec<Proof<Vec<u8>, BlakeDigest>> (commitment/src/merkle_tree.rs:14-18).
@@ -214,6 +215,32 @@ void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t le
       json_bytes(o, nodes.data() + (i * depth + d) * 32, 32);
     }
     o += "]}";
+  }
+  o.push_back(']');
+}
+
+// serde_json of Vec<FriProof<BlakeDigest>> (fri.rs:16-26), appended to o.
+void fri_proof_json_string(const stark_fri_proof* proof, std::string& o) {
+  o.push_back('[');
+  for (size_t l = 0; l < proof->layers.size(); ++l) {
+    const stark_fri_layer& L = proof->layers[l];
+    if (l) o.push_back(',');
+    if (L.last) {
+      o += "{\"Last\":{\"last\":[";
+      for (size_t i = 0; i < L.last_values.size() / 32; ++i) {
+        if (i) o.push_back(',');
+        json_bytes(o, L.last_values.data() + 32 * i, 32);
+      }
+      o += "]}}";
+    } else {
+      o += "{\"Middle\":{\"root2\":";
+      json_bytes(o, L.root2, 32);
+      o += ",\"column_branches\":";
+      json_branches(o, L.col_leaves, 32, L.col_nodes, L.col_idx.size(), L.col_depth);
+      o += ",\"poly_branches\":";
+      json_branches(o, L.poly_leaves, 32, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
+      o += "}}";
+    }
   }
   o.push_back(']');
 }
@@ -237,19 +264,11 @@ stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size
   if (!ctx || !root || !out || (n && !values)) return STARK_ERR_BAD_ARG;
   *out = nullptr;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
-  DevBuf buf;
-  stark_status st = ensure_buf(ctx, buf, (n ? n : 1) * sizeof(fe));
+  stark_status st = ensure_buf(ctx, ctx->io, (n ? n : 1) * sizeof(fe));
   if (st != STARK_OK) return st;
-  if (n) {
-    hipError_t e = hipMemcpyAsync(buf.ptr, values, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream);
-    if (e != hipSuccess) {
-      hipFree(buf.ptr);
-      return hip_fail(ctx, e, "hipMemcpyAsync");
-    }
-  }
-  st = prove_impl(ctx, (const fe*)buf.ptr, n, root, max_deg_plus_1, exclude_multiples_of, out);
+  if (n) STARK_HIP(ctx, hipMemcpyAsync(ctx->io.ptr, values, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  st = prove_impl(ctx, (const fe*)ctx->io.ptr, n, root, max_deg_plus_1, exclude_multiples_of, out);
   hipStreamSynchronize(ctx->stream);
-  hipFree(buf.ptr);
   return st;
 }
 
@@ -257,28 +276,8 @@ void stark_fri_proof_free(stark_fri_proof* proof) { delete proof; }
 
 stark_status stark_fri_proof_json(const stark_fri_proof* proof, char* buf, size_t cap, size_t* len) {
   if (!proof || !len) return STARK_ERR_BAD_ARG;
-  std::string o = "[";
-  for (size_t l = 0; l < proof->layers.size(); ++l) {
-    const stark_fri_layer& L = proof->layers[l];
-    if (l) o.push_back(',');
-    if (L.last) {
-      o += "{\"Last\":{\"last\":[";
-      for (size_t i = 0; i < L.last_values.size() / 32; ++i) {
-        if (i) o.push_back(',');
-        json_bytes(o, L.last_values.data() + 32 * i, 32);
-      }
-      o += "]}}";
-    } else {
-      o += "{\"Middle\":{\"root2\":";
-      json_bytes(o, L.root2, 32);
-      o += ",\"column_branches\":";
-      json_branches(o, L.col_leaves, 32, L.col_nodes, L.col_idx.size(), L.col_depth);
-      o += ",\"poly_branches\":";
-      json_branches(o, L.poly_leaves, 32, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
-      o += "}}";
-    }
-  }
-  o.push_back(']');
+  std::string o;
+  fri_proof_json_string(proof, o);
   *len = o.size();
   if (buf && cap) {
     const size_t k = o.size() < cap ? o.size() : cap;

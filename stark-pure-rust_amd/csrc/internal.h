@@ -48,6 +48,11 @@ struct stark_ctx {
   stark::DevBuf scratch;   // NTT ping-pong partner
   stark::DevBuf io;        // staging for host-buffer entry points
   stark::DevBuf io2;
+  stark::DevBuf fri_cols;    // folded FRI columns (prove_low_degree)
+  stark::DevBuf r1cs_arena;  // mk_r1cs_proof working set
+  // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
+  // accumulator, main and linear-combination trees of mk_r1cs_proof.
+  stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
 };
@@ -62,6 +67,8 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
   } while (0)
 
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
+// Context-owned Merkle tree slot (created on first use).
+stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out);
 hipStream_t pick_stream(stark_ctx* ctx, void* stream);
 
 // Returns tables for `root` (canonical limbs) of order exactly 2^log_n, or

@@ -38,6 +38,7 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
 void json_bytes(std::string& o, const uint8_t* p, size_t n);
 void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
                    const std::vector<uint8_t>& nodes, size_t k, size_t depth);
+void fri_proof_json_string(const stark_fri_proof* proof, std::string& o);
 }  // namespace stark
 
 struct stark_r1cs_proof {
@@ -380,22 +381,20 @@ static std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const 
   return b;
 }
 
-// Owned device allocations of one proof.
-struct Arena {
-  std::vector<void*> ptrs;
-  ~Arena() {
-    for (void* p : ptrs) hipFree(p);
-  }
+// Carves the proof's buffers out of the context's grow-only arena (no
+// hipMalloc/hipFree per proof).
+struct Carve {
+  size_t off = 0;
+  std::vector<std::pair<void**, size_t>> req;
   template <class T>
-  stark_status get(stark_ctx* ctx, size_t count, T** out) {
-    void* p = nullptr;
-    const hipError_t e = hipMalloc(&p, (count ? count : 1) * sizeof(T));
-    if (e != hipSuccess) {
-      ctx->last_error = std::string("hipMalloc: ") + hipGetErrorString(e);
-      return STARK_ERR_OOM;
-    }
-    ptrs.push_back(p);
-    *out = (T*)p;
+  void add(T** p, size_t count) {
+    req.push_back({(void**)p, off});
+    off += ((count ? count : 1) * sizeof(T) + 255) & ~(size_t)255;
+  }
+  stark_status commit(stark_ctx* ctx, DevBuf& arena) {
+    stark_status st = ensure_buf(ctx, arena, off);
+    if (st != STARK_OK) return st;
+    for (auto& r : req) *r.first = (uint8_t*)arena.ptr + r.second;
     return STARK_OK;
   }
 };
@@ -430,11 +429,6 @@ static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint3
   STARK_HIP(ctx, hipGetLastError());
   return ntt_device(ctx, out, log_prec, batch, tw_g2, false, s);
 }
-
-struct TreeGuard {
-  stark_merkle_tree* t = nullptr;
-  ~TreeGuard() { stark_merkle_free(t); }
-};
 
 static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                size_t os, const uint64_t* public_wires, size_t n_public,
@@ -474,28 +468,29 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
   const Mont mc = mont();
 
-  Arena ar;
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
   uint64_t* perm;
   uint64_t* acc_leaves;
   int* d_err;
   const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
-  STARK_TRY(ar.get(ctx, 8 * steps, &raw));  // K F0 F1 F2 S P IDX PIDX (then A's slot reuses K's)
-  STARK_TRY(ar.get(ctx, steps, &wcopy));
-  STARK_TRY(ar.get(ctx, steps, &perm));
-  STARK_TRY(ar.get(ctx, 5 * steps, &acc_leaves));
-  STARK_TRY(ar.get(ctx, 9 * prec, &cols));
-  STARK_TRY(ar.get(ctx, steps, &nmr));
-  STARK_TRY(ar.get(ctx, steps, &dnm));
-  STARK_TRY(ar.get(ctx, 2 * (size_t)nb, &tot));
-  STARK_TRY(ar.get(ctx, steps, &dnm_c));
-  STARK_TRY(ar.get(ctx, steps, &inv_dnm));
-  STARK_TRY(ar.get(ctx, 2 * prec, &zb));
-  STARK_TRY(ar.get(ctx, 2 * prec, &inv_zb));
-  STARK_TRY(ar.get(ctx, 2 * n_pfi + 2, &consts));
-  STARK_TRY(ar.get(ctx, 8 * prec, &rows));
-  STARK_TRY(ar.get(ctx, prec, &lvals));
-  STARK_TRY(ar.get(ctx, 1, &d_err));
+  Carve cv;
+  cv.add(&raw, 8 * steps);  // K F0 F1 F2 S P IDX PIDX (then A's coefficients reuse K's slot)
+  cv.add(&wcopy, steps);
+  cv.add(&perm, steps);
+  cv.add(&acc_leaves, 5 * steps);
+  cv.add(&cols, 9 * prec);
+  cv.add(&nmr, steps);
+  cv.add(&dnm, steps);
+  cv.add(&tot, 2 * (size_t)nb);
+  cv.add(&dnm_c, steps);
+  cv.add(&inv_dnm, steps);
+  cv.add(&zb, 2 * prec);
+  cv.add(&inv_zb, 2 * prec);
+  cv.add(&consts, 2 * n_pfi + 2);
+  cv.add(&rows, 8 * prec);
+  cv.add(&lvals, prec);
+  cv.add(&d_err, 1);
+  STARK_TRY(cv.commit(ctx, ctx->r1cs_arena));
 
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
@@ -513,14 +508,14 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
 
   auto proof = std::make_unique<stark_r1cs_proof>();
   // Accumulator tree -> a_root (utils.rs:250-270) -> r (utils.rs:272-290).
-  TreeGuard acc_tree, m_tree, l_tree;
-  STARK_TRY(stark_merkle_new(ctx, &acc_tree.t));
-  STARK_TRY(stark_merkle_new(ctx, &m_tree.t));
-  STARK_TRY(stark_merkle_new(ctx, &l_tree.t));
-  STARK_TRY(merkle_build(ctx, acc_tree.t, (const uint8_t*)acc_leaves, steps, 40, s));
+  stark_merkle_tree *acc_tree, *m_tree, *l_tree;
+  STARK_TRY(ctx_tree(ctx, 2, &acc_tree));
+  STARK_TRY(ctx_tree(ctx, 3, &m_tree));
+  STARK_TRY(ctx_tree(ctx, 4, &l_tree));
+  STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
   // The eight LDEs overlap with the host's wait for a_root below.
   STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
-  STARK_TRY(merkle_root_d2h(ctx, acc_tree.t, s, proof->a_root));
+  STARK_TRY(merkle_root_d2h(ctx, acc_tree, s, proof->a_root));
   HostFp r[3];
   {
     uint32_t rnd[24];
@@ -627,8 +622,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
   // Main tree over the 256-B rows (prove.rs:261-264).
-  STARK_TRY(merkle_build(ctx, m_tree.t, (const uint8_t*)rows, prec, 256, s));
-  STARK_TRY(merkle_root_d2h(ctx, m_tree.t, s, proof->m_root));
+  STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s));
+  STARK_TRY(merkle_root_d2h(ctx, m_tree, s, proof->m_root));
   int h_err = 0;
   STARK_HIP(ctx, hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s));
   STARK_HIP(ctx, hipStreamSynchronize(s));
@@ -661,8 +656,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(merkle_build(ctx, l_tree.t, (const uint8_t*)lvals, prec, 32, s));
-  STARK_TRY(merkle_root_d2h(ctx, l_tree.t, s, proof->l_root));
+  STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s));
+  STARK_TRY(merkle_root_d2h(ctx, l_tree, s, proof->l_root));
 
   // Spot checks (prove.rs:337-362).
   uint32_t pos32[kSpotChecks];
@@ -678,22 +673,16 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   std::vector<uint8_t> l_leaves(32 * kSpotChecks), l_nodes(32 * kSpotChecks * log_prec);
   std::vector<uint8_t> m_leaves(256 * 4 * kSpotChecks), m_nodes(32 * 4 * kSpotChecks * log_prec);
-  STARK_TRY(merkle_gather(ctx, l_tree.t, positions.data(), kSpotChecks, l_leaves.data(), l_nodes.data(), s));
-  STARK_TRY(merkle_gather(ctx, m_tree.t, aug.data(), 4 * kSpotChecks, m_leaves.data(), m_nodes.data(), s));
+  STARK_TRY(merkle_gather(ctx, l_tree, positions.data(), kSpotChecks, l_leaves.data(), l_nodes.data(), s));
+  STARK_TRY(merkle_gather(ctx, m_tree, aug.data(), 4 * kSpotChecks, m_leaves.data(), m_nodes.data(), s));
 
   // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367).
   stark_fri_proof* fri = nullptr;
   STARK_TRY(stark_prove_low_degree_dev(ctx, (const uint64_t*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri));
-  size_t fri_len = 0;
-  stark_status st = stark_fri_proof_json(fri, nullptr, 0, &fri_len);
-  std::string fri_json(fri_len, '\0');
-  if (st == STARK_OK) st = stark_fri_proof_json(fri, &fri_json[0], fri_len, &fri_len);
-  stark_fri_proof_free(fri);
-  if (st != STARK_OK) return st;
-
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
   std::string& o = proof->json;
-  o.reserve(fri_len + 4 * kSpotChecks * (256 * 4 + log_prec * 32 * 4) + kSpotChecks * (log_prec + 1) * 32 * 4);
+  o.reserve((size_t)4 * kSpotChecks * (256 + log_prec * 32) * 4 + (size_t)kSpotChecks * (log_prec + 1) * 32 * 4 +
+            ((size_t)3 << 20));
   o += "{\"m_root\":";
   json_bytes(o, proof->m_root, 32);
   o += ",\"l_root\":";
@@ -705,7 +694,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   o += ",\"linear_comb_branches\":";
   json_branches(o, l_leaves, 32, l_nodes, kSpotChecks, log_prec);
   o += ",\"fri_proof\":";
-  o += fri_json;
+  fri_proof_json_string(fri, o);
+  stark_fri_proof_free(fri);
   o += "}";
   *out = proof.release();
   return STARK_OK;

@@ -141,9 +141,17 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   t->n_wires = n_wires;
   const size_t n_public = 1 + (size_t)n_pub_in + n_pub_out;  // run.rs:359-360
   if (n_public > n_wit) return STARK_ERR_BAD_ARG;
-  for (size_t i = 0; i < n_public; ++i) push_canon(t->public_wires, witness[i]);
+  for (size_t i = 0; i < n_public; ++i) push_canon(t->public_wires, witness[i]);  // run.rs:359-360
 
   // ---- calc_coefficients_and_witness (run.rs:109-281)
+  // Canonical arithmetic: montmul(c_canonical, w_montgomery) = c * w canonical,
+  // so each slot costs one modular product and no conversions.
+  std::vector<HostFp> wcan(n_wit);
+  for (uint32_t i = 0; i < n_wit; ++i) {
+    uint64_t cc[4];
+    F.to_canonical(witness[i], cc);
+    memcpy(wcan[i].v, cc, 32);
+  }
   std::vector<HostFp> wit_l[3], tr_l[3], co_l[3];
   std::vector<std::vector<std::pair<uint8_t, size_t>>> wire_using(n_wires);
   std::vector<size_t> last_coeff;
@@ -160,13 +168,13 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
         HostFp coef = F.zero();
         if (i < fac[f].size()) {
           wire = fac[f][i].wire_id;
-          coef = F.from_bytes_le(fac[f][i].value, 32);
+          coef = F.reduce_bytes_le(fac[f][i].value, 32);  // canonical from_bytes_le
           tacc = F.add(tacc, F.mul(coef, witness[wire]));
         } else {
           wire = n_wires - 1;  // padding slot uses the last wire with coefficient 0
         }
         wire_using[wire].push_back({(uint8_t)f, co_l[f].size()});
-        wit_l[f].push_back(witness[wire]);
+        wit_l[f].push_back(wcan[wire]);
         co_l[f].push_back(coef);
         tr_l[f].push_back(tacc);
       }
@@ -177,11 +185,14 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   const size_t a_len = co_l[0].size();
   const size_t os = 3 * a_len;
   if (a_len == 0) return STARK_ERR_BAD_ARG;
+  t->witness_trace.reserve(4 * os);
+  t->computational_trace.reserve(4 * os);
+  t->coefficients.reserve(4 * os);
   for (int f = 0; f < 3; ++f)
     for (size_t i = 0; i < a_len; ++i) {
-      push_canon(t->witness_trace, wit_l[f][i]);
-      push_canon(t->computational_trace, tr_l[f][i]);
-      push_canon(t->coefficients, co_l[f][i]);
+      t->witness_trace.insert(t->witness_trace.end(), wit_l[f][i].v, wit_l[f][i].v + 4);
+      t->computational_trace.insert(t->computational_trace.end(), tr_l[f][i].v, tr_l[f][i].v + 4);
+      t->coefficients.insert(t->coefficients.end(), co_l[f][i].v, co_l[f][i].v + 4);
     }
   // ---- calc_flags (run.rs:283-308)
   std::vector<uint8_t> f1(os, 1), f2(os, 0);
