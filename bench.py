@@ -66,6 +66,38 @@ def timed_events(fn, stream, reps):
     return start.elapsed_time(end) / reps
 
 
+def end_to_end(ctx):
+    """prove_with_witness wall-clock on the reference's pedersen_test fixture and on a
+    synthetic 2^20-step circuit (stand-in for sha256_2_test, whose .r1cs is not shipped)."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth_r1cs
+    from stark_amd.r1cs import prove_with_witness
+    fix = os.path.join(ROOT, "tests", "golden", "r1cs")
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
+    out = {}
+    r1 = open(os.path.join(fix, "pedersen_test.r1cs"), "rb").read()
+    wt = open(os.path.join(fix, "pedersen_test.wtns"), "rb").read()
+    js = prove_with_witness(ctx, r1, wt).to_json()
+    out["prove_pedersen_bitexact_vs_golden"] = \
+        hashlib.sha256(js.encode()).hexdigest() == golden["pedersen_test"]["json_sha256"]
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        prove_with_witness(ctx, r1, wt).to_json()
+        ts.append(time.perf_counter() - t0)
+    out["prove_pedersen_ms"] = round(min(ts) * 1000.0, 3)
+    rs, ws = synth_r1cs.for_steps(20)
+    prove_with_witness(ctx, rs, ws).to_json()
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        prove_with_witness(ctx, rs, ws).to_json()
+        ts.append(time.perf_counter() - t0)
+    out["prove_synth_2^20_steps_ms"] = round(min(ts) * 1000.0, 3)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -167,6 +199,10 @@ def main():
         proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
         extras["fri_prove_2^23_ms"] = round((time.perf_counter() - t1) * 1000.0, 3)
         extras["fri_layers"] = len(proof)
+        del bf, proof
+        # End-to-end proof wall-clock (config 3: pedersen_test full prove on 1 GPU):
+        # prove_with_witness = .r1cs/.wtns bytes -> trace -> mk_r1cs_proof -> StarkProof JSON.
+        extras.update(end_to_end(ctx))
 
     # Roofline of the dominant kernel, ntt_pass_kernel: one 2^24 transform is
     # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element
@@ -216,6 +252,15 @@ def main():
         cpu = {"value": (1 << lc) / tc, "unit": "field-elems/s", "cores": threads, "kind": "port",
                "sample": f"one 2^{lc}-point best_fft (oracle C restatement of fft.rs parallel_fft, "
                          f"{threads} threads), {tc:.2f} s"}
+
+    if cpu is not None and not args.no_extras:
+        # End-to-end CPU baseline: the oracle's restatement of mk_r1cs_proof on pedersen_test.
+        import r1cs as R
+        tr = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "pedersen_test"))
+        t3 = time.perf_counter()
+        R.mk_r1cs_proof_json(o, tr, cpus=threads)
+        extras["prove_pedersen_cpu_port_ms"] = round((time.perf_counter() - t3) * 1000.0, 1)
+        extras["prove_pedersen_cpu_port_threads"] = threads
 
     if rank == 0:
         line = {"metric": "2^24-pt NTT field-elems/sec", "value": value, "unit": "field-elems/s",
