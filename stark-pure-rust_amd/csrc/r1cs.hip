@@ -105,6 +105,14 @@ __global__ void r1cs_index_kernel(const uint64_t* __restrict__ perm, uint64_t os
   for (int k = 0; k < 4; ++k) leaf[1 + k] = (uint64_t)x.w[2 * k] | ((uint64_t)x.w[2 * k + 1] << 32);
 }
 
+// Flag columns F0, F1, F2 (run.rs:283-308) from bytes: dst[f * steps + i] = fb[f * os + i].
+__global__ void r1cs_flags_kernel(const uint8_t* __restrict__ fb, uint64_t os, uint64_t steps, fe* __restrict__ dst) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 3 * os) return;
+  const uint64_t f = g / os, i = g - f * os;
+  fe_store(dst + f * steps + i, fe_from_u64(fb[g]));
+}
+
 // dst[c][i] = i < steps ? src[c][i] : 0 (best_fft's zero padding, fft.rs:327-357).
 __global__ void r1cs_pad_kernel(const fe* __restrict__ src, fe* __restrict__ dst, uint32_t log_steps,
                                 uint32_t log_prec, uint64_t total) {
@@ -434,7 +442,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                size_t os, const uint64_t* public_wires, size_t n_public,
                                const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
                                const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
-                               const uint64_t* flag2, size_t n_constraints, size_t n_wires, stark_r1cs_proof** out) {
+                               const uint64_t* flag2, const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
+                               stark_r1cs_proof** out) {
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
   // prove.rs:30-53
@@ -495,8 +504,16 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
   for (int c = 0; c < 6; ++c) {
-    STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyHostToDevice, s));
+    if (!(flag_bytes && c >= 1 && c <= 3))
+      STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyHostToDevice, s));
     if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
+  }
+  if (flag_bytes) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
+    uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel
+    STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
+                       (uint64_t)os, steps, raw + steps);
+    STARK_HIP(ctx, hipGetLastError());
   }
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyHostToDevice, s));
@@ -701,6 +718,22 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   return STARK_OK;
 }
 
+stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
+                                      const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                      size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                      const size_t* permuted_indices, const uint64_t* coefficients,
+                                      const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
+                                      stark_r1cs_proof** out) {
+  if (!ctx || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const stark_status st = prove_r1cs(ctx, witness_trace, computational_trace, os, public_wires, n_public,
+                                     public_first_indices, n_pfi, permuted_indices, coefficients, nullptr, nullptr,
+                                     nullptr, flag_bytes, n_constraints, n_wires, out);
+  hipStreamSynchronize(ctx->stream);
+  return st;
+}
+
 }  // namespace stark
 
 using namespace stark;
@@ -722,7 +755,7 @@ stark_status stark_mk_r1cs_proof(stark_ctx* ctx, const uint64_t* witness_trace, 
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   const stark_status st = prove_r1cs(ctx, witness_trace, computational_trace, original_steps, public_wires, n_public,
                                      public_first_indices, n_public_first, permuted_indices, coefficients, flag0,
-                                     flag1, flag2, n_constraints, n_wires, out);
+                                     flag1, flag2, nullptr, n_constraints, n_wires, out);
   hipStreamSynchronize(ctx->stream);
   return st;
 }

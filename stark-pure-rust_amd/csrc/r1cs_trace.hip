@@ -11,17 +11,42 @@
 // this returns STARK_ERR_BAD_ARG instead.
 #include <string.h>
 
+#include <memory>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
 
+// Uninitialised u64 array (every element is written by the builder).
+struct U64Array {
+  std::unique_ptr<uint64_t[]> p;
+  size_t n = 0;
+  void alloc(size_t count) {
+    p.reset(new uint64_t[count ? count : 1]);
+    n = count;
+  }
+  uint64_t* data() const { return p.get(); }
+  uint64_t& operator[](size_t i) { return p[i]; }
+  size_t size() const { return n; }
+};
+
 struct stark_r1cs_trace {
   size_t n_constraints = 0, n_wires = 0;
-  std::vector<uint64_t> witness_trace, computational_trace, coefficients, flag0, flag1, flag2;  // 4 limbs each
-  std::vector<size_t> permuted_indices;
+  U64Array witness_trace, computational_trace, coefficients;  // 4 limbs per element
+  std::vector<uint8_t> flags;                                // flag0 | flag1 | flag2, one byte per slot
+  U64Array permuted_indices;
   std::vector<uint64_t> public_wires;
   std::vector<size_t> public_first_indices;  // (k, w) pairs
 };
+
+namespace stark {
+stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
+                                      const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                      size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                      const size_t* permuted_indices, const uint64_t* coefficients,
+                                      const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
+                                      stark_r1cs_proof** out);
+}
 
 namespace stark {
 namespace {
@@ -104,19 +129,21 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   if (!c.ok || memcmp(prime, kBn254R, 32) != 0) return STARK_ERR_BAD_ARG;  // run.rs:344-350
   if (c.u32() != 2) return STARK_ERR_BAD_ARG;                               // ConstraintSection
   c.u64();
-  std::vector<std::vector<Coefficient>> factors;  // 3 per constraint
-  factors.reserve((size_t)3 * n_constraints);
+  std::vector<Coefficient> coefs;                 // all coefficients, in file order
+  coefs.reserve(r1cs_len / 36);
+  std::vector<uint64_t> fac_off((size_t)3 * n_constraints + 1, 0);  // factor k = coefs[fac_off[k], fac_off[k+1])
   for (uint32_t i = 0; i < n_constraints && c.ok; ++i)
     for (int f = 0; f < 3; ++f) {
       const uint32_t nc = c.u32();
       if (nc > c.left / 36) return STARK_ERR_BAD_ARG;
-      std::vector<Coefficient> v(nc);
       for (uint32_t k = 0; k < nc; ++k) {
-        v[k].wire_id = c.u32();
-        v[k].value = c.raw(32);
-        if (v[k].wire_id >= n_wires) return STARK_ERR_BAD_ARG;
+        Coefficient cf;
+        cf.wire_id = c.u32();
+        cf.value = c.raw(32);
+        if (cf.wire_id >= n_wires) return STARK_ERR_BAD_ARG;
+        coefs.push_back(cf);
       }
-      factors.push_back(std::move(v));
+      fac_off[(size_t)3 * i + f + 1] = coefs.size();
     }
   if (!c.ok || n_wires == 0) return STARK_ERR_BAD_ARG;
 
@@ -144,6 +171,20 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   for (size_t i = 0; i < n_public; ++i) push_canon(t->public_wires, witness[i]);  // run.rs:359-360
 
   // ---- calc_coefficients_and_witness (run.rs:109-281)
+  // Constraint ci owns n_coeff = max(|A|, |B|, |C|) slots starting at base[ci]
+  // in each of the three factor thirds of the trace.
+  std::vector<uint64_t> base((size_t)n_constraints + 1, 0);
+  for (uint32_t ci = 0; ci < n_constraints; ++ci) {
+    uint64_t n_coeff = 0;
+    for (int f = 0; f < 3; ++f) {
+      const uint64_t k = fac_off[(size_t)3 * ci + f + 1] - fac_off[(size_t)3 * ci + f];
+      if (k > n_coeff) n_coeff = k;
+    }
+    base[ci + 1] = base[ci] + n_coeff;
+  }
+  const size_t a_len = base[n_constraints];
+  const size_t os = 3 * a_len;
+  if (a_len == 0) return STARK_ERR_BAD_ARG;
   // Canonical arithmetic: montmul(c_canonical, w_montgomery) = c * w canonical,
   // so each slot costs one modular product and no conversions.
   std::vector<HostFp> wcan(n_wit);
@@ -152,79 +193,88 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
     F.to_canonical(witness[i], cc);
     memcpy(wcan[i].v, cc, 32);
   }
-  std::vector<HostFp> wit_l[3], tr_l[3], co_l[3];
-  std::vector<std::vector<std::pair<uint8_t, size_t>>> wire_using(n_wires);
-  std::vector<size_t> last_coeff;
-  size_t acc_n = 0;
-  for (uint32_t ci = 0; ci < n_constraints; ++ci) {
-    const std::vector<Coefficient>* fac = &factors[(size_t)3 * ci];
-    size_t n_coeff = fac[0].size();
-    if (fac[1].size() > n_coeff) n_coeff = fac[1].size();
-    if (fac[2].size() > n_coeff) n_coeff = fac[2].size();
-    for (int f = 0; f < 3; ++f) {
-      HostFp tacc = F.zero();
-      for (size_t i = 0; i < n_coeff; ++i) {
-        size_t wire;
-        HostFp coef = F.zero();
-        if (i < fac[f].size()) {
-          wire = fac[f][i].wire_id;
-          coef = F.reduce_bytes_le(fac[f][i].value, 32);  // canonical from_bytes_le
-          tacc = F.add(tacc, F.mul(coef, witness[wire]));
-        } else {
-          wire = n_wires - 1;  // padding slot uses the last wire with coefficient 0
+  t->witness_trace.alloc(4 * os);
+  t->computational_trace.alloc(4 * os);
+  t->coefficients.alloc(4 * os);
+  // Slot filling is independent per constraint: split the constraints over threads.
+  auto fill = [&](uint32_t c0, uint32_t c1) {
+    for (uint32_t ci = c0; ci < c1; ++ci) {
+      const uint64_t n_coeff = base[ci + 1] - base[ci];
+      for (int f = 0; f < 3; ++f) {
+        const uint64_t lo = fac_off[(size_t)3 * ci + f], hi = fac_off[(size_t)3 * ci + f + 1];
+        HostFp tacc = F.zero();
+        for (uint64_t i = 0; i < n_coeff; ++i) {
+          const size_t slot = (size_t)f * a_len + base[ci] + i;
+          size_t wire = n_wires - 1;  // padding slot: last wire, coefficient 0, trace unchanged
+          HostFp coef = F.zero();
+          if (lo + i < hi) {
+            wire = coefs[lo + i].wire_id;
+            coef = F.reduce_bytes_le(coefs[lo + i].value, 32);  // canonical from_bytes_le
+            tacc = F.add(tacc, F.mul(coef, witness[wire]));
+          }
+          memcpy(&t->witness_trace[4 * slot], wcan[wire].v, 32);
+          memcpy(&t->computational_trace[4 * slot], tacc.v, 32);
+          memcpy(&t->coefficients[4 * slot], coef.v, 32);
         }
-        wire_using[wire].push_back({(uint8_t)f, co_l[f].size()});
-        wit_l[f].push_back(wcan[wire]);
-        co_l[f].push_back(coef);
-        tr_l[f].push_back(tacc);
       }
     }
-    acc_n += n_coeff;
-    last_coeff.push_back(acc_n - 1);
+  };
+  {
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
+    if (os < (1u << 16)) nt = 1;
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < nt; ++k)
+      th.emplace_back(fill, (uint32_t)((uint64_t)n_constraints * k / nt), (uint32_t)((uint64_t)n_constraints * (k + 1) / nt));
+    fill(0, (uint32_t)((uint64_t)n_constraints / nt));
+    for (auto& x : th) x.join();
   }
-  const size_t a_len = co_l[0].size();
-  const size_t os = 3 * a_len;
-  if (a_len == 0) return STARK_ERR_BAD_ARG;
-  t->witness_trace.reserve(4 * os);
-  t->computational_trace.reserve(4 * os);
-  t->coefficients.reserve(4 * os);
-  for (int f = 0; f < 3; ++f)
-    for (size_t i = 0; i < a_len; ++i) {
-      t->witness_trace.insert(t->witness_trace.end(), wit_l[f][i].v, wit_l[f][i].v + 4);
-      t->computational_trace.insert(t->computational_trace.end(), tr_l[f][i].v, tr_l[f][i].v + 4);
-      t->coefficients.insert(t->coefficients.end(), co_l[f][i].v, co_l[f][i].v + 4);
-    }
-  // ---- calc_flags (run.rs:283-308)
-  std::vector<uint8_t> f1(os, 1), f2(os, 0);
-  for (size_t v : last_coeff) {
-    const size_t k = (v + 1) % a_len;
+  // ---- calc_flags (run.rs:283-308): flag0 = 1, flag1 = 0 at each constraint's
+  // first slot (in all three thirds), flag2 = 1 at its last slot.
+  t->flags.assign(3 * os, 0);
+  uint8_t* f0 = t->flags.data();
+  uint8_t* f1 = f0 + os;
+  uint8_t* f2 = f1 + os;
+  memset(f0, 1, os);
+  memset(f1, 1, os);
+  for (uint32_t ci = 0; ci < n_constraints; ++ci) {
+    const size_t k = base[ci + 1] % a_len;  // (last_coeff + 1) % a_trace_len
     f1[k] = f1[k + a_len] = f1[k + 2 * a_len] = 0;
   }
-  for (size_t k : last_coeff) f2[k] = 1;
-  t->flag0.assign(4 * os, 0);
-  t->flag1.assign(4 * os, 0);
-  t->flag2.assign(4 * os, 0);
-  for (size_t i = 0; i < os; ++i) {
-    t->flag0[4 * i] = 1;
-    t->flag1[4 * i] = f1[i];
-    t->flag2[4 * i] = f2[i];
-  }
+  for (uint32_t ci = 0; ci < n_constraints; ++ci) f2[base[ci + 1] - 1] = 1;
+  // ---- wire uses in push order (run.rs:160, 195, 230: factor A's slots, then B's, then C's per
+  // constraint), as trace positions a_len * factor + slot; counting sort by wire.
+  std::vector<uint64_t> use_off((size_t)n_wires + 1, 0);
+  auto for_each_use = [&](auto&& fn) {
+    for (uint32_t ci = 0; ci < n_constraints; ++ci) {
+      const uint64_t n_coeff = base[ci + 1] - base[ci];
+      for (int f = 0; f < 3; ++f) {
+        const uint64_t lo = fac_off[(size_t)3 * ci + f], hi = fac_off[(size_t)3 * ci + f + 1];
+        for (uint64_t i = 0; i < n_coeff; ++i)
+          fn(lo + i < hi ? coefs[lo + i].wire_id : n_wires - 1, (size_t)f * a_len + base[ci] + i);
+      }
+    }
+  };
+  for_each_use([&](size_t wire, size_t) { ++use_off[wire + 1]; });
+  for (size_t wi = 0; wi < n_wires; ++wi) use_off[wi + 1] += use_off[wi];
+  std::vector<uint64_t> uses(os), cur(use_off.begin(), use_off.end() - 1);
+  for_each_use([&](size_t wire, size_t pos) { uses[cur[wire]++] = pos; });
   // ---- permuted indices (run.rs:388-401): a cycle through every wire's uses.
-  t->permuted_indices.assign(os, 0);
-  for (const auto& vs : wire_using) {
-    if (vs.empty()) continue;
-    size_t old_w = a_len * vs.back().first + vs.back().second;
-    for (const auto& kv : vs) {
-      const size_t wpos = a_len * kv.first + kv.second;
-      t->permuted_indices[wpos] = old_w;
-      old_w = wpos;
+  t->permuted_indices.alloc(os);
+  for (size_t wi = 0; wi < n_wires; ++wi) {
+    const uint64_t lo = use_off[wi], hi = use_off[wi + 1];
+    if (lo == hi) continue;
+    uint64_t old_w = uses[hi - 1];
+    for (uint64_t j = lo; j < hi; ++j) {
+      t->permuted_indices[uses[j]] = old_w;
+      old_w = uses[j];
     }
   }
   // ---- public_first_indices (run.rs:411-419)
   for (size_t wi = 0; wi < n_public && wi < n_wires; ++wi)
-    if (!wire_using[wi].empty()) {
+    if (use_off[wi] != use_off[wi + 1]) {
       t->public_first_indices.push_back(wi);
-      t->public_first_indices.push_back(a_len * wire_using[wi][0].first + wire_using[wi][0].second);
+      t->public_first_indices.push_back(uses[use_off[wi]]);
     }
   *out = t.release();
   return STARK_OK;
@@ -251,9 +301,14 @@ stark_status stark_r1cs_trace_export(const stark_r1cs_trace* t, uint64_t* witnes
   cp(witness_trace, t->witness_trace.data(), t->witness_trace.size() * 8);
   cp(computational_trace, t->computational_trace.data(), t->computational_trace.size() * 8);
   cp(coefficients, t->coefficients.data(), t->coefficients.size() * 8);
-  cp(flag0, t->flag0.data(), t->flag0.size() * 8);
-  cp(flag1, t->flag1.data(), t->flag1.size() * 8);
-  cp(flag2, t->flag2.data(), t->flag2.size() * 8);
+  const size_t os = t->coefficients.size() / 4;
+  uint64_t* fl[3] = {flag0, flag1, flag2};
+  for (int f = 0; f < 3; ++f)
+    if (fl[f])
+      for (size_t i = 0; i < os; ++i) {
+        fl[f][4 * i] = t->flags[f * os + i];
+        fl[f][4 * i + 1] = fl[f][4 * i + 2] = fl[f][4 * i + 3] = 0;
+      }
   cp(permuted_indices, t->permuted_indices.data(), t->permuted_indices.size() * sizeof(size_t));
   cp(public_wires, t->public_wires.data(), t->public_wires.size() * 8);
   cp(public_first_indices, t->public_first_indices.data(), t->public_first_indices.size() * sizeof(size_t));
@@ -264,10 +319,11 @@ void stark_r1cs_trace_free(stark_r1cs_trace* t) { delete t; }
 
 stark_status stark_prove_r1cs_trace(stark_ctx* ctx, const stark_r1cs_trace* t, stark_r1cs_proof** out) {
   if (!t) return STARK_ERR_BAD_ARG;
-  return stark_mk_r1cs_proof(ctx, t->witness_trace.data(), t->computational_trace.data(), t->coefficients.size() / 4,
-                             t->public_wires.data(), t->public_wires.size() / 4, t->public_first_indices.data(),
-                             t->public_first_indices.size() / 2, t->permuted_indices.data(), t->coefficients.data(),
-                             t->flag0.data(), t->flag1.data(), t->flag2.data(), t->n_constraints, t->n_wires, out);
+  return mk_r1cs_proof_bytes_flags(ctx, t->witness_trace.data(), t->computational_trace.data(),
+                                   t->coefficients.size() / 4, t->public_wires.data(), t->public_wires.size() / 4,
+                                   t->public_first_indices.data(), t->public_first_indices.size() / 2,
+                                   (const size_t*)t->permuted_indices.data(), t->coefficients.data(),
+                                   t->flags.data(), t->n_constraints, t->n_wires, out);
 }
 
 }  // extern "C"
