@@ -136,52 +136,119 @@ __device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
   return r;
 }
 
-// acc(64) + carry word c += a * b: one v_mad_u64_u32 whose carry-out is
-// counted into c by v_addc_co_u32 (gfx950: ~5 + ~2 cycles per wave64).
-__device__ __forceinline__ void fe_mac(uint64_t& acc, uint32_t& c, uint32_t a, uint32_t b) {
-  uint64_t cy;
-  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
-      "v_addc_co_u32 %2, %1, %2, 0, %1"
-      : "+v"(acc), "=&s"(cy), "+v"(c)
-      : "v"(a), "v"(b));
-}
+// The Montgomery product as one inline-asm block (fe_mul_lazy, generated by
+// tools/gen_fe_mul_asm.py): FIPS product scanning, 64 a*b + 64 m*p word
+// products, each one v_mad_u64_u32 into a 96-bit column accumulator whose
+// carry-outs v_addc_co_u32 counts.  One block instead of one per product
+// removes hipcc's boundary wait state after every block.
+#include "fe_mul_asm.inc"
 
-// Montgomery product a*b*2^-256 mod p, product scanning with the reduction
-// interleaved per column (FIPS order): 64 a*b + 64 m*p word products, each a
-// single mad_u64_u32 into a 96-bit column accumulator; no partial-product
-// arrays, no carry-propagation chains.  Inputs < p, output < p.
+// Montgomery product, canonical result: inputs < p (or a < 4p, b < p).
 __device__ __forceinline__ fe fe_mul(const fe& a, const fe& b) {
-  uint32_t m[8];
-  fe r;
-  uint64_t acc = 0;
-  uint32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-#pragma unroll
-    for (int j = 0; j < k; ++j) {
-      fe_mac(acc, c, a.w[j], b.w[k - j]);
-      fe_mac(acc, c, m[j], p_limb(k - j));
-    }
-    fe_mac(acc, c, a.w[k], b.w[0]);
-    m[k] = (uint32_t)acc * STARK_PINV32;
-    fe_mac(acc, c, m[k], STARK_P0);  // clears the low word
-    acc = (acc >> 32) | ((uint64_t)c << 32);
-    c = 0;
-  }
-#pragma unroll
-  for (int k = 8; k < 15; ++k) {
-#pragma unroll
-    for (int j = k - 7; j < 8; ++j) {
-      fe_mac(acc, c, a.w[j], b.w[k - j]);
-      fe_mac(acc, c, m[j], p_limb(k - j));
-    }
-    r.w[k - 8] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)c << 32);
-    c = 0;
-  }
-  r.w[7] = (uint32_t)acc;  // result < 2p < 2^255
+  fe r = fe_mul_lazy(a, b);
   fe_reduce_once(r);
   return r;
+}
+
+// ---- lazy ("Harvey") representation: values in [0, 4p) -------------------
+// 4p < 2^256 < 5p for BN254 r, so sums of two values below 2p never carry
+// out of limb 7.  The NTT butterflies keep data in [0, 4p) and only the last
+// pass reduces to canonical.
+#define STARK_2P0 0xe0000002u
+#define STARK_2P1 0x87c3eb27u
+#define STARK_2P2 0xf372e122u
+#define STARK_2P3 0x5067d090u
+#define STARK_2P4 0x0302b0bau
+#define STARK_2P5 0x70a08b6du
+#define STARK_2P6 0xc2634053u
+#define STARK_2P7 0x60c89ce5u
+
+struct P2Limbs {
+  uint32_t l[8];
+};
+__device__ __forceinline__ P2Limbs p2_vgprs() {
+  P2Limbs q;
+  q.l[0] = STARK_2P0; q.l[1] = STARK_2P1; q.l[2] = STARK_2P2; q.l[3] = STARK_2P3;
+  q.l[4] = STARK_2P4; q.l[5] = STARK_2P5; q.l[6] = STARK_2P6; q.l[7] = STARK_2P7;
+  return q;
+}
+
+// x <- x - 2p if x >= 2p (x < 4p on entry, < 2p on exit).
+__device__ __forceinline__ void fe_csub2p(fe& t) {
+  const P2Limbs q = p2_vgprs();
+  uint32_t d0, d1, d2, d3, d4, d5, d6, d7;
+  asm("v_sub_co_u32 %8, vcc, %0, %16\n\t"
+      "v_subb_co_u32 %9, vcc, %1, %17, vcc\n\t"
+      "v_subb_co_u32 %10, vcc, %2, %18, vcc\n\t"
+      "v_subb_co_u32 %11, vcc, %3, %19, vcc\n\t"
+      "v_subb_co_u32 %12, vcc, %4, %20, vcc\n\t"
+      "v_subb_co_u32 %13, vcc, %5, %21, vcc\n\t"
+      "v_subb_co_u32 %14, vcc, %6, %22, vcc\n\t"
+      "v_subb_co_u32 %15, vcc, %7, %23, vcc\n\t"
+      "v_cndmask_b32 %0, %8, %0, vcc\n\t"
+      "v_cndmask_b32 %1, %9, %1, vcc\n\t"
+      "v_cndmask_b32 %2, %10, %2, vcc\n\t"
+      "v_cndmask_b32 %3, %11, %3, vcc\n\t"
+      "v_cndmask_b32 %4, %12, %4, vcc\n\t"
+      "v_cndmask_b32 %5, %13, %5, vcc\n\t"
+      "v_cndmask_b32 %6, %14, %6, vcc\n\t"
+      "v_cndmask_b32 %7, %15, %7, vcc"
+      : "+v"(t.w[0]), "+v"(t.w[1]), "+v"(t.w[2]), "+v"(t.w[3]), "+v"(t.w[4]), "+v"(t.w[5]), "+v"(t.w[6]),
+        "+v"(t.w[7]), "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "=&v"(d4), "=&v"(d5), "=&v"(d6), "=&v"(d7)
+      : "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7])
+      : "vcc");
+}
+
+// Radix-2 butterfly in the lazy representation (Harvey):
+//   X in [0, 4p), T in [0, 2p)  ->  X' = X mod 2p in [0, 2p),
+//   x <- X' + T in [0, 4p),  y <- X' - T + 2p in (0, 4p).
+__device__ __forceinline__ void fe_bfly_lazy(fe& x, fe& y, const fe& t) {
+  fe_csub2p(x);
+  const P2Limbs q = p2_vgprs();
+  fe s = x;
+  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
+      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
+      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
+      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
+      "v_addc_co_u32 %7, vcc, %7, %15, vcc"
+      : "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]), "+v"(s.w[3]), "+v"(s.w[4]), "+v"(s.w[5]), "+v"(s.w[6]),
+        "+v"(s.w[7])
+      : "v"(t.w[0]), "v"(t.w[1]), "v"(t.w[2]), "v"(t.w[3]), "v"(t.w[4]), "v"(t.w[5]), "v"(t.w[6]), "v"(t.w[7])
+      : "vcc");
+  // y = (X' + 2p) - T: X' + 2p < 4p < 2^256, and >= T, so neither chain carries out.
+  fe d = x;
+  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
+      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
+      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
+      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
+      "v_addc_co_u32 %7, vcc, %7, %15, vcc\n\t"
+      "v_sub_co_u32 %0, vcc, %0, %16\n\t"
+      "v_subb_co_u32 %1, vcc, %1, %17, vcc\n\t"
+      "v_subb_co_u32 %2, vcc, %2, %18, vcc\n\t"
+      "v_subb_co_u32 %3, vcc, %3, %19, vcc\n\t"
+      "v_subb_co_u32 %4, vcc, %4, %20, vcc\n\t"
+      "v_subb_co_u32 %5, vcc, %5, %21, vcc\n\t"
+      "v_subb_co_u32 %6, vcc, %6, %22, vcc\n\t"
+      "v_subb_co_u32 %7, vcc, %7, %23, vcc"
+      : "+v"(d.w[0]), "+v"(d.w[1]), "+v"(d.w[2]), "+v"(d.w[3]), "+v"(d.w[4]), "+v"(d.w[5]), "+v"(d.w[6]),
+        "+v"(d.w[7])
+      : "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7]),
+        "v"(t.w[0]), "v"(t.w[1]), "v"(t.w[2]), "v"(t.w[3]), "v"(t.w[4]), "v"(t.w[5]), "v"(t.w[6]), "v"(t.w[7])
+      : "vcc");
+  x = s;
+  y = d;
+}
+
+// [0, 4p) -> canonical [0, p).
+__device__ __forceinline__ void fe_reduce_lazy(fe& t) {
+  fe_csub2p(t);
+  fe_reduce_once(t);
 }
 
 __device__ __forceinline__ fe fe_zero() {

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
           }
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = fe_mul(v[t], tw[t]);
+        for (int t = 0; t < 4; ++t) v[t] = fe_mul_lazy(v[t], tw[t]);  // v < 4p, tw < p -> [0, 2p)
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
     }
 
     // ---- R-point DIT over the bit-reversed image ----
+    // Lazy representation: every value in LDS is in [0, 4p); products are
+    // left in [0, 2p) and each radix-2 butterfly reduces only its X input
+    // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
+    // it is the transform's last pass.
     int s = 0;
     if (LOG_R & 1) {
       if (active) {  // radix-2 stage 0: twiddles are all 1
@@ -121,9 +125,11 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
           const uint32_t g = q * 2 + h;
           fe* xa = &X[((2 * g) << log_b) + b];
           fe* xb = &X[((2 * g + 1) << log_b) + b];
-          const fe a = *xa, c = *xb;
-          *xa = fe_add(a, c);
-          *xb = fe_sub(a, c);
+          fe a = *xa, c = *xb;
+          fe_csub2p(c);
+          fe_bfly_lazy(a, c, c);
+          *xa = a;
+          *xb = c;
         }
       }
       __syncthreads();
@@ -139,28 +145,41 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         fe x1 = X[((base + m) << log_b) + b];
         fe x2 = X[((base + 2 * m) << log_b) + b];
         fe x3 = X[((base + 3 * m) << log_b) + b];
+        fe t1, t3;
         if (s != 0) {
           const fe ta = sm[jj << (LOG_R - 1 - s)];  // w_{2m}^jj
-          x1 = fe_mul(x1, ta);
-          x3 = fe_mul(x3, ta);
+          t1 = fe_mul_lazy(x1, ta);
+          t3 = fe_mul_lazy(x3, ta);
+        } else {
+          t1 = x1;
+          t3 = x3;
+          fe_csub2p(t1);
+          fe_csub2p(t3);
         }
-        const fe y0 = fe_add(x0, x1), y1 = fe_sub(x0, x1);
-        fe y2 = fe_add(x2, x3), y3 = fe_sub(x2, x3);
+        fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
+        fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
         const fe tc = sm[(jj + m) << (LOG_R - 2 - s)];  // w_{4m}^(jj+m)
+        fe t2;
         if (s != 0) {
           const fe tb = sm[jj << (LOG_R - 2 - s)];  // w_{4m}^jj
-          y2 = fe_mul(y2, tb);
+          t2 = fe_mul_lazy(x2, tb);
+        } else {
+          t2 = x2;
+          fe_csub2p(t2);
         }
-        y3 = fe_mul(y3, tc);
-        X[(base << log_b) + b] = fe_add(y0, y2);
-        X[((base + 2 * m) << log_b) + b] = fe_sub(y0, y2);
-        X[((base + m) << log_b) + b] = fe_add(y1, y3);
-        X[((base + 3 * m) << log_b) + b] = fe_sub(y1, y3);
+        t3 = fe_mul_lazy(x3, tc);
+        fe_bfly_lazy(x0, x2, t2);
+        fe_bfly_lazy(x1, x3, t3);
+        X[(base << log_b) + b] = x0;
+        X[((base + 2 * m) << log_b) + b] = x2;
+        X[((base + m) << log_b) + b] = x1;
+        X[((base + 3 * m) << log_b) + b] = x3;
       }
       __syncthreads();
     }
 
     // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
+    const bool last = log_ns + LOG_R == log_n;  // the transform's last pass stores canonical values
     if (active) {
       fe* dst = out + boff;
       if (((size_t)1 << log_ns) >= B) {
@@ -169,6 +188,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
           const size_t j = j0 + eb[t];
           const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
           fe val = X[(er[t] << log_b) + eb[t]];
+          if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
           fe_store(dst + o, val);
         }
@@ -182,6 +202,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
           const uint32_t r = rem >> log_ns;
           const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
           fe val = X[(r << log_b) + bb];
+          if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
           fe_store(dst + (j0 << LOG_R) + o, val);
         }
