@@ -10,9 +10,11 @@
 //
 // Build: one workgroup owns a block of 1024 nodes of its input level: it
 // hashes them (leaf mode: one leaf per node; pair mode: two child digests per
-// node read from the level below), then reduces the block in LDS for up to
-// 10 further levels, writing every level to HBM.  Three launches cover
-// 2^24 leaves.
+// node read from the level below), then reduces the block in LDS for the
+// next levels, writing every level to HBM.  While the grid is large only the
+// levels with >= 256 nodes per block (one per thread) are reduced in LDS, so
+// no lane idles through the narrow levels; the top of the tree (< 64K nodes)
+// is finished with up to 10 LDS levels per launch.
 #include "internal.h"
 #include "blake2s.h"
 
@@ -202,8 +204,12 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   while (true) {
     // Levels reducible inside a block of min(count, 1024) nodes.
     const uint64_t blk = count < kMerkleBlock ? count : kMerkleBlock;
+    // Levels reduced in LDS: while the grid is large, only those at least one
+    // node per thread wide (1024 -> 512 -> 256), so no thread idles; the
+    // narrow top of the tree is finished by small launches.
+    const uint32_t max_extra = count >= (uint64_t)kMerkleBlock * 64 ? 2 : 10;
     uint32_t extra = 0;
-    while ((blk >> (extra + 1)) >= 1 && extra + 1 <= 10 && level + extra + 1 <= depth) ++extra;
+    while ((blk >> (extra + 1)) >= 1 && extra + 1 <= max_extra && level + extra + 1 <= depth) ++extra;
     LevelPtrs lp;
     for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
     const unsigned grid = (unsigned)((count + kMerkleBlock - 1) / kMerkleBlock);

@@ -169,6 +169,96 @@ __global__ void k_mad_nodep(uint64_t* out, uint32_t s) {
 }
 
 typedef void (*kfn)(uint64_t*, uint32_t);
+__global__ void k_perm(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_xor(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_add3(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_lshlor(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_bitop3(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_xad(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_pkmov(uint64_t* out, uint32_t s) {
+  uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_pk_mov_b32 %0, %0, %0 op_sel:[1,0]" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_lshr64(uint64_t* out, uint32_t s) {
+  uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_lshrrev_b64 %0, 32, %0" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_alignbyte(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_alignbyte_b32 %0, %0, %0, 1" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
 static void run(const char* name, kfn k, uint64_t* buf) {
   const int blocks = 256 * 4, threads = 1024;  // 16 waves per CU = 4 per SIMD
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
@@ -198,5 +288,14 @@ int main() {
   run("add_co+addc vcc chain", k_addc2vcc, buf);
   run("v_alignbit_b32", k_alignbit, buf);
   run("v_cndmask_e64", k_cndmask, buf);
+  run("v_perm_b32", k_perm, buf);
+  run("v_xor_b32", k_xor, buf);
+  run("v_add3_u32", k_add3, buf);
+  run("v_lshl_or_b32", k_lshlor, buf);
+  run("v_bitop3_b32", k_bitop3, buf);
+  run("v_xad_u32", k_xad, buf);
+  run("v_pk_mov_b32", k_pkmov, buf);
+  run("v_lshrrev_b64", k_lshr64, buf);
+  run("v_alignbyte_b32", k_alignbyte, buf);
   return 0;
 }

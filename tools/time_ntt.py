@@ -34,13 +34,22 @@ def main():
         assert lib.stark_dev_alloc(ctx, n * 32, ctypes.byref(d)) == 0
         lib.stark_memcpy_h2d(ctx, d, host.ctypes.data, n * 32)
         wp = w.ctypes.data_as(u64p)
+        if os.environ.get("WHAT") == "merkle":   # Merkle commit of n 32-B leaves instead
+            lib.stark_merkle_new.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+            lib.stark_merkle_update_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                    ctypes.c_size_t, ctypes.c_void_p]
+            tree = ctypes.c_void_p()
+            assert lib.stark_merkle_new(ctx, ctypes.byref(tree)) == 0
+            step = lambda: lib.stark_merkle_update_dev(tree, d, n, 32, None)  # noqa: E731
+        else:
+            step = lambda: lib.stark_ntt_dev(ctx, d, log_n, 1, wp, 0, None)  # noqa: E731
         for _ in range(3):
-            lib.stark_ntt_dev(ctx, d, log_n, 1, wp, 0, None)
+            step()
         lib.stark_ctx_synchronize(ctx)
         reps = 20
         t0 = time.perf_counter()
         for _ in range(reps):
-            lib.stark_ntt_dev(ctx, d, log_n, 1, wp, 0, None)
+            step()
         lib.stark_ctx_synchronize(ctx)
         ms = (time.perf_counter() - t0) * 1000 / reps
         results[path] = ms
