@@ -89,6 +89,22 @@ __device__ __forceinline__ Digest hash_leaf(const uint8_t* __restrict__ p, uint3
   return d;
 }
 
+// A 32-byte leaf (one canonical field element): one final block whose words
+// 8..15 are compile-time zeros, so their message additions fold away.
+__device__ __forceinline__ Digest hash_leaf32(const uint8_t* __restrict__ p) {
+  Digest d;
+  b2s_init(d.h);
+  uint32_t m[16];
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  const uint4 x = q[0], y = q[1];
+  m[0] = x.x; m[1] = x.y; m[2] = x.z; m[3] = x.w;
+  m[4] = y.x; m[5] = y.y; m[6] = y.z; m[7] = y.w;
+#pragma unroll
+  for (int i = 8; i < 16; ++i) m[i] = 0;
+  b2s_compress(d.h, m, 32, 0, true);
+  return d;
+}
+
 __device__ __forceinline__ Digest hash_pair(const Digest& l, const Digest& r) {
   uint32_t m[16];
 #pragma unroll
@@ -124,6 +140,7 @@ struct LevelPtrs {
   Digest* lv[12];
 };
 
+template <bool LEAF32>
 __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint8_t* __restrict__ leaves,
                                                                       uint32_t leaf_len,
                                                                       const Digest* __restrict__ below,
@@ -136,7 +153,7 @@ __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint
     const uint64_t node = base + i;
     Digest d;
     if (leaves) {
-      d = hash_leaf(leaves + node * leaf_len, leaf_len);
+      d = LEAF32 ? hash_leaf32(leaves + node * 32) : hash_leaf(leaves + node * leaf_len, leaf_len);
     } else {
       d = hash_pair(load_digest(below + 2 * node), load_digest(below + 2 * node + 1));
     }
@@ -214,7 +231,8 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
     for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
     const unsigned grid = (unsigned)((count + kMerkleBlock - 1) / kMerkleBlock);
     const Digest* below = leaf_mode ? nullptr : nodes + level_offset(n, level - 1);
-    hipLaunchKernelGGL(merkle_build_kernel, dim3(grid), dim3(kMerkleThreads), 0, stream,
+    const bool leaf32 = leaf_mode && leaf_len == 32 && (((uintptr_t)d_leaves) & 15) == 0;
+    hipLaunchKernelGGL(leaf32 ? merkle_build_kernel<true> : merkle_build_kernel<false>, dim3(grid), dim3(kMerkleThreads), 0, stream,
                        leaf_mode ? d_leaves : nullptr, (uint32_t)leaf_len, below, count, extra, lp);
     STARK_HIP(ctx, hipGetLastError());
     level += extra;
