@@ -211,17 +211,23 @@ def main():
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     passes = (log_n + 7) // 8
     traffic = None
+    prof_avg = None
     try:
         prof = json.load(open(PROFILE))
         rec = prof["pmc_bytes_per_launch"].get("stark::ntt_pass_kernel<8, false>")
         if rec and log_n == 24:
-            traffic = passes * rec["hbm_bytes"]   # PMC bytes of one transform (per-launch x passes)
+            # HBM bytes of one transform: the PMC per-launch average (FETCH_SIZE x 2 + WRITE_SIZE,
+            # MI355X_MICROARCH.md) x the transform's launches.
+            traffic = passes * rec["hbm_bytes"]
+            prof_avg = prof["kernels"]["stark::ntt_pass_kernel<8, false>"]["avg_ns"] / 1e6
     except (OSError, KeyError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "kernel": f"ntt_pass_kernel<8> x {passes} launches per 2^{log_n} transform",
-                "ms_per_transform": round(ev_ms, 4)}
+                "ms_per_transform": round(ev_ms, 4), "avg_launch_ms": round(ev_ms / passes, 4),
+                "rocprof_avg_launch_ms": round(prof_avg, 4) if prof_avg else None,
+                "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
     # modular products per transform: radix-4 steps (3 per group of 4, 1 in the
     # first step) + column twiddles (1 per element in table passes, 2 in two-level passes)
     lr = [log_n // passes + (1 if i < log_n % passes else 0) for i in range(passes)]

@@ -14,7 +14,7 @@ import sys
 
 
 def load(pattern):
-    files = glob.glob(pattern)
+    files = glob.glob(pattern) or glob.glob(pattern.replace("/*", "/**/*"), recursive=True)
     return list(csv.DictReader(open(files[0]))) if files else []
 
 
