@@ -8,10 +8,11 @@ the transform per second.  The N=1 line also carries the Merkle leaves/s (2^24
 wall-clock.
 
 N > 1 GPUs: one process per GPU (torch.distributed.run, backend "nccl" = RCCL);
-the GPUs jointly transform ONE 2^(24+log2 N)-point vector, block-sharded, with
-the four-step algorithm whose three exchanges are RCCL all-to-alls over xGMI
-(stark_amd/distributed.py).  Per-GPU work is fixed, so scaling is weak; timing
-is barrier-bracketed and the max over ranks is used.
+the GPUs jointly transform ONE 2^(24+log2 N)-point vector with the one-exchange
+distributed NTT (stark_amd/distributed.py `cyclic_ntt`: cyclic distribution in,
+chunked out; local 2^24-point NTT + twiddle, one RCCL all-to-all over xGMI,
+local N-point DFTs).  Per-GPU work is fixed, so scaling is weak; timing is
+barrier-bracketed and the max over ranks is used.
 """
 import argparse
 import json
@@ -102,10 +103,16 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # One rank per GPU.  (local % device_count and STARK_BENCH_BACKEND=gloo exist only to rehearse
+    # the N > 1 path with several ranks on a one-GPU box; the driver's runs use RCCL, one GPU per rank.)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=torch.device(f"cuda:{local}"))
+        backend = os.environ.get("STARK_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend, init_method="env://")
     ctx = S.Context(local)
     # Every library launch and every RCCL collective goes to this stream, so
     # the HIP events below bracket exactly the timed work.
@@ -124,12 +131,16 @@ def main():
     torch.cuda.synchronize()
     dptr = buf.data_ptr()
     if world > 1:
-        from stark_amd.distributed import GpuOps, four_step_ntt
+        from stark_amd.distributed import GpuOps, cyclic_ntt
         ops = GpuOps(ctx)
-        state = {"x": buf}
+        bufs = [buf, torch.empty_like(buf)]
+        state = {"i": 0}
 
         def step():
-            state["x"] = four_step_ntt(state["x"], log_total, w_total, ops)
+            # in place on this rank's shard, result into the other buffer (ping-pong)
+            a, b = bufs[state["i"]], bufs[1 - state["i"]]
+            cyclic_ntt(a, log_total, w_total, ops, out=b, in_place=True)
+            state["i"] ^= 1
     else:
         def step():
             ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr)
@@ -146,7 +157,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    on_gloo = world > 1 and dist.get_backend() == "gloo"
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if on_gloo else f"cuda:{local}")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.cpu()[0])
@@ -274,9 +286,10 @@ def main():
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32x8 (BN254 Fr)",
                 "data": "synthetic (splitmix64 uniform in [0,p), BASELINE.md)",
                 "config": {"workload": f"forward NTT 2^{log_total} BN254 Fr, natural order, HBM-resident"
-                                       + (f", four-step over {world} GPUs (RCCL all-to-all)" if world > 1 else ""),
+                                       + (f", distributed over {world} GPUs (cyclic in / chunked out, one RCCL "
+                                          "all-to-all)" if world > 1 else ""),
                            "global_batch": 1, "seq_len": n * world, "shard_per_gpu": n,
-                           "parallelism": f"four-step NTT x{world} (block shards)" if world > 1 else "single GPU"},
+                           "parallelism": f"distributed NTT x{world} (one all-to-all)" if world > 1 else "single GPU"},
                 "roofline": roofline, "valu_roofline": valu, "cpu_baseline": cpu}
         line.update(extras)
         print(json.dumps(line))

@@ -204,6 +204,13 @@ stark_status stark_transpose_dev(stark_ctx* ctx, const uint64_t* d_src, uint64_t
 stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, size_t cols, uint64_t row_base,
                                  uint64_t col_base, const uint64_t root[4], uint32_t log_order, void* stream);
 
+/* In-place small DFTs across a stride: for each i < stride, the 2^log_g points
+ * d[i + stride*j] become sum_j d[i + stride*j] root^(j*k) (inverse: root^-1 and
+ * scaled by 2^-log_g).  root is a primitive 2^log_g-th root; log_g <= 4.  This is
+ * the cross-rank DFT of the one-exchange distributed NTT. */
+stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
+                                   const uint64_t root[4], int inverse, void* stream);
+
 /* ---- device memory helpers (for callers without their own allocator) ------ */
 stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);
 stark_status stark_dev_free(stark_ctx* ctx, void* d_ptr);

@@ -40,6 +40,48 @@ __global__ void twiddle2d_kernel(fe* __restrict__ data, uint64_t rows, uint64_t 
   fe_store(data + idx, fe_mul(fe_load(data + idx), t));
 }
 
+// Small DFTs across a stride: for each i < stride, the G = 2^LOG_G points
+// d[i + stride j], j < G, are replaced by their DFT (root w_G), in place:
+//   out[i + stride k] = sum_j d[i + stride j] w_G^(j k)   [* G^-1 when scaling].
+// One thread per i, the G values in registers; adjacent threads touch
+// adjacent elements, so every access is coalesced.  This is the cross-rank
+// DFT of the one-exchange distributed NTT (stark_amd/distributed.py).
+struct SmallRoots {
+  fe w[8];  // w_G^k, k < G/2 (Montgomery)
+};
+
+template <int LOG_G>
+__global__ __launch_bounds__(256) void strided_ntt_kernel(fe* __restrict__ d, uint64_t stride, SmallRoots rt,
+                                                          fe scale, int do_scale) {
+  constexpr int G = 1 << LOG_G;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= stride) return;
+  fe x[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    int br = 0;
+#pragma unroll
+    for (int b = 0; b < LOG_G; ++b) br |= ((j >> b) & 1) << (LOG_G - 1 - b);
+    x[br] = fe_load(d + i + stride * (uint64_t)j);  // bit-reversed order for the in-place DIT
+  }
+#pragma unroll
+  for (int s = 0; s < LOG_G; ++s) {
+    const int m = 1 << s;
+#pragma unroll
+    for (int k = 0; k < G; k += 2 * m)
+#pragma unroll
+      for (int jj = 0; jj < m; ++jj) {
+        fe t = x[k + jj + m];
+        if (jj) t = fe_mul(t, rt.w[jj << (LOG_G - 1 - s)]);  // w_{2m}^jj
+        const fe u = x[k + jj];
+        x[k + jj] = fe_add(u, t);
+        x[k + jj + m] = fe_sub(u, t);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < G; ++k) fe_store(d + i + stride * (uint64_t)k, do_scale ? fe_mul(x[k], scale) : x[k]);
+}
+
 }  // namespace stark
 
 using namespace stark;
@@ -55,6 +97,39 @@ stark_status stark_transpose_dev(stark_ctx* ctx, const uint64_t* d_src, uint64_t
   dim3 grid((unsigned)((cols + kTT - 1) / kTT), (unsigned)((rows + kTT - 1) / kTT), batch);
   hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, pick_stream(ctx, stream), (const fe*)d_src, (fe*)d_dst,
                      (uint64_t)rows, (uint64_t)cols);
+  STARK_HIP(ctx, hipGetLastError());
+  return STARK_OK;
+}
+
+stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
+                                   const uint64_t root[4], int inverse, void* stream) {
+  if (!ctx || !d_data || !root) return STARK_ERR_BAD_ARG;
+  if (log_g > 4) return STARK_ERR_BAD_LENGTH;
+  if (stride == 0 || log_g == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  HostFp w = F.from_canonical(root);
+  // root must be a primitive 2^log_g-th root: w^(G/2) = -1.
+  const HostFp half = F.pow_u64(w, (uint64_t)1 << (log_g - 1));
+  if (!FieldHost::eq(F.add(half, F.one()), F.zero())) return STARK_ERR_BAD_ROOT;
+  if (inverse) w = F.inv(w);
+  SmallRoots rt;
+  HostFp p = F.one();
+  for (int k = 0; k < 8; ++k) {
+    rt.w[k] = to_dev(p);
+    p = F.mul(p, w);
+  }
+  const fe scale = to_dev(F.inv(F.from_u64((uint64_t)1 << log_g)));
+  const unsigned grid = (unsigned)((stride + 255) / 256);
+  hipStream_t s = pick_stream(ctx, stream);
+  fe* d = (fe*)d_data;
+  const int sc = inverse ? 1 : 0;
+  switch (log_g) {
+    case 1: hipLaunchKernelGGL(strided_ntt_kernel<1>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
+    case 2: hipLaunchKernelGGL(strided_ntt_kernel<2>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
+    case 3: hipLaunchKernelGGL(strided_ntt_kernel<3>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
+    default: hipLaunchKernelGGL(strided_ntt_kernel<4>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
+  }
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
 }

@@ -89,6 +89,7 @@ _SIGNATURES = {
     "stark_r1cs_trace_export": ([_vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _szp, _u64p, _szp], ctypes.c_int),
     "stark_r1cs_trace_free": ([_vp], None),
     "stark_prove_r1cs_trace": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_ntt_strided_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, ctypes.c_int, _vp], ctypes.c_int),
     "stark_transpose_dev": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32, _vp], ctypes.c_int),
     "stark_twiddle2d_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _u64p,
                              ctypes.c_uint32, _vp], ctypes.c_int),
@@ -207,6 +208,13 @@ class Context:
         r = _limbs(root)
         self.check(self.lib.stark_ntt_dev(self.h, d_ptr, log_n, batch, _p64(r), 1 if inverse else 0, stream or None),
                    "ntt_dev")
+
+    def ntt_strided_dev(self, d_ptr: int, log_g: int, stride: int, root, inverse: bool = False,
+                        stream: int = 0) -> None:
+        """For each i < stride: DFT over d[i + stride*j], j < 2^log_g (in place)."""
+        r = _limbs(root)
+        self.check(self.lib.stark_ntt_strided_dev(self.h, d_ptr, log_g, stride, _p64(r), 1 if inverse else 0,
+                                                  stream or None), "ntt_strided")
 
     def transpose_dev(self, d_src: int, d_dst: int, rows: int, cols: int, batch: int = 1, stream: int = 0) -> None:
         self.check(self.lib.stark_transpose_dev(self.h, d_src, d_dst, rows, cols, batch, stream or None), "transpose")

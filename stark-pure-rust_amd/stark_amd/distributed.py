@@ -81,6 +81,48 @@ def four_step_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = F
     return out
 
 
+def cyclic_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = False, group=None,
+               out: torch.Tensor = None, in_place: bool = False) -> torch.Tensor:
+    """Distributed NTT with ONE all-to-all: cyclic distribution in, chunked out.
+
+    Input: rank r holds u_r[j2] = x[r + G j2], j2 < M (shape (M, 4), M = n / G).
+    Output: rank r holds out[k1][i] = X[r c + i + M k1], k1 < G, i < c = M / G
+    (G runs of c consecutive outputs, M apart).  With j = j1 + G j2 and
+    k = k2 + M k1:
+
+        X[k2 + M k1] = sum_j1 wG^(j1 k1) * w^(j1 k2) * DFT_M(u_j1)[k2]
+
+    so each rank runs its M-point NTT (root w^G) and the twiddle w^(r k2)
+    locally, one all_to_all_single sends chunk k2 in [s c, (s+1) c) to rank s,
+    and the G-point DFTs over j1 (root w^M) run locally across the received
+    chunks (stark_ntt_strided_dev: no transposes).  The inverse uses the same
+    steps with inverse transforms and w^-1 in the twiddle (n^-1 = M^-1 G^-1).
+    The block-in/block-out `four_step_ntt` needs three exchanges for the same
+    transform; this layout is the one-exchange form.  in_place=True lets the
+    local transform overwrite x (no copy); `out` receives the result if given.
+    """
+    G = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    n = 1 << log_n
+    M = n // G
+    if M * G != n or M % G != 0 or x.shape[0] != M:
+        raise ValueError(f"cyclic_ntt: need M = n/G divisible by G (n=2^{log_n}, G={G}, shard={x.shape[0]})")
+    w = root % P
+    y = x if in_place else x.clone()
+    if G == 1:
+        ops.ntt(y, log_n, 1, w, inverse)
+        return y
+    log_m = M.bit_length() - 1
+    log_g = G.bit_length() - 1
+    c = M // G
+    ops.ntt(y, log_m, 1, pow(w, G, P), inverse)                     # M-point, root w^G
+    ops.twiddle2d(y, 1, M, r, 0, pow(w, P - 2, P) if inverse else w, log_n)   # y[k2] *= w^(+-r k2)
+    z = torch.empty_like(y) if out is None else out
+    _exchange(z, y, group)                                          # z[j1][i] = Y_j1[r c + i]
+    ops.ntt_strided(z, log_g, c, pow(w, M, P), inverse)             # G-point over j1, root w^M
+    return z
+
+
 class GpuOps:
     """Local steps on this rank's GPU through libstark_hip (kernels on the
     torch current stream, so they order with the RCCL collectives)."""
@@ -94,6 +136,9 @@ class GpuOps:
 
     def ntt(self, t: torch.Tensor, log_len: int, batch: int, root: int, inverse: bool) -> None:
         self.ctx.ntt_dev(t.data_ptr(), log_len, batch, root, inverse=inverse, stream=self._stream())
+
+    def ntt_strided(self, t: torch.Tensor, log_g: int, stride: int, root: int, inverse: bool) -> None:
+        self.ctx.ntt_strided_dev(t.data_ptr(), log_g, stride, root, inverse=inverse, stream=self._stream())
 
     def transpose(self, src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int) -> None:
         self.ctx.transpose_dev(src.data_ptr(), dst.data_ptr(), rows, cols, 1, stream=self._stream())

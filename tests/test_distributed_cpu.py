@@ -39,6 +39,12 @@ class OracleOps:
             f = self.o.inv_best_fft if inverse else self.o.best_fft
             seg[:] = f(seg.copy(), root, log_len, cpus=1)
 
+    def ntt_strided(self, t, log_g, stride, root, inverse):
+        a = self._u64(t).reshape(1 << log_g, stride, 4)
+        f = self.o.inv_best_fft if inverse else self.o.best_fft
+        for i in range(stride):
+            a[:, i] = f(a[:, i].copy(), root, log_g, cpus=1)
+
     def transpose(self, src, dst, rows, cols):
         s = self._u64(src).reshape(rows, cols, 4)
         self._u64(dst)[:] = s.transpose(1, 0, 2).reshape(-1, 4)
@@ -68,6 +74,48 @@ def _worker(rank, world, port, log_n, inverse, out_q):
     out_q.put((rank, y.numpy().view(np.uint64).copy()))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from stark_amd.distributed import cyclic_ntt
+    n = 1 << log_n
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    x = torch.from_numpy(full[rank::world].copy().view(np.int64))   # cyclic: x[rank + G j]
+    y = cyclic_ntt(x, log_n, O.root_of_unity(log_n), OracleOps(), inverse=inverse)
+    out_q.put((rank, y.numpy().view(np.uint64).copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n,inverse", [(2, 6, False), (2, 9, True), (4, 8, False), (4, 10, True),
+                                                 (8, 12, False), (8, 9, True)])
+def test_cyclic_ntt_gloo(world, log_n, inverse):
+    """One-exchange layout: rank r gets X[r c + i + M k1] at out[k1 c + i]."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = 1 << log_n
+    M, c = n // world, n // world // world
+    got = np.zeros((n, 4), dtype=np.uint64)
+    for r in range(world):
+        out = parts[r].reshape(world, c, 4)
+        for k1 in range(world):
+            got[r * c + k1 * M: r * c + k1 * M + c] = out[k1]
+    o = O.Oracle()
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    w = O.root_of_unity(log_n)
+    want = o.inv_best_fft(full, w, log_n, cpus=4) if inverse else o.best_fft(full, w, log_n, cpus=4)
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("world,log_n,inverse", [(2, 6, False), (2, 9, True), (4, 8, False), (4, 10, True),

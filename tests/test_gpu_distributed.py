@@ -23,6 +23,73 @@ def _free_port():
     return port
 
 
+def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stark_amd as S
+    from stark_amd.distributed import GpuOps, cyclic_ntt
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = S.Context(0)
+    n = 1 << log_n
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    x = torch.from_numpy(full[rank::world].copy().view(np.int64)).cuda()
+    y = cyclic_ntt(x, log_n, O.root_of_unity(log_n), GpuOps(ctx), inverse=inverse)
+    torch.cuda.synchronize()
+    out_q.put((rank, y.cpu().numpy().view(np.uint64).copy()))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_n,inverse", [(2, 12, False), (2, 17, True), (4, 16, False), (8, 15, True)])
+def test_cyclic_ntt_gpu(world, log_n, inverse):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = 1 << log_n
+    M, c = n // world, n // world // world
+    got = np.zeros((n, 4), dtype=np.uint64)
+    for r in range(world):
+        out = parts[r].reshape(world, c, 4)
+        for k1 in range(world):
+            got[r * c + k1 * M: r * c + k1 * M + c] = out[k1]
+    o = O.Oracle()
+    full = O.random_elements(n, 0x5EED0000 + log_n)
+    w = O.root_of_unity(log_n)
+    want = o.inv_best_fft(full, w, log_n, cpus=8) if inverse else o.best_fft(full, w, log_n, cpus=8)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("log_g,inverse", [(1, False), (2, True), (3, False), (3, True), (4, False)])
+def test_ntt_strided(ctx, oracle, log_g, inverse):
+    G, stride = 1 << log_g, 1000
+    a = O.random_elements(G * stride, 17 + log_g)
+    d = ctx.alloc(a.nbytes)
+    try:
+        ctx.h2d(d, a)
+        w = O.root_of_unity(log_g)
+        ctx.ntt_strided_dev(d, log_g, stride, w, inverse=inverse)
+        got = np.empty_like(a)
+        ctx.d2h(got, d)
+    finally:
+        ctx.free(d)
+    want = a.reshape(G, stride, 4).copy()
+    f = oracle.inv_best_fft if inverse else oracle.best_fft
+    for i in range(0, stride, 97):
+        want[:, i] = f(want[:, i].copy(), w, log_g, cpus=1)
+        assert np.array_equal(got.reshape(G, stride, 4)[:, i], want[:, i])
+
+
 def _worker(rank, world, port, log_n, inverse, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
