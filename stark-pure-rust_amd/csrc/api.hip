@@ -33,6 +33,22 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   return STARK_OK;
 }
 
+stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
+  if (ctx->pinned_bytes[slot] < bytes) {
+    if (ctx->pinned[slot]) {
+      hipStreamSynchronize(ctx->stream);  // no copy may still target the old buffer
+      hipHostFree(ctx->pinned[slot]);
+    }
+    ctx->pinned[slot] = nullptr;
+    ctx->pinned_bytes[slot] = 0;
+    const size_t want = bytes < 4096 ? 4096 : bytes;
+    STARK_HIP(ctx, hipHostMalloc(&ctx->pinned[slot], want, hipHostMallocDefault));
+    ctx->pinned_bytes[slot] = want;
+  }
+  *out = ctx->pinned[slot];
+  return STARK_OK;
+}
+
 stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out) {
   if (!ctx->trees[slot]) {
     stark_status st = stark_merkle_new(ctx, &ctx->trees[slot]);
@@ -124,7 +140,11 @@ void stark_ctx_destroy(stark_ctx* ctx) {
     stark_merkle_free(t);
     t = nullptr;
   }
-  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena})
+  for (stark_merkle_tree* t : ctx->fri_trees) stark_merkle_free(t);
+  for (void* p : ctx->pinned)
+    if (p) hipHostFree(p);
+  ctx->fri_trees.clear();
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->fri_misc, &ctx->gather_dev})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -16,30 +16,16 @@ struct MontConsts {
   fe one;  // Montgomery image of 1 (= R mod p)
 };
 
-// x^(p-2) for x in Montgomery form (Fermat inverse), fixed exponent.
-__device__ fe fe_inv_mont(const fe& x, const fe& one_m) {
-  // p - 2 limbs, most significant first.
-  const uint32_t e[8] = {STARK_P7, STARK_P6, STARK_P5, STARK_P4, STARK_P3, STARK_P2, STARK_P1, STARK_P0 - 2u};
-  fe r = one_m;
-  for (int i = 0; i < 8; ++i) {
-    for (int b = 31; b >= 0; --b) {
-      r = fe_mul(r, r);
-      if ((e[i] >> b) & 1u) r = fe_mul(r, x);
-    }
-  }
-  return r;
-}
-
 // Phase 1: chunk c of kInvChunk elements -> prefix products (Montgomery,
 // zeros skipped) into pref, chunk product into tot[c].  MONT_IN: the input
 // already holds Montgomery images (the chunk products of a lower level).
-template <bool MONT_IN>
+template <bool MONT_IN, uint32_t CHUNK>
 __global__ void inv_prefix_kernel(const fe* __restrict__ v, uint64_t n, fe* __restrict__ pref, fe* __restrict__ tot,
                                   MontConsts mc) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t lo = c * kInvChunk;
+  const uint64_t lo = c * CHUNK;
   if (lo >= n) return;
-  const uint64_t hi = lo + kInvChunk < n ? lo + kInvChunk : n;
+  const uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
   fe acc = mc.one;
   for (uint64_t i = lo; i < hi; ++i) {
     pref[i] = acc;  // product of the non-zero elements before i (exclusive)
@@ -49,23 +35,16 @@ __global__ void inv_prefix_kernel(const fe* __restrict__ v, uint64_t n, fe* __re
   tot[c] = acc;
 }
 
-// Phase 2: invert every chunk product (Fermat; ~380 products per chunk).
-__global__ void inv_chunk_kernel(fe* __restrict__ tot, uint64_t chunks, MontConsts mc) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= chunks) return;
-  tot[c] = fe_inv_mont(tot[c], mc.one);
-}
-
 // Phase 3: walk each chunk backwards (poly_utils.rs:55-67 order).  `tot`
 // holds the Montgomery inverse of each chunk product.  Output canonical, or
 // Montgomery when MONT_IN.
-template <bool MONT_IN>
+template <bool MONT_IN, uint32_t CHUNK>
 __global__ void inv_back_kernel(const fe* __restrict__ v, uint64_t n, const fe* __restrict__ pref,
                                 const fe* __restrict__ tot, fe* __restrict__ out, MontConsts mc) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t lo = c * kInvChunk;
+  const uint64_t lo = c * CHUNK;
   if (lo >= n) return;
-  const uint64_t hi = lo + kInvChunk < n ? lo + kInvChunk : n;
+  const uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
   fe inv = tot[c];  // Montgomery
   fe unit = fe_zero();
   unit.w[0] = 1;
@@ -115,37 +94,63 @@ MontConsts mont_consts() {
   return mc;
 }
 
-// Batch inverse (0 -> 0).  Chunk products of kInvChunk elements; when there
-// are many chunks their inverses come from a second batch-inverse level, so
-// only n / kInvChunk^2 Fermat inversions run.
+// Batch inverse (0 -> 0), the tree form of multi_inv (poly_utils.rs:38-70):
+// chunk products of 32 inputs, then of 16 chunk products per level until at
+// most 16 remain.  Those few are inverted on the host (one Fermat inversion
+// there takes microseconds; on one GPU lane it is a ~250-product dependent
+// chain, a quarter millisecond), and the inverses flow back down the levels.
+constexpr uint32_t kInvChunkUp = 16;
+constexpr uint64_t kInvTop = 16;
+
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s) {
   if (n == 0) return STARK_OK;
-  const uint64_t c1 = (n + kInvChunk - 1) / kInvChunk;
-  const uint64_t c2 = (c1 + kInvChunk - 1) / kInvChunk;
-  const bool two = c1 > 4096;
-  stark_status st = ensure_buf(ctx, ctx->io2, (n + c1 + (two ? 2 * c1 + c2 : 0)) * sizeof(fe));
+  // Level sizes: c[0] = ceil(n / 32) chunk products, c[i] = ceil(c[i-1] / 16).
+  std::vector<uint64_t> c{(n + kInvChunk - 1) / kInvChunk};
+  while (c.back() > kInvTop) c.push_back((c.back() + kInvChunkUp - 1) / kInvChunkUp);
+  // Scratch: pref0[n], then per level i: tot_i[c_i], inv_i[c_i], pref_{i+1}[c_i] (for i < top).
+  size_t total = n;
+  for (size_t i = 0; i < c.size(); ++i) total += 3 * c[i];
+  stark_status st = ensure_buf(ctx, ctx->io2, total * sizeof(fe));
   if (st != STARK_OK) return st;
-  fe* pref1 = (fe*)ctx->io2.ptr;
-  fe* tot1 = pref1 + n;
-  const MontConsts mc = mont_consts();
-  const unsigned b1 = (unsigned)((c1 + 255) / 256);
-  hipLaunchKernelGGL(inv_prefix_kernel<false>, dim3(b1), dim3(256), 0, s, d_in, n, pref1, tot1, mc);
-  const fe* tot1_inv = tot1;
-  if (two) {
-    fe* pref2 = tot1 + c1;
-    fe* tot2 = pref2 + c1;
-    fe* inv1 = tot2 + c2;
-    const unsigned b2 = (unsigned)((c2 + 255) / 256);
-    hipLaunchKernelGGL(inv_prefix_kernel<true>, dim3(b2), dim3(256), 0, s, (const fe*)tot1, c1, pref2, tot2, mc);
-    hipLaunchKernelGGL(inv_chunk_kernel, dim3(b2), dim3(256), 0, s, tot2, c2, mc);
-    hipLaunchKernelGGL(inv_back_kernel<true>, dim3(b2), dim3(256), 0, s, (const fe*)tot1, c1, (const fe*)pref2,
-                       (const fe*)tot2, inv1, mc);
-    tot1_inv = inv1;
-  } else {
-    hipLaunchKernelGGL(inv_chunk_kernel, dim3(b1), dim3(256), 0, s, tot1, c1, mc);
+  fe* pref0 = (fe*)ctx->io2.ptr;
+  std::vector<fe*> tot(c.size()), inv(c.size()), pref(c.size());
+  fe* at = pref0 + n;
+  for (size_t i = 0; i < c.size(); ++i) {
+    tot[i] = at;
+    inv[i] = at + c[i];
+    pref[i] = at + 2 * c[i];  // prefixes of level i+1's chunks over tot[i]
+    at += 3 * c[i];
   }
-  hipLaunchKernelGGL(inv_back_kernel<false>, dim3(b1), dim3(256), 0, s, d_in, n, (const fe*)pref1, tot1_inv, d_out,
+  const MontConsts mc = mont_consts();
+  auto blocks = [](uint64_t chunks) { return (unsigned)((chunks + 255) / 256); };
+  hipLaunchKernelGGL((inv_prefix_kernel<false, kInvChunk>), dim3(blocks(c[0])), dim3(256), 0, s, d_in, n, pref0, tot[0],
                      mc);
+  for (size_t i = 1; i < c.size(); ++i)
+    hipLaunchKernelGGL((inv_prefix_kernel<true, kInvChunkUp>), dim3(blocks(c[i])), dim3(256), 0, s,
+                       (const fe*)tot[i - 1], c[i - 1], pref[i - 1], tot[i], mc);
+  STARK_HIP(ctx, hipGetLastError());
+  // Top level: at most 16 non-zero Montgomery products, inverted on the host.
+  const size_t top = c.size() - 1;
+  uint8_t* pinned = nullptr;
+  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
+  if (st != STARK_OK) return st;
+  fe* h_top = (fe*)(pinned + 2560);  // pinned slot 1 layout: [2560, 3072) batch-inverse top level
+  STARK_HIP(ctx, hipMemcpyAsync(h_top, tot[top], c[top] * sizeof(fe), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  {
+    const FieldHost& F = FieldHost::get();
+    for (uint64_t i = 0; i < c[top]; ++i) {
+      HostFp x;
+      for (int k = 0; k < 4; ++k) x.v[k] = (uint64_t)h_top[i].w[2 * k] | ((uint64_t)h_top[i].w[2 * k + 1] << 32);
+      h_top[i] = to_dev(F.inv(x));  // Montgomery in, Montgomery out; products are never zero
+    }
+  }
+  STARK_HIP(ctx, hipMemcpyAsync(inv[top], h_top, c[top] * sizeof(fe), hipMemcpyHostToDevice, s));
+  for (size_t i = top; i >= 1; --i)
+    hipLaunchKernelGGL((inv_back_kernel<true, kInvChunkUp>), dim3(blocks(c[i])), dim3(256), 0, s,
+                       (const fe*)tot[i - 1], c[i - 1], (const fe*)pref[i - 1], (const fe*)inv[i], inv[i - 1], mc);
+  hipLaunchKernelGGL((inv_back_kernel<false, kInvChunk>), dim3(blocks(c[0])), dim3(256), 0, s, d_in, n,
+                     (const fe*)pref0, (const fe*)inv[0], d_out, mc);
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
 }

@@ -23,14 +23,6 @@
 #include "internal.h"
 #include "blake2s.h"
 
-// Defined in merkle.hip.
-namespace stark {
-stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream);
-stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
-stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
-                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream);
-}  // namespace stark
 
 struct stark_fri_layer {
   bool last = false;
@@ -48,11 +40,25 @@ struct stark_fri_proof {
 
 namespace stark {
 
+// special_x = T::from_bytes_le(m_root) (fri.rs:135) computed on the device from
+// the tree's root digest (LE bytes = LE words), reduced mod p, as a Montgomery
+// image for the fold.  The transcript never leaves the GPU between layers.
+__global__ void fri_special_x_kernel(const uint32_t* __restrict__ root, fe* __restrict__ s_m, fe r2) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  fe x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x.w[i] = root[i];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) fe_reduce_once(x);  // x < 2^256 < 6p
+  *s_m = fe_mul(x, r2);
+}
+
 __global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
-                                const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, fe s_m, fe zeta_m,
-                                fe inv4_m) {
+                                const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
+                                const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= q) return;
+  const fe s_m = *s_ptr;
   const fe y0 = fe_load(v + i), y1 = fe_load(v + i + q), y2 = fe_load(v + i + 2 * q), y3 = fe_load(v + i + 3 * q);
   const uint64_t e = i << shift;
   const fe winv = fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]);  // Montgomery w^-i
@@ -68,11 +74,40 @@ __global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, 
   fe_store(col + i, fe_mul(acc, inv4_m));
 }
 
-static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
-                               size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out) {
+// Roots of up to 16 trees gathered into one buffer (one D2H for the transcript).
+struct RootPtrs {
+  const uint32_t* p[16];
+};
+__global__ void collect_roots_kernel(RootPtrs r, uint32_t count, uint32_t* __restrict__ out) {
+  const uint32_t t = threadIdx.x;
+  if (t < 8 * count) out[t] = r.p[t / 8][t % 8];
+}
+
+// Pinned slot 1 layout: [0, 2048) mk_r1cs_proof's transcript, [2048, 2560) FRI roots.
+constexpr size_t kFriRootsOff = 2048;
+
+struct FriPending {
+  std::unique_ptr<stark_fri_proof> proof;
+  size_t layers = 0, last_len = 0;
+  uint32_t excl = 0;
+  std::vector<size_t> qs;
+  const fe* last_dev = nullptr;  // the last layer's values (device)
+  const uint8_t* h_roots = nullptr;  // pinned: roots of trees[0..layers]
+};
+
+// prove_low_degree on device values, phase 1.  Per layer everything is
+// enqueued on the context stream with no host round trip: build the values'
+// tree, derive special_x from its root on the device, fold, build the
+// column's tree; finally the roots are queued for download.
+void FriPendingDeleter::operator()(FriPending* p) const { delete p; }
+
+stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
+                         uint32_t excl, FriPendingPtr* out) {
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
-  auto proof = std::make_unique<stark_fri_proof>();
+  FriPendingPtr p(new FriPending());
+  p->proof = std::make_unique<stark_fri_proof>();
+  p->excl = excl;
   // Layer sizes and checks up front (the reference panics on these).
   size_t layers = 0;
   {
@@ -86,6 +121,8 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
       ++layers;
     }
   }
+  if (layers + 1 > 16) return STARK_ERR_BAD_LENGTH;
+  p->layers = layers;
   const Twiddles* tw = nullptr;
   uint32_t log_n0 = 0;
   while (((size_t)1 << log_n0) < n) ++log_n0;
@@ -96,7 +133,7 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
     stark_status st = get_twiddles(ctx, inv_root, log_n0, &tw);
     if (st != STARK_OK) return st;
   }
-  // Column buffers: n/4 + n/16 + ... elements.
+  // Column buffers: n/4 + n/16 + ... elements; special_x per layer; the roots.
   size_t col_total = 0;
   {
     size_t m = n;
@@ -107,41 +144,80 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
   }
   stark_status st = ensure_buf(ctx, ctx->fri_cols, (col_total ? col_total : 1) * sizeof(fe));
   if (st != STARK_OK) return st;
-  stark_merkle_tree* trees[2] = {nullptr, nullptr};
-  st = ctx_tree(ctx, 0, &trees[0]);
-  if (st == STARK_OK) st = ctx_tree(ctx, 1, &trees[1]);
+  st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
   if (st != STARK_OK) return st;
+  uint8_t* pinned = nullptr;
+  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
+  if (st != STARK_OK) return st;
+  p->h_roots = pinned + kFriRootsOff;
+  fe* d_sx = (fe*)ctx->fri_misc.ptr;
+  uint32_t* d_roots = (uint32_t*)(d_sx + 16);
+  while (ctx->fri_trees.size() < layers + 1) {
+    stark_merkle_tree* t = nullptr;
+    st = stark_merkle_new(ctx, &t);
+    if (st != STARK_OK) return st;
+    ctx->fri_trees.push_back(t);
+  }
+  std::vector<stark_merkle_tree*>& trees = ctx->fri_trees;  // trees[l] commits layer l's values
 
   const fe* cur = d_values;
   fe* next = (fe*)ctx->fri_cols.ptr;
   size_t m = n;
-  int tc = 0;  // trees[tc] holds the tree of `cur`
   HostFp w = F.from_canonical(root);
   const HostFp inv4 = F.inv(F.from_u64(4));
+  const fe r2 = to_dev(F.from_canonical(F.one().v));  // Montgomery image of R
   for (size_t layer = 0; layer < layers; ++layer) {
     if (layer == 0) {
-      st = merkle_build(ctx, trees[tc], (const uint8_t*)cur, m, 32, s);
+      st = merkle_build(ctx, trees[0], (const uint8_t*)cur, m, 32, s);
       if (st != STARK_OK) return st;
     }
-    uint8_t m_root[32];
-    st = merkle_root_d2h(ctx, trees[tc], s, m_root);
-    if (st != STARK_OK) return st;
-    // special_x = T::from_bytes_le(m_root) (fri.rs:135): reduced mod p.
-    const HostFp sx = F.from_bytes_le(m_root, 32);
+    hipLaunchKernelGGL(fri_special_x_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(trees[layer]),
+                       d_sx + layer, r2);
     const size_t q = m / 4;
     const HostFp zeta = F.pow_u64(w, q);  // w^(n/4)
     const unsigned blocks = (unsigned)((q + 255) / 256);
     hipLaunchKernelGGL(fri_fold_kernel, dim3(blocks), dim3(256), 0, s, cur, next, (uint64_t)q, (uint32_t)(2 * layer),
-                       tw->d_lo, tw->d_hi, tw->kb, to_dev(sx), to_dev(zeta), to_dev(inv4));
+                       tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4));
     STARK_HIP(ctx, hipGetLastError());
-    st = merkle_build(ctx, trees[1 - tc], (const uint8_t*)next, q, 32, s);
+    st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s);
     if (st != STARK_OK) return st;
-    stark_fri_layer L;
-    st = merkle_root_d2h(ctx, trees[1 - tc], s, L.root2);
-    if (st != STARK_OK) return st;
+    p->qs.push_back(q);
+    // Recurse on the column with w^4 (fri.rs:215-223).
+    cur = next;
+    next += q;
+    m = q;
+    w = F.pow_u64(w, 4);
+  }
+  p->last_dev = cur;
+  p->last_len = m;
+  if (layers) {
+    RootPtrs rp;
+    for (size_t l = 0; l <= layers; ++l) rp.p[l] = (const uint32_t*)merkle_root_dev(trees[l]);
+    hipLaunchKernelGGL(collect_roots_kernel, dim3(1), dim3(128), 0, s, rp, (uint32_t)(layers + 1), d_roots);
+    STARK_HIP(ctx, hipGetLastError());
+    STARK_HIP(ctx, hipMemcpyAsync((void*)p->h_roots, d_roots, 32 * (layers + 1), hipMemcpyDeviceToHost, s));
+  }
+  *out = std::move(p);
+  return STARK_OK;
+}
+
+// Phase 2: the host transcript (fri.rs:181-204), every opening in one gather
+// batch together with the caller's `extra` requests, and the Last layer
+// (fri.rs:108-110).
+stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out) {
+  hipStream_t s = ctx->stream;
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  std::vector<stark_merkle_tree*>& trees = ctx->fri_trees;
+  stark_fri_proof* proof = p->proof.get();
+  proof->layers.resize(p->layers);
+  std::vector<GatherReq> reqs = extra;
+  for (size_t layer = 0; layer < p->layers; ++layer) {
+    stark_fri_layer& L = proof->layers[layer];
+    const size_t q = p->qs[layer];
+    memcpy(L.root2, p->h_roots + 32 * (layer + 1), 32);
     // ys = get_pseudorandom_indices(m2_root, column.len(), 40, exclude) (fri.rs:181-189)
     uint32_t ys[40];
-    st = stark_get_pseudorandom_indices(L.root2, 32, (uint32_t)q, 40, excl, ys);
+    stark_status st = stark_get_pseudorandom_indices(L.root2, 32, (uint32_t)q, 40, p->excl, ys);
     if (st != STARK_OK) return st;
     L.col_idx.assign(ys, ys + 40);
     for (int i = 0; i < 40; ++i)
@@ -153,27 +229,28 @@ static stark_status prove_impl(stark_ctx* ctx, const fe* d_values, size_t n, con
     L.col_nodes.resize(40 * L.col_depth * 32);
     L.poly_leaves.resize(160 * 32);
     L.poly_nodes.resize(160 * L.poly_depth * 32);
-    st = merkle_gather(ctx, trees[1 - tc], L.col_idx.data(), 40, L.col_leaves.data(), L.col_nodes.data(), s);
-    if (st != STARK_OK) return st;
-    st = merkle_gather(ctx, trees[tc], L.poly_idx.data(), 160, L.poly_leaves.data(), L.poly_nodes.data(), s);
-    if (st != STARK_OK) return st;
-    proof->layers.push_back(std::move(L));
-    // Recurse on the column with w^4 (fri.rs:215-223); its tree is the one just built.
-    cur = next;
-    next += q;
-    m = q;
-    w = F.pow_u64(w, 4);
-    tc = 1 - tc;
+    reqs.push_back({trees[layer + 1], L.col_idx.data(), 40, L.col_leaves.data(), L.col_nodes.data()});
+    reqs.push_back({trees[layer], L.poly_idx.data(), 160, L.poly_leaves.data(), L.poly_nodes.data()});
   }
-  // Last { last: values.map(to_bytes_le) } (fri.rs:108-110)
+  stark_status st = merkle_gather_batch(ctx, reqs, s);
+  if (st != STARK_OK) return st;
   stark_fri_layer last;
   last.last = true;
-  last.last_values.resize(m * 32);
-  if (m) STARK_HIP(ctx, hipMemcpyAsync(last.last_values.data(), cur, m * 32, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
+  last.last_values.resize(p->last_len * 32);
+  if (p->last_len)
+    STARK_HIP(ctx, hipMemcpy(last.last_values.data(), p->last_dev, p->last_len * 32, hipMemcpyDeviceToHost));
   proof->layers.push_back(std::move(last));
-  *out = proof.release();
+  *out = p->proof.release();
   return STARK_OK;
+}
+
+stark_status fri_prove_device(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
+                              size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out) {
+  FriPendingPtr p;
+  stark_status st = fri_enqueue(ctx, d_values, n, root, max_deg_plus_1, excl, &p);
+  if (st != STARK_OK) return st;
+  std::vector<GatherReq> none;
+  return fri_finish(ctx, p.get(), none, out);
 }
 
 // "[b0,b1,...]" for a byte string (serde_json of Vec<u8>), table driven.
@@ -256,7 +333,7 @@ stark_status stark_prove_low_degree_dev(stark_ctx* ctx, const uint64_t* d_values
   if (!ctx || !root || !out || (n && !d_values)) return STARK_ERR_BAD_ARG;
   *out = nullptr;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
-  return prove_impl(ctx, (const fe*)d_values, n, root, max_deg_plus_1, exclude_multiples_of, out);
+  return fri_prove_device(ctx, (const fe*)d_values, n, root, max_deg_plus_1, exclude_multiples_of, out);
 }
 
 stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size_t n, const uint64_t root[4],
@@ -267,7 +344,7 @@ stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size
   stark_status st = ensure_buf(ctx, ctx->io, (n ? n : 1) * sizeof(fe));
   if (st != STARK_OK) return st;
   if (n) STARK_HIP(ctx, hipMemcpyAsync(ctx->io.ptr, values, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
-  st = prove_impl(ctx, (const fe*)ctx->io.ptr, n, root, max_deg_plus_1, exclude_multiples_of, out);
+  st = fri_prove_device(ctx, (const fe*)ctx->io.ptr, n, root, max_deg_plus_1, exclude_multiples_of, out);
   hipStreamSynchronize(ctx->stream);
   return st;
 }

@@ -53,6 +53,11 @@ struct stark_ctx {
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  std::vector<stark_merkle_tree*> fri_trees;  // one per FRI layer (+ the input's), reused across proofs
+  stark::DevBuf fri_misc;                     // per-layer special_x (device transcript)
+  void* pinned[2] = {nullptr, nullptr};       // pinned host scratch (ctx_pinned)
+  size_t pinned_bytes[2] = {0, 0};
+  stark::DevBuf gather_dev;                   // merkle_gather_batch device region
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
 };
@@ -67,6 +72,9 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
   } while (0)
 
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
+// Context-owned pinned host scratch of at least `bytes` (async copy target).
+// Slot 0: gather batches; slot 1: transcript values and roots.
+stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
 // Context-owned Merkle tree slot (created on first use).
 stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out);
 hipStream_t pick_stream(stark_ctx* ctx, void* stream);
@@ -78,6 +86,39 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
 // Device NTT over `batch` contiguous transforms (in place, canonical values).
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
                         bool inverse, hipStream_t stream);
+
+// Merkle internals (merkle.hip).
+stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                          hipStream_t stream);
+stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
+const uint8_t* merkle_root_dev(const stark_merkle_tree* t);
+stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
+                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream, bool sync = true);
+
+struct GatherReq {
+  stark_merkle_tree* t;
+  const size_t* idx;
+  size_t k;
+  uint8_t* leaves_out;  // k * leaf_len bytes
+  uint8_t* nodes_out;   // k * depth * 32 bytes
+};
+// All requests in one pinned upload, one download, one synchronisation.
+stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream);
+
+// FRI prover on device values (fri.hip).  fri_enqueue puts every layer on the
+// context stream with a device-side transcript and queues the roots' download;
+// after the caller's stream synchronisation, fri_finish samples the indices
+// and gathers all openings (with the caller's extra requests) in one batch.
+struct FriPending;
+struct FriPendingDeleter {
+  void operator()(FriPending* p) const;
+};
+using FriPendingPtr = std::unique_ptr<FriPending, FriPendingDeleter>;
+stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
+                         uint32_t excl, FriPendingPtr* out);
+stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out);
+stark_status fri_prove_device(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
+                              size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out);
 
 // Montgomery image of a host value as a device fe (same bytes).
 inline fe to_dev(const HostFp& x) {

@@ -254,6 +254,11 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   return STARK_OK;
 }
 
+// Device address of the root digest (valid after merkle_build).
+const uint8_t* merkle_root_dev(const stark_merkle_tree* t) {
+  return (const uint8_t*)t->nodes.ptr + (2 * t->n - 2) * sizeof(Digest);
+}
+
 stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]) {
   const Digest* nodes = (const Digest*)t->nodes.ptr;
   STARK_HIP(ctx, hipMemcpyAsync(out, nodes + (2 * t->n - 2), 32, hipMemcpyDeviceToHost, stream));
@@ -261,9 +266,11 @@ stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t s
   return STARK_OK;
 }
 
-// Gathers k proofs (leaf bytes + siblings) to host buffers.
+// Gathers k proofs (leaf bytes + siblings) to host buffers.  sync = false
+// leaves the copies in flight: `indices` and the outputs must stay alive until
+// the caller synchronises the stream.
 stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
-                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream) {
+                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream, bool sync) {
   if (k == 0) return STARK_OK;
   for (size_t i = 0; i < k; ++i)
     if (indices[i] >= t->n) return STARK_ERR_BAD_ARG;
@@ -277,8 +284,8 @@ stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* i
   uint64_t* d_idx = (uint64_t*)base;
   uint8_t* d_leaf = base + idx_bytes;
   Digest* d_node = (Digest*)(base + idx_bytes + ((leaf_bytes + 15) & ~(size_t)15));
-  std::vector<uint64_t> h_idx(indices, indices + k);
-  STARK_HIP(ctx, hipMemcpyAsync(d_idx, h_idx.data(), idx_bytes, hipMemcpyHostToDevice, stream));
+  static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t indices are uploaded as u64");
+  STARK_HIP(ctx, hipMemcpyAsync(d_idx, indices, idx_bytes, hipMemcpyHostToDevice, stream));
   hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)k), dim3(64), 0, stream, t->d_leaves,
                      (uint32_t)t->leaf_len, (const Digest*)t->nodes.ptr, (uint64_t)t->n, t->depth, d_idx,
                      (uint32_t)k, d_leaf, d_node);
@@ -286,7 +293,64 @@ stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* i
   if (leaves_out) STARK_HIP(ctx, hipMemcpyAsync(leaves_out, d_leaf, leaf_bytes, hipMemcpyDeviceToHost, stream));
   if (nodes_out && node_bytes)
     STARK_HIP(ctx, hipMemcpyAsync(nodes_out, d_node, node_bytes, hipMemcpyDeviceToHost, stream));
+  if (sync) STARK_HIP(ctx, hipStreamSynchronize(stream));
+  return STARK_OK;
+}
+
+// Many gathers with one upload and one download: the indices go through the
+// context's pinned scratch, every request's leaves and siblings land in one
+// device region, and a single D2H brings all of them back (pageable copies
+// of many small buffers each cost a staged, synchronous round trip).
+stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream) {
+  size_t n_idx = 0, out_bytes = 0;
+  std::vector<size_t> off(reqs.size());
+  for (size_t r = 0; r < reqs.size(); ++r) {
+    const GatherReq& q = reqs[r];
+    for (size_t i = 0; i < q.k; ++i)
+      if (q.idx[i] >= q.t->n) return STARK_ERR_BAD_ARG;
+    n_idx += q.k;
+    off[r] = out_bytes;
+    out_bytes += ((q.k * q.t->leaf_len + 15) & ~(size_t)15) + q.k * q.t->depth * sizeof(Digest);
+  }
+  if (n_idx == 0) return STARK_OK;
+  const size_t idx_bytes = n_idx * sizeof(uint64_t);
+  stark_status st = ensure_buf(ctx, ctx->gather_dev, idx_bytes + out_bytes);
+  if (st != STARK_OK) return st;
+  uint8_t* host = nullptr;
+  st = ctx_pinned(ctx, 0, idx_bytes + out_bytes, (void**)&host);
+  if (st != STARK_OK) return st;
+  uint64_t* h_idx = (uint64_t*)host;
+  uint8_t* h_out = host + idx_bytes;
+  uint8_t* d_base = (uint8_t*)ctx->gather_dev.ptr;
+  uint64_t* d_idx = (uint64_t*)d_base;
+  uint8_t* d_out = d_base + idx_bytes;
+  size_t at = 0;
+  for (const GatherReq& q : reqs) {
+    for (size_t i = 0; i < q.k; ++i) h_idx[at + i] = q.idx[i];
+    at += q.k;
+  }
+  STARK_HIP(ctx, hipMemcpyAsync(d_idx, h_idx, idx_bytes, hipMemcpyHostToDevice, stream));
+  at = 0;
+  for (size_t r = 0; r < reqs.size(); ++r) {
+    const GatherReq& q = reqs[r];
+    if (q.k == 0) continue;
+    uint8_t* leaf = d_out + off[r];
+    Digest* node = (Digest*)(leaf + ((q.k * q.t->leaf_len + 15) & ~(size_t)15));
+    hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)q.k), dim3(64), 0, stream, q.t->d_leaves,
+                       (uint32_t)q.t->leaf_len, (const Digest*)q.t->nodes.ptr, (uint64_t)q.t->n, q.t->depth,
+                       (const uint64_t*)(d_idx + at), (uint32_t)q.k, leaf, node);
+    STARK_HIP(ctx, hipGetLastError());
+    at += q.k;
+  }
+  STARK_HIP(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, stream));
   STARK_HIP(ctx, hipStreamSynchronize(stream));
+  for (size_t r = 0; r < reqs.size(); ++r) {
+    const GatherReq& q = reqs[r];
+    const uint8_t* leaf = h_out + off[r];
+    const uint8_t* node = leaf + ((q.k * q.t->leaf_len + 15) & ~(size_t)15);
+    if (q.leaves_out) memcpy(q.leaves_out, leaf, q.k * q.t->leaf_len);
+    if (q.nodes_out) memcpy(q.nodes_out, node, q.k * q.t->depth * sizeof(Digest));
+  }
   return STARK_OK;
 }
 
@@ -359,7 +423,7 @@ stark_status stark_merkle_gen_proofs(stark_merkle_tree* t, const size_t* indices
   stark_status st = merkle_root_d2h(ctx, t, ctx->stream, t->root);
   if (st != STARK_OK) return st;
   t->has_root = true;
-  return merkle_gather(ctx, t, indices, k, leaves_out, nodes_out, ctx->stream);
+  return merkle_gather(ctx, t, indices, k, leaves_out, nodes_out, ctx->stream, true);
 }
 
 stark_status stark_merkle_verify(const uint8_t root[32], const size_t* indices, size_t k, const uint8_t* leaves,

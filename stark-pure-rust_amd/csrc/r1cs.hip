@@ -29,11 +29,6 @@
 #include "blake2s.h"
 
 namespace stark {
-stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream);
-stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
-stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
-                           uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream);
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
 void json_bytes(std::string& o, const uint8_t* p, size_t n);
 void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
@@ -82,6 +77,87 @@ __device__ __forceinline__ fe fe_from_u64(uint64_t v) {
   return r;
 }
 
+// Fiat-Shamir values derived on the device from the tree roots, so the proof
+// is enqueued end to end without waiting for the host.
+struct Transcript {
+  fe r0;       // canonical r[0]
+  fe r1_m;     // Montgomery r[1], r[2]
+  fe r2_m;
+  fe k_m[11];  // Montgomery k[0..10]
+  uint32_t roots[3][8];  // a_root, m_root, l_root (LE words = the digest bytes)
+  int err;
+};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Digest of a 32- or 33-byte message (words LE, zero padded).
+__device__ __forceinline__ void b2s_short(const uint32_t* w, uint32_t extra_byte, uint32_t len, uint32_t out[8]) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = w[i];
+  m[8] = extra_byte;
+#pragma unroll
+  for (int i = 9; i < 16; ++i) m[i] = 0;
+  b2s_init(out);
+  b2s_compress(out, m, len, 0, true);
+}
+
+// r = get_random_ff_values(a_root, precision, 3, 0) (utils.rs:272-290):
+// get_pseudorandom_indices(seed, precision, 24, 0) (fri/src/utils.rs:82-109)
+// expands seed || B(seed) || B(B(seed)), reads 24 big-endian words mod
+// precision; each group of 8 is written as big-endian bytes and read back
+// with from_bytes_le (mod p).
+__global__ void r1cs_r_kernel(const uint32_t* __restrict__ a_root, uint32_t prec_mask, fe r2,
+                              Transcript* __restrict__ tr) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t data[24];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) data[i] = a_root[i];
+  b2s_short(data, 0, 32, data + 8);
+  b2s_short(data + 8, 0, 32, data + 16);
+  fe r[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t v = bswap32(data[8 * c + i]) & prec_mask;  // BE word mod 2^k
+      r[c].w[i] = bswap32(v);                                  // BE bytes read as LE words
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) fe_reduce_once(r[c]);
+  }
+  tr->r0 = r[0];
+  tr->r1_m = fe_mul(r[1], r2);
+  tr->r2_m = fe_mul(r[2], r2);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) tr->roots[0][i] = a_root[i];
+}
+
+// k_0 = 1, k_i = from_str(mk_seed([m_root, [i]])) = BE integer of
+// Blake2s(m_root || i) mod p (prove.rs:274-283, utils.rs:25-27, 51-57).
+__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, Transcript* __restrict__ tr) {
+  const uint32_t i = threadIdx.x;
+  if (i > 10) return;
+  if (i == 0) {
+    tr->k_m[0] = one_m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tr->roots[1][j] = m_root[j];
+    return;
+  }
+  uint32_t h[8];
+  b2s_short(m_root, i, 33, h);
+  fe k;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k.w[j] = bswap32(h[7 - j]);
+#pragma unroll
+  for (int t = 0; t < 5; ++t) fe_reduce_once(k);
+  tr->k_m[i] = fe_mul(k, r2);
+}
+
+__global__ void r1cs_l_root_kernel(const uint32_t* __restrict__ l_root, Transcript* __restrict__ tr) {
+  if (threadIdx.x < 8) tr->roots[2][threadIdx.x] = l_root[threadIdx.x];
+}
+
 // Montgomery image of g^i from the two-level tables of g.
 __device__ __forceinline__ fe pow_tab(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint64_t i) {
   return fe_mul(lo[i & (((uint64_t)1 << kb) - 1)], hi[i >> kb]);
@@ -127,10 +203,11 @@ __global__ void r1cs_pad_kernel(const fe* __restrict__ src, fe* __restrict__ dst
 // val_nmr / val_dnm of calc_a_mini_evaluations (utils.rs:317-318), written as
 // Montgomery images for the product scans.
 __global__ void r1cs_a_vals_kernel(const fe* __restrict__ ext_idx, const fe* __restrict__ ext_pidx,
-                                   const fe* __restrict__ w, uint64_t steps, fe r0, fe r1_m, fe r2_m, fe mr2,
+                                   const fe* __restrict__ w, uint64_t steps, const Transcript* __restrict__ tr, fe mr2,
                                    fe* __restrict__ nmr_m, fe* __restrict__ dnm_m) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= steps) return;
+  const fe r0 = tr->r0, r1_m = tr->r1_m, r2_m = tr->r2_m;
   const fe rw = fe_mul(fe_load(w + j), r2_m);
   const fe vn = fe_add(fe_add(r0, fe_mul(fe_load(ext_idx + j * kExtensionFactor), r1_m)), rw);
   const fe vd = fe_add(fe_add(r0, fe_mul(fe_load(ext_pidx + j * kExtensionFactor), r1_m)), rw);
@@ -180,14 +257,18 @@ __global__ __launch_bounds__(256) void scan_tot_kernel(fe* __restrict__ tot, uin
   for (uint32_t i = lo; i < hi; ++i) acc = fe_mul(acc, tot[i]);
   part[threadIdx.x] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    fe run = one_m;
-    for (int t = 0; t < 256; ++t) {
-      const fe p = part[t];
-      part[t] = run;
-      run = fe_mul(run, p);
-    }
+  // Inclusive Hillis-Steele scan of the 256 run products (8 dependent
+  // products instead of a 256-long serial chain), then shift to exclusive.
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    fe t = part[threadIdx.x];
+    if (threadIdx.x >= off) t = fe_mul(part[threadIdx.x - off], t);
+    __syncthreads();
+    part[threadIdx.x] = t;
+    __syncthreads();
   }
+  const fe excl = threadIdx.x ? part[threadIdx.x - 1] : one_m;
+  __syncthreads();
+  part[threadIdx.x] = excl;
   __syncthreads();
   acc = part[threadIdx.x];
   for (uint32_t i = lo; i < hi; ++i) {
@@ -244,7 +325,8 @@ struct ConstraintArgs {
   uint64_t prec;
   uint64_t shift1, shift2;  // original_steps/3*skips, original_steps/3*2*skips (mod precision)
   uint32_t log_prec, kb, n2, n3;
-  fe r0, r1_m, r2_m, mr2;
+  const Transcript* tr;  // r0, r1, r2 (device transcript)
+  fe mr2;
   fe invz_m[8];          // Montgomery inv(w8^t - 1), 0 for t = 0 (multi_inv of Z, prove.rs:203)
 };
 
@@ -265,6 +347,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe* PIDX = IDX + n;
   const fe* A = PIDX + n;
   const uint64_t prev = (i + n - kExtensionFactor) & mask;
+  const fe r0 = a.tr->r0, r1_m = a.tr->r1_m, r2_m = a.tr->r2_m;
   const fe p = fe_load(Pc + i), s = fe_load(S + i), av = fe_load(A + i);
   const fe p_prev = fe_load(Pc + prev), a_prev = fe_load(A + prev);
   const fe p2 = fe_load(Pc + ((i + a.shift1) & mask)), p3 = fe_load(Pc + ((i + a.shift2) & mask));
@@ -273,9 +356,9 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe q1 = fe_mul(fe_mul(fe_load(F0 + i), a.mr2),
                        fe_sub(fe_sub(p, fe_mul(fe_mul(fe_load(F1 + i), a.mr2), p_prev)), fe_mul(fe_load(K + i), s_m)));
   const fe q2 = fe_mul(fe_mul(fe_load(F2 + i), a.mr2), fe_sub(p3, fe_mul(fe_mul(p, a.mr2), p2)));
-  const fe rs = fe_mul(s, a.r2_m);
-  const fe nmr = fe_add(fe_add(a.r0, fe_mul(fe_load(IDX + i), a.r1_m)), rs);
-  const fe dnm = fe_add(fe_add(a.r0, fe_mul(fe_load(PIDX + i), a.r1_m)), rs);
+  const fe rs = fe_mul(s, r2_m);
+  const fe nmr = fe_add(fe_add(r0, fe_mul(fe_load(IDX + i), r1_m)), rs);
+  const fe dnm = fe_add(fe_add(r0, fe_mul(fe_load(PIDX + i), r1_m)), rs);
   const fe q3 = fe_sub(fe_mul(fe_mul(av, a.mr2), dnm), fe_mul(fe_mul(a_prev, a.mr2), nmr));
   const uint32_t t = (uint32_t)(i & 7);
   fe iz = a.invz_m[0];
@@ -310,7 +393,7 @@ struct LincombArgs {
   const fe* rows;
   fe* out;
   uint64_t prec;
-  fe k_m[11];
+  const Transcript* tr;  // k (device transcript)
   fe xs_m[8];  // (g2^steps)^t, t = i mod 8 (prove.rs:287-291)
 };
 
@@ -327,17 +410,18 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
 #pragma unroll
   for (uint32_t k = 1; k < 8; ++k)
     if (t == k) xs = a.xs_m[k];
-  fe acc = fe_mul(d1, a.k_m[0]);
-  acc = fe_add(acc, fe_mul(d2, a.k_m[1]));
-  acc = fe_add(acc, fe_mul(d3, a.k_m[2]));
-  acc = fe_add(acc, fe_mul(p, a.k_m[3]));
-  acc = fe_add(acc, fe_mul(fe_mul(p, a.k_m[4]), xs));
-  acc = fe_add(acc, fe_mul(b2, a.k_m[5]));
-  acc = fe_add(acc, fe_mul(fe_mul(b2, a.k_m[6]), xs));
-  acc = fe_add(acc, fe_mul(b3, a.k_m[7]));
-  acc = fe_add(acc, fe_mul(fe_mul(b3, a.k_m[8]), xs));
-  acc = fe_add(acc, fe_mul(av, a.k_m[9]));
-  acc = fe_add(acc, fe_mul(s, a.k_m[10]));
+  const fe* k_m = a.tr->k_m;
+  fe acc = fe_mul(d1, k_m[0]);
+  acc = fe_add(acc, fe_mul(d2, k_m[1]));
+  acc = fe_add(acc, fe_mul(d3, k_m[2]));
+  acc = fe_add(acc, fe_mul(p, k_m[3]));
+  acc = fe_add(acc, fe_mul(fe_mul(p, k_m[4]), xs));
+  acc = fe_add(acc, fe_mul(b2, k_m[5]));
+  acc = fe_add(acc, fe_mul(fe_mul(b2, k_m[6]), xs));
+  acc = fe_add(acc, fe_mul(b3, k_m[7]));
+  acc = fe_add(acc, fe_mul(fe_mul(b3, k_m[8]), xs));
+  acc = fe_add(acc, fe_mul(av, k_m[9]));
+  acc = fe_add(acc, fe_mul(s, k_m[10]));
   fe_store(a.out + i, acc);
 }
 
@@ -480,7 +564,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
   uint64_t* perm;
   uint64_t* acc_leaves;
-  int* d_err;
+  Transcript* d_tr;
   const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
   Carve cv;
   cv.add(&raw, 8 * steps);  // K F0 F1 F2 S P IDX PIDX (then A's coefficients reuse K's slot)
@@ -498,9 +582,37 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   cv.add(&consts, 2 * n_pfi + 2);
   cv.add(&rows, 8 * prec);
   cv.add(&lvals, prec);
-  cv.add(&d_err, 1);
+  cv.add(&d_tr, 1);
   STARK_TRY(cv.commit(ctx, ctx->r1cs_arena));
 
+  // Interpolants and boundary points (utils.rs:421-474), host side (#pub points).
+  const HostFp x_last = F.pow_u64(g2, prec - skips);
+  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
+  for (size_t i = 0; i < n_pfi; ++i) {
+    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
+    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
+  }
+  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
+  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
+  std::vector<fe> h(2 * n_pfi + 2);  // alive until the proof's final synchronisation
+  {
+    for (size_t i = 0; i < n_pfi; ++i) {
+      h[i] = to_dev(xv[i]);  // Montgomery x_k for Zb2
+      uint64_t c[4];
+      F.to_canonical(interp2[i], c);
+      for (int k = 0; k < 4; ++k) {
+        h[n_pfi + i].w[2 * k] = (uint32_t)c[k];
+        h[n_pfi + i].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+      }
+    }
+    uint64_t c[4];
+    F.to_canonical(interp3[0], c);
+    for (int k = 0; k < 4; ++k) {
+      h[2 * n_pfi].w[2 * k] = (uint32_t)c[k];
+      h[2 * n_pfi].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+    }
+    STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+  }
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
   for (int c = 0; c < 6; ++c) {
@@ -518,7 +630,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
-  STARK_HIP(ctx, hipMemsetAsync(d_err, 0, sizeof(int), s));
+  STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
                      (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
   STARK_HIP(ctx, hipGetLastError());
@@ -530,38 +642,15 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(ctx_tree(ctx, 3, &m_tree));
   STARK_TRY(ctx_tree(ctx, 4, &l_tree));
   STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
-  // The eight LDEs overlap with the host's wait for a_root below.
   STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
-  STARK_TRY(merkle_root_d2h(ctx, acc_tree, s, proof->a_root));
-  HostFp r[3];
-  {
-    uint32_t rnd[24];
-    STARK_TRY(stark_get_pseudorandom_indices(proof->a_root, 32, (uint32_t)prec, 24, 0, rnd));
-    for (int c = 0; c < 3; ++c) {
-      uint8_t be[32];
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t v = rnd[8 * c + i];
-        be[4 * i] = (uint8_t)(v >> 24);
-        be[4 * i + 1] = (uint8_t)(v >> 16);
-        be[4 * i + 2] = (uint8_t)(v >> 8);
-        be[4 * i + 3] = (uint8_t)v;
-      }
-      r[c] = F.from_bytes_le(be, 32);
-    }
-  }
-  uint64_t r0c[4];
-  F.to_canonical(r[0], r0c);
-  fe r0_canon;
-  for (int k = 0; k < 4; ++k) {
-    r0_canon.w[2 * k] = (uint32_t)r0c[k];
-    r0_canon.w[2 * k + 1] = (uint32_t)(r0c[k] >> 32);
-  }
+  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(acc_tree),
+                     (uint32_t)(prec - 1), mc.r2, d_tr);
+  STARK_HIP(ctx, hipGetLastError());
   // A (utils.rs:293-339, prove.rs:183-184).
   fe* ext_idx = cols + 6 * prec;
   fe* ext_pidx = cols + 7 * prec;
   hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
-                     (const fe*)ext_pidx, (const fe*)wcopy, steps, r0_canon, to_dev(r[1]), to_dev(r[2]), mc.r2, nmr,
-                     dnm);
+                     (const fe*)ext_pidx, (const fe*)wcopy, steps, (const Transcript*)d_tr, mc.r2, nmr, dnm);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
   STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
@@ -571,35 +660,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(lde(ctx, raw, 1, cols + 8 * prec, log_steps, log_prec, *tw1i, *tw2, s));
 
-  // Interpolants and boundary points (utils.rs:421-474), host side (#pub points).
-  const HostFp x_last = F.pow_u64(g2, prec - skips);
-  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
-  for (size_t i = 0; i < n_pfi; ++i) {
-    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
-    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
-  }
-  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
-  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
-  {
-    std::vector<fe> h(2 * n_pfi + 2);
-    for (size_t i = 0; i < n_pfi; ++i) {
-      h[i] = to_dev(xv[i]);  // Montgomery x_k for Zb2
-      uint64_t c[4];
-      F.to_canonical(interp2[i], c);
-      for (int k = 0; k < 4; ++k) {
-        h[n_pfi + i].w[2 * k] = (uint32_t)c[k];
-        h[n_pfi + i].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
-      }
-    }
-    uint64_t c[4];
-    F.to_canonical(interp3[0], c);
-    for (int k = 0; k < 4; ++k) {
-      h[2 * n_pfi].w[2 * k] = (uint32_t)c[k];
-      h[2 * n_pfi].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
-    }
-    STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
-    STARK_HIP(ctx, hipStreamSynchronize(s));  // h is a stack buffer
-  }
   hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                      (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one, zb, zb + prec);
   STARK_HIP(ctx, hipGetLastError());
@@ -614,7 +674,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.lo = tw2->d_lo;
   ca.hi = tw2->d_hi;
   ca.rows = rows;
-  ca.err = d_err;
+  ca.err = &d_tr->err;
   ca.prec = prec;
   ca.shift1 = (os / 3 * skips) % prec;
   ca.shift2 = (os / 3 * 2 * skips) % prec;
@@ -622,9 +682,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.kb = tw2->kb;
   ca.n2 = (uint32_t)n_pfi;
   ca.n3 = 1;
-  ca.r0 = r0_canon;
-  ca.r1_m = to_dev(r[1]);
-  ca.r2_m = to_dev(r[2]);
+  ca.tr = d_tr;
   ca.mr2 = mc.r2;
   {
     // Z(g2^i) = (g2^steps)^(i mod 8) - 1; inverse with 0 -> 0 (prove.rs:128-129, 203).
@@ -640,29 +698,14 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   // Main tree over the 256-B rows (prove.rs:261-264).
   STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s));
-  STARK_TRY(merkle_root_d2h(ctx, m_tree, s, proof->m_root));
-  int h_err = 0;
-  STARK_HIP(ctx, hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
-  if (h_err) {
-    ctx->last_error = (h_err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
-                                  : "invalid B: boundary value mismatch (utils.rs:477-524)";
-    return STARK_ERR_CHECK;
-  }
-  // k (prove.rs:274-283): k_i = BE integer of Blake2s(m_root || i) mod p.
+  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(m_tree), mc.r2, mc.one,
+                     d_tr);
+  STARK_HIP(ctx, hipGetLastError());
   LincombArgs la;
   la.rows = rows;
   la.out = lvals;
   la.prec = prec;
-  la.k_m[0] = to_dev(F.one());
-  for (int i = 1; i < 11; ++i) {
-    uint8_t msg[33], h[32], le[32];
-    memcpy(msg, proof->m_root, 32);
-    msg[32] = (uint8_t)i;
-    b2s_host(msg, 33, h);
-    for (int b = 0; b < 32; ++b) le[b] = h[31 - b];
-    la.k_m[i] = to_dev(F.from_bytes_le(le, 32));
-  }
+  la.tr = d_tr;
   {
     const HostFp w8 = F.pow_u64(g2, steps);
     HostFp wt = F.one();
@@ -674,9 +717,27 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s));
-  STARK_TRY(merkle_root_d2h(ctx, l_tree, s, proof->l_root));
+  hipLaunchKernelGGL(r1cs_l_root_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(l_tree), d_tr);
+  STARK_HIP(ctx, hipGetLastError());
+  // Roots and the constraint flags come back with the FRI prover's synchronisation.
+  Transcript* h_tr = nullptr;
+  STARK_TRY(ctx_pinned(ctx, 1, sizeof(Transcript) + 1024, (void**)&h_tr));
+  STARK_HIP(ctx, hipMemcpyAsync(h_tr, d_tr, sizeof(Transcript), hipMemcpyDeviceToHost, s));
 
-  // Spot checks (prove.rs:337-362).
+  // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367), enqueued behind the rest.
+  FriPendingPtr fri_pending;
+  STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending));
+  STARK_HIP(ctx, hipStreamSynchronize(s));  // the proof's one wait for the device
+  if (h_tr->err) {
+    ctx->last_error = (h_tr->err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
+                                      : "invalid B: boundary value mismatch (utils.rs:477-524)";
+    return STARK_ERR_CHECK;
+  }
+  memcpy(proof->a_root, h_tr->roots[0], 32);
+  memcpy(proof->m_root, h_tr->roots[1], 32);
+  memcpy(proof->l_root, h_tr->roots[2], 32);
+
+  // Spot checks (prove.rs:337-362); their openings join the FRI openings in one gather batch.
   uint32_t pos32[kSpotChecks];
   STARK_TRY(stark_get_pseudorandom_indices(proof->l_root, 32, (uint32_t)prec, kSpotChecks, (uint32_t)skips, pos32));
   std::vector<size_t> positions(kSpotChecks), aug(4 * kSpotChecks);
@@ -690,12 +751,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   std::vector<uint8_t> l_leaves(32 * kSpotChecks), l_nodes(32 * kSpotChecks * log_prec);
   std::vector<uint8_t> m_leaves(256 * 4 * kSpotChecks), m_nodes(32 * 4 * kSpotChecks * log_prec);
-  STARK_TRY(merkle_gather(ctx, l_tree, positions.data(), kSpotChecks, l_leaves.data(), l_nodes.data(), s));
-  STARK_TRY(merkle_gather(ctx, m_tree, aug.data(), 4 * kSpotChecks, m_leaves.data(), m_nodes.data(), s));
-
-  // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367).
+  std::vector<GatherReq> extra = {{l_tree, positions.data(), (size_t)kSpotChecks, l_leaves.data(), l_nodes.data()},
+                                  {m_tree, aug.data(), (size_t)4 * kSpotChecks, m_leaves.data(), m_nodes.data()}};
   stark_fri_proof* fri = nullptr;
-  STARK_TRY(stark_prove_low_degree_dev(ctx, (const uint64_t*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri));
+  STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
+  std::unique_ptr<stark_fri_proof, void (*)(stark_fri_proof*)> fri_guard(fri, stark_fri_proof_free);
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
   std::string& o = proof->json;
   o.reserve((size_t)4 * kSpotChecks * (256 + log_prec * 32) * 4 + (size_t)kSpotChecks * (log_prec + 1) * 32 * 4 +
@@ -712,7 +772,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   json_branches(o, l_leaves, 32, l_nodes, kSpotChecks, log_prec);
   o += ",\"fri_proof\":";
   fri_proof_json_string(fri, o);
-  stark_fri_proof_free(fri);
   o += "}";
   *out = proof.release();
   return STARK_OK;
