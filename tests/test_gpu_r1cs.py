@@ -90,3 +90,31 @@ def test_repeated_proofs_identical(ctx):
     c = prove_with_witness(ctx, _read("compute", "r1cs"), _read("compute", "wtns")).to_json()
     assert a == c
     assert hashlib.sha256(b.encode()).hexdigest() == GOLDEN["pedersen_test"]["json_sha256"]
+
+
+def _synth(log_steps):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    import synth_r1cs
+    return synth_r1cs.for_steps(log_steps)
+
+
+def test_synthetic_circuit_matches_oracle(ctx, oracle):
+    """A larger circuit than the fixtures (2^13 steps, precision 2^16), byte-identical to the oracle."""
+    from stark_amd.r1cs import prove_with_witness
+    r1, wt = _synth(13)
+    got = prove_with_witness(ctx, r1, wt).to_json()
+    tr = R.build_trace(R.read_r1cs(r1), R.read_witness(wt))
+    assert got == R.mk_r1cs_proof_json(oracle, tr)
+
+
+def test_synthetic_2_17_steps_matches_oracle_and_verifies(ctx, oracle):
+    """precision 2^20 (7 FRI layers): byte-identical to the oracle, and accepted by the restated
+    verifier (verify.rs:13-258)."""
+    from stark_amd.r1cs import prove_with_witness
+    r1, wt = _synth(17)
+    proof = prove_with_witness(ctx, r1, wt).to_json()
+    tr = R.build_trace(R.read_r1cs(r1), R.read_witness(wt))
+    assert proof == R.mk_r1cs_proof_json(oracle, tr, cpus=16)
+    assert verify_r1cs_proof(oracle, proof, tr.public_wires, tr.public_first_indices, tr.permuted_indices,
+                             tr.coefficients, tr.flag0, tr.flag1, tr.flag2, tr.n_constraints, tr.n_wires)
