@@ -183,6 +183,14 @@ def main():
         ok = bool(np.array_equal(b20.cpu().numpy().view(np.uint64).reshape(-1, 4), h20))
         extras["ntt_2^20_fwd_inv_ms"] = round(pair_ms, 4)
         extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
+        # The host-buffer entry point (best_fft on a host Vec: H2D + NTT + D2H), PCIe-inclusive;
+        # reported beside `value`, never as it.
+        hc = buf.cpu().numpy().view(np.uint64).reshape(-1, 4)
+        ctx.best_fft(hc, w, log_n)
+        t_h = time.perf_counter()
+        ctx.best_fft(hc, w, log_n)
+        extras["best_fft_host_2^24_ms_pcie_inclusive"] = round((time.perf_counter() - t_h) * 1000.0, 2)
+        del hc
         # inverse 2^24 throughput
         ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr)   # warm: builds the w^-1 tables
         inv_ms = timed_events(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream, 5)
@@ -215,6 +223,24 @@ def main():
         # End-to-end proof wall-clock (config 3: pedersen_test full prove on 1 GPU):
         # prove_with_witness = .r1cs/.wtns bytes -> trace -> mk_r1cs_proof -> StarkProof JSON.
         extras.update(end_to_end(ctx))
+
+    if not args.no_extras and world > 1:
+        # Distributed Merkle commitment (north star: per-GPU subtrees combined across ranks):
+        # 2^log_n 32-B leaves per GPU, subtree roots all-gathered, top levels on the host.
+        from stark_amd.distributed import DistributedMerkle
+        dm = DistributedMerkle(ops)
+        dm.commit(bufs[0], n, 32)
+        dist.barrier()
+        t_m = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            dm.commit(bufs[0], n, 32)
+        dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t_m], dtype=torch.float64,
+                          device="cpu" if on_gloo else f"cuda:{local}")
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        extras["merkle_distributed_leaves_per_s"] = world * n * reps / float(tm.cpu()[0])
+        extras["merkle_distributed_ms"] = round(float(tm.cpu()[0]) * 1000.0 / reps, 3)
 
     # Roofline of the dominant kernel, ntt_pass_kernel: one 2^24 transform is
     # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element

@@ -143,7 +143,84 @@ class GpuOps:
     def transpose(self, src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int) -> None:
         self.ctx.transpose_dev(src.data_ptr(), dst.data_ptr(), rows, cols, 1, stream=self._stream())
 
+    def merkle_commit(self, shard: torch.Tensor, m: int, leaf_len: int) -> bytes:
+        """Subtree over this rank's m leaves (device tensor of m * leaf_len bytes)."""
+        from . import MerkleProofInPlace
+        self._tree = MerkleProofInPlace(self.ctx)
+        self._tree.update_dev(shard.data_ptr(), m, leaf_len, stream=self._stream())
+        torch.cuda.current_stream().synchronize()
+        self._tree.gen_proofs([])  # sets the root (MerkleProofInPlace::get_root semantics)
+        return self._tree.get_root()
+
+    def merkle_open(self, local_indices) -> list:
+        return [(p.leaf, p.nodes) for p in self._tree.gen_proofs(local_indices)]
+
     def twiddle2d(self, t: torch.Tensor, rows: int, cols: int, row_base: int, col_base: int, root: int,
                   log_order: int) -> None:
         self.ctx.twiddle2d_dev(t.data_ptr(), rows, cols, row_base, col_base, root, log_order,
                                stream=self._stream())
+
+
+class DistributedMerkle:
+    """Blake2s Merkle commitment of n = G * m leaves sharded in rank order
+    (rank r holds leaves [r m, (r+1) m)), one GPU per rank.
+
+    commit(): every rank builds its subtree on its GPU (`ops.merkle_commit`);
+    the G subtree roots are all-gathered (RCCL with backend "nccl") and the
+    top log2(G) levels are hashed on the host.  The root is the single-tree
+    root: the reference itself builds 2^k subtrees and a top tree over their
+    roots (gen_multi_proofs_multi_core, merkle_proof_in_place.rs:106-206).
+
+    gen_proofs(indices): each rank opens the indices inside its shard (leaf +
+    subtree siblings) and appends the top-tree siblings; the proofs are
+    all-gathered so every rank returns them in the caller's order, duplicates
+    kept (merkle_proof_in_place.rs:191-205).
+    """
+
+    def __init__(self, ops, group=None):
+        self.ops = ops
+        self.group = group
+        self.G = dist.get_world_size(group)
+        self.r = dist.get_rank(group)
+        self.levels = []      # top tree: levels[0] = subtree roots, ..., levels[-1] = [root]
+        self.m = 0
+
+    def _all_gather_bytes(self, b: bytes) -> list:
+        out = [None] * self.G
+        dist.all_gather_object(out, b, group=self.group)
+        return out
+
+    def commit(self, shard, m: int, leaf_len: int) -> bytes:
+        if m == 0 or m & (m - 1) or self.G & (self.G - 1):
+            raise ValueError("DistributedMerkle: power-of-two shard size and world size required")
+        self.m = m
+        local = self.ops.merkle_commit(shard, m, leaf_len)
+        from . import blake
+        roots = self._all_gather_bytes(local)
+        self.levels = [roots]
+        while len(self.levels[-1]) > 1:
+            lv = self.levels[-1]
+            self.levels.append([blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)])
+        return self.levels[-1][0]
+
+    def root(self) -> bytes:
+        return self.levels[-1][0]
+
+    def gen_proofs(self, indices) -> list:
+        from . import Proof
+        idx = list(indices)
+        mine = [(k, i - self.r * self.m) for k, i in enumerate(idx) if i // self.m == self.r]
+        local = self.ops.merkle_open([li for _, li in mine]) if mine else []
+        part = [(k, leaf, nodes) for (k, _), (leaf, nodes) in zip(mine, local)]
+        parts = [None] * self.G
+        dist.all_gather_object(parts, part, group=self.group)
+        out = [None] * len(idx)
+        for p in parts:
+            for k, leaf, nodes in p:
+                pos = idx[k] // self.m
+                top = []
+                for lv in self.levels[:-1]:   # siblings of the subtree root up to the top
+                    top.append(lv[pos ^ 1])
+                    pos >>= 1
+                out[k] = Proof(leaf, list(nodes) + top)
+        return out

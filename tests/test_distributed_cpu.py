@@ -45,6 +45,16 @@ class OracleOps:
         for i in range(stride):
             a[:, i] = f(a[:, i].copy(), root, log_g, cpus=1)
 
+    def merkle_commit(self, shard, m, leaf_len):
+        self._leaves = bytes(shard.numpy().view(np.uint8)) if hasattr(shard, "numpy") else bytes(shard)
+        self._m, self._ll = m, leaf_len
+        root, _ = self.o.merkle(self._leaves, m, leaf_len)
+        return root
+
+    def merkle_open(self, local_indices):
+        _, paths = self.o.merkle(self._leaves, self._m, self._ll, list(local_indices))
+        return [(self._leaves[i * self._ll:(i + 1) * self._ll], paths[k]) for k, i in enumerate(local_indices)]
+
     def transpose(self, src, dst, rows, cols):
         s = self._u64(src).reshape(rows, cols, 4)
         self._u64(dst)[:] = s.transpose(1, 0, 2).reshape(-1, 4)
@@ -138,3 +148,48 @@ def test_four_step_ntt_gloo(world, log_n, inverse):
     w = O.root_of_unity(log_n)
     want = o.inv_best_fft(full, w, log_n, cpus=4) if inverse else o.best_fft(full, w, log_n, cpus=4)
     assert np.array_equal(got, want)
+
+
+def _worker_merkle(rank, world, port, log_m, leaf_len, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from stark_amd.distributed import DistributedMerkle
+    m = 1 << log_m
+    rng = np.random.default_rng(7)
+    blob = rng.integers(0, 256, size=world * m * leaf_len, dtype=np.uint8)
+    shard = torch.from_numpy(blob[rank * m * leaf_len:(rank + 1) * m * leaf_len].copy())
+    dm = DistributedMerkle(OracleOps())
+    root = dm.commit(shard, m, leaf_len)
+    n = world * m
+    idx = [0, n - 1, 5 % n, n // 2, 5 % n, (n * 3) // 4 + 1]
+    proofs = dm.gen_proofs(idx)
+    out_q.put((rank, root, [(p.leaf, p.nodes) for p in proofs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_m,leaf_len", [(2, 5, 32), (4, 6, 40), (8, 3, 256)])
+def test_distributed_merkle_gloo(world, log_m, leaf_len):
+    """Per-rank subtrees + all-gathered roots = the single tree (root and paths)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_merkle, args=(r, world, port, log_m, leaf_len, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    m = 1 << log_m
+    n = world * m
+    rng = np.random.default_rng(7)
+    blob = bytes(rng.integers(0, 256, size=n * leaf_len, dtype=np.uint8))
+    idx = [0, n - 1, 5 % n, n // 2, 5 % n, (n * 3) // 4 + 1]
+    want_root, want_paths = O.Oracle().merkle(blob, n, leaf_len, idx)
+    for _, root, proofs in res:
+        assert root == want_root
+        for k, (leaf, nodes) in enumerate(proofs):
+            assert leaf == blob[idx[k] * leaf_len:(idx[k] + 1) * leaf_len]
+            assert list(nodes) == want_paths[k]

@@ -90,6 +90,51 @@ def test_ntt_strided(ctx, oracle, log_g, inverse):
         assert np.array_equal(got.reshape(G, stride, 4)[:, i], want[:, i])
 
 
+def _worker_merkle(rank, world, port, log_m, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import stark_amd as S
+    from stark_amd.distributed import DistributedMerkle, GpuOps
+    torch.cuda.set_device(0)
+    ctx = S.Context(0)
+    m = 1 << log_m
+    full = O.random_elements(world * m, 99)
+    shard = torch.from_numpy(full[rank * m:(rank + 1) * m].copy().view(np.int64)).cuda()
+    dm = DistributedMerkle(GpuOps(ctx))
+    root = dm.commit(shard, m, 32)
+    n = world * m
+    idx = [0, n - 1, 3, n // 2 + 7, 3]
+    proofs = dm.gen_proofs(idx)
+    out_q.put((rank, root, [(p.leaf, p.nodes) for p in proofs]))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,log_m", [(2, 12), (4, 10)])
+def test_distributed_merkle_gpu(world, log_m):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_merkle, args=(r, world, port, log_m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = world << log_m
+    blob = O.random_elements(n, 99).tobytes()
+    idx = [0, n - 1, 3, n // 2 + 7, 3]
+    want_root, want_paths = O.Oracle().merkle(blob, n, 32, idx)
+    for _, root, proofs in res:
+        assert root == want_root
+        for k, (leaf, nodes) in enumerate(proofs):
+            assert leaf == blob[idx[k] * 32:(idx[k] + 1) * 32]
+            assert list(nodes) == want_paths[k]
+
+
 def _worker(rank, world, port, log_n, inverse, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
