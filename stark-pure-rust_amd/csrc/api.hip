@@ -134,8 +134,11 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
-  for (auto& kv : ctx->tw)
+  for (auto& kv : ctx->tw) {
     if (kv.second->d_lo) hipFree(kv.second->d_lo);
+    if (kv.second->d_full) hipFree(kv.second->d_full);
+    if (kv.second->d_full_s) hipFree(kv.second->d_full_s);
+  }
   for (stark_merkle_tree*& t : ctx->trees) {
     stark_merkle_free(t);
     t = nullptr;

@@ -35,6 +35,12 @@ struct Twiddles {
   fe* d_t16_s = nullptr; // t16[i] * n^-1
   uint32_t l16 = 0;
   uint32_t small_off[16] = {0};
+  // Full column-twiddle table of the last pass (built on first use when that
+  // pass's twiddles do not fit t16): full[c R + r] = w^(c r), c < n/R, r < R;
+  // full_s = full * n^-1 for the inverse.  One product per element instead of
+  // the two of lo * hi, for one 32-B coalesced read.
+  fe* d_full = nullptr;
+  fe* d_full_s = nullptr;
   HostFp root;      // the root these tables were built for (Montgomery)
   HostFp inv_n;     // n^-1 (Montgomery)
 };

@@ -14,6 +14,8 @@
 // Data stays canonical, twiddles are Montgomery (see fp_dev.h), so no
 // to/from-Montgomery passes are needed; the inverse's n^-1 is folded into
 // the last pass's store.
+#include <stdlib.h>
+
 #include "internal.h"
 
 namespace stark {
@@ -24,6 +26,7 @@ struct ColTw {
   const fe* t16;    // t16[i] = w^(i * n / 2^l16), i < 2^l16
   const fe* lo;     // lo[i]  = w^i,                i < 2^kb
   const fe* hi;     // hi[i]  = w^(i 2^kb),         i < 2^(log_n - kb)
+  const fe* full;   // last pass only: full[c R + r] = w^(c r) (or null)
   uint32_t l16, kb;
 };
 
@@ -79,7 +82,11 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
       if (log_ns != 0) {
         const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
         fe tw[4];
-        if (lnr <= ct.l16) {
+        if (ct.full != nullptr) {  // the transform's last pass (lnr == log_n) with a full table
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
+        } else if (lnr <= ct.l16) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
@@ -374,6 +381,46 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
   return STARK_OK;
 }
 
+// full[g] = w^(c r) (Montgomery), g = c R + r; times `scale` when given.
+__global__ void full_tw_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint32_t log_r,
+                               uint64_t n, fe scale, int do_scale, fe* __restrict__ out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const uint64_t e = (g >> log_r) * (g & (((uint64_t)1 << log_r) - 1));  // c r < n
+  fe t = fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]);
+  if (do_scale) t = fe_mul(t, scale);
+  fe_store(out + g, t);
+}
+
+// The last pass's full twiddle table, built once per (root, n, direction).
+static stark_status full_table(stark_ctx* ctx, const Twiddles& tw_c, uint32_t log_r, bool scaled, hipStream_t stream,
+                               const fe** out) {
+  Twiddles& tw = const_cast<Twiddles&>(tw_c);  // lazily filled cache entry
+  fe*& slot = scaled ? tw.d_full_s : tw.d_full;
+  if (!slot) {
+    const uint64_t n = (uint64_t)1 << tw.log_n;
+    void* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(fe)) != hipSuccess) {
+      *out = nullptr;  // no room: fall back to the two-level form
+      return STARK_OK;
+    }
+    hipLaunchKernelGGL(full_tw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, tw.d_lo, tw.d_hi,
+                       tw.kb, log_r, n, to_dev(tw.inv_n), scaled ? 1 : 0, (fe*)d);
+    STARK_HIP(ctx, hipGetLastError());
+    slot = (fe*)d;
+  }
+  *out = slot;
+  return STARK_OK;
+}
+
+static bool full_table_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("STARK_NTT_FULL_TW");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
                         bool inverse, hipStream_t stream) {
   if (batch == 0) return STARK_OK;
@@ -409,7 +456,12 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
     // Inverse: n^-1 rides on the last pass's column twiddles (scaled tables)
     // when that pass has them (log_ns > 0), else it is an explicit product.
     const bool fold = inverse && last && log_ns > 0;
-    ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, tw.l16, tw.kb};
+    const fe* full = nullptr;
+    if (last && log_ns > 0 && log_n > tw.l16 && log_n >= 17 && log_n <= 26 && full_table_enabled()) {
+      st = full_table(ctx, tw, lr, fold, stream, &full);
+      if (st != STARK_OK) return st;
+    }
+    ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
     hipLaunchKernelGGL(pass_kernel(lr, persist), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], scale, (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total);
