@@ -132,7 +132,7 @@ char* oracle_mk_r1cs_proof_json(const uint64_t* witness_trace_c, const uint64_t*
   if (steps < 8) steps = 8;                                      /* prove.rs:38-41 */
   const size_t precision = steps * EXTENSION_FACTOR;             /* prove.rs:43 */
   const uint32_t log_precision = log_steps + LOG_EXTENSION_FACTOR;
-  if (log_precision > 28) { *err = 1; return NULL; }             /* prove.rs:51-53 */
+  if (log_precision >= 24) { *err = 1; return NULL; } /* prove.rs:51-53; precision < 2^24 (fri/src/utils.rs:88) */
 
   /* prove.rs:55-69: pad to steps */
   size_t* permuted_indices = (size_t*)malloc(sizeof(size_t) * steps);

@@ -535,7 +535,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   if (os < 5) return STARK_ERR_BAD_LENGTH;  // the reference's steps/log_steps disagree below 8 steps
   const uint32_t log_steps = log2_ceil_ref(os - 1);
   const uint32_t log_prec = log_steps + kLogExtensionFactor;
-  if (log_prec > 28) return STARK_ERR_BAD_LENGTH;
+  // get_pseudorandom_indices(_, precision, ...) asserts precision < 2^24 (fri/src/utils.rs:88), first reached
+  // when r is derived (utils.rs:279); the reference cannot prove larger traces.
+  if (log_prec >= 24) return STARK_ERR_BAD_LENGTH;
   const uint64_t steps = (uint64_t)1 << log_steps, prec = (uint64_t)1 << log_prec;
   const uint64_t skips = prec / steps;
   for (size_t i = 0; i < n_pfi; ++i)

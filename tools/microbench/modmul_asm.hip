@@ -1,7 +1,7 @@
 // fe_mul (per-product asm, fp_dev.h) vs fe_mul_lazy (one asm block,
 // fe_mul_asm.h) throughput, 2 independent chains per thread.
 #include "../../stark-pure-rust_amd/csrc/fp_dev.h"
-#include "../../stark-pure-rust_amd/csrc/fe_mul_asm.h"
+
 #include <cstdio>
 using namespace stark;
 #define ITERS 128
