@@ -13,7 +13,7 @@
  *
  * Parity: the reference commits no golden proof; this
  * restatement is pinned through its parts (oracle.c KATs), by the restated
- * verifier (oracle/verify.py, verify.rs:13-258 + fri.rs:226-404) accepting
+ * verifier (oracle/stark_verify.py, verify.rs:13-258 + fri.rs:226-404) accepting
  * its proofs, and by the committed digests in tests/golden/r1cs_proofs.json.
  */
 #include <stdint.h>

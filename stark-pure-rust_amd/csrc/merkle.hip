@@ -11,10 +11,11 @@
 // Build: one workgroup owns a block of 1024 nodes of its input level: it
 // hashes them (leaf mode: one leaf per node; pair mode: two child digests per
 // node read from the level below), then reduces the block in LDS for the
-// next levels, writing every level to HBM.  While the grid is large only the
-// levels with >= 256 nodes per block (one per thread) are reduced in LDS, so
-// no lane idles through the narrow levels; the top of the tree (< 64K nodes)
-// is finished with up to 10 LDS levels per launch.
+// next levels, writing every level to HBM.  Only the levels with >= 256
+// nodes per block (one per thread) are reduced in LDS, so no lane idles
+// through the narrow levels; the top of the tree (< 64K nodes per level) is
+// finished by merkle_tail_kernel, which spreads each compression over a quad
+// of lanes to cut the per-level latency.
 #include "internal.h"
 #include "blake2s.h"
 
@@ -144,11 +145,11 @@ template <bool LEAF32>
 __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint8_t* __restrict__ leaves,
                                                                       uint32_t leaf_len,
                                                                       const Digest* __restrict__ below,
-                                                                      uint64_t count, uint32_t extra,
-                                                                      LevelPtrs out) {
+                                                                      uint64_t count, uint32_t block,
+                                                                      uint32_t extra, LevelPtrs out) {
   __shared__ __attribute__((aligned(16))) Digest lds[kMerkleBlock];
-  const uint64_t base = (uint64_t)blockIdx.x * kMerkleBlock;
-  const uint32_t here = (uint32_t)((count - base) < kMerkleBlock ? (count - base) : kMerkleBlock);
+  const uint64_t base = (uint64_t)blockIdx.x * block;
+  const uint32_t here = (uint32_t)((count - base) < block ? (count - base) : block);
   for (uint32_t i = threadIdx.x; i < here; i += blockDim.x) {
     const uint64_t node = base + i;
     Digest d;
@@ -175,6 +176,110 @@ __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint
       ++c;
     }
     __syncthreads();
+  }
+}
+
+// ---- Narrow top of the tree: one compression per quad of lanes ----
+//
+// Once a level has fewer nodes than the chip has lanes, a level costs one
+// full compression's latency (a single lane issues ~1100 dependent-ish
+// VALU ops: about 2 us).  Here the 4x4 Blake2s state is spread over the 4
+// lanes of a quad, lane q holding column q (v[q], v[4+q], v[8+q], v[12+q]):
+// the column step is one G per lane, the diagonal step is one G per lane
+// after rotating b, c, d by 1, 2, 3 lanes with quad_perm DPP moves.  Each
+// lane fetches its two message words per step from the children's digests
+// in LDS with a lane-dependent SIGMA index.
+
+// SIGMA row r packed as 16 nibbles (entry i at bits 4i..4i+3).
+__host__ __device__ constexpr uint64_t b2s_sigma_packed(int r) {
+  uint64_t x = 0;
+  for (int i = 0; i < 16; ++i) x |= (uint64_t)b2s_sigma(r, i) << (4 * i);
+  return x;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+// quad_perm controls: lane i reads lane (i + k) & 3.
+constexpr int kQuadRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);
+constexpr int kQuadRot2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);
+constexpr int kQuadRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);
+
+__device__ __forceinline__ void b2s_g(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t x, uint32_t y) {
+  a = a + b + x;
+  d = __builtin_amdgcn_alignbit(d ^ a, d ^ a, 16);
+  c = c + d;
+  b = __builtin_amdgcn_alignbit(b ^ c, b ^ c, 12);
+  a = a + b + y;
+  d = __builtin_amdgcn_alignbit(d ^ a, d ^ a, 8);
+  c = c + d;
+  b = __builtin_amdgcn_alignbit(b ^ c, b ^ c, 7);
+}
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  return q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
+}
+
+// Blake2s(m) of the 64-byte message at msg (LDS, 16 words) on the quad; lane
+// q returns digest words q (lo) and 4 + q (hi).  All 4 lanes must be active.
+__device__ __forceinline__ void hash_pair_quad(const uint32_t* msg, uint32_t q, uint32_t& lo, uint32_t& hi) {
+  const uint32_t h_a = sel4(q, STARK_B2S_H0, STARK_B2S_IV1, STARK_B2S_IV2, STARK_B2S_IV3);
+  const uint32_t h_b = sel4(q, STARK_B2S_IV4, STARK_B2S_IV5, STARK_B2S_IV6, STARK_B2S_IV7);
+  uint32_t a = h_a, b = h_b;
+  uint32_t c = sel4(q, STARK_B2S_IV0, STARK_B2S_IV1, STARK_B2S_IV2, STARK_B2S_IV3);
+  // t = 64 (one final block) into v[12]; final flag into v[14].
+  uint32_t d = h_b ^ sel4(q, 64u, 0u, 0xFFFFFFFFu, 0u);
+  const uint32_t sh = 8 * q;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t sg = b2s_sigma_packed(r);
+    const uint32_t col = (uint32_t)sg, dia = (uint32_t)(sg >> 32);
+    const uint32_t x0 = msg[(col >> sh) & 15], y0 = msg[(col >> (sh + 4)) & 15];
+    const uint32_t x1 = msg[(dia >> sh) & 15], y1 = msg[(dia >> (sh + 4)) & 15];
+    b2s_g(a, b, c, d, x0, y0);
+    b = quad_perm<kQuadRot1>(b);
+    c = quad_perm<kQuadRot2>(c);
+    d = quad_perm<kQuadRot3>(d);
+    b2s_g(a, b, c, d, x1, y1);
+    b = quad_perm<kQuadRot3>(b);
+    c = quad_perm<kQuadRot2>(c);
+    d = quad_perm<kQuadRot1>(d);
+  }
+  lo = h_a ^ a ^ c;
+  hi = h_b ^ b ^ d;
+}
+
+constexpr uint32_t kTailThreads = 1024;
+constexpr uint32_t kTailBlock = kTailThreads / 4;  // input-level nodes per workgroup
+constexpr uint64_t kTailFrom = 65536;              // pair levels narrower than this take the quad kernel
+
+// Pair mode only: input level (count nodes) from `below`, then `extra` more
+// levels in LDS; same LevelPtrs convention as merkle_build_kernel.
+__global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest* __restrict__ below, uint64_t count,
+                                                                   uint32_t extra, LevelPtrs out) {
+  __shared__ __attribute__((aligned(16))) uint32_t msg[2 * kTailBlock * 8];
+  const uint64_t base = (uint64_t)blockIdx.x * kTailBlock;
+  const uint32_t here = (uint32_t)((count - base) < kTailBlock ? (count - base) : kTailBlock);
+  const uint4* src = reinterpret_cast<const uint4*>(below + 2 * base);
+  for (uint32_t i = threadIdx.x; i < here * 4; i += blockDim.x) reinterpret_cast<uint4*>(msg)[i] = src[i];
+  __syncthreads();
+  const uint32_t node = threadIdx.x >> 2, q = threadIdx.x & 3;
+  uint32_t width = here;
+  for (uint32_t k = 0; k <= extra; ++k) {
+    const bool active = node < width;
+    uint32_t lo = 0, hi = 0;
+    if (active) hash_pair_quad(msg + node * 16, q, lo, hi);
+    __syncthreads();
+    if (active) {
+      msg[node * 8 + q] = lo;
+      msg[node * 8 + 4 + q] = hi;
+      uint32_t* g = reinterpret_cast<uint32_t*>(out.lv[k] + (base >> k) + node);
+      g[q] = lo;
+      g[4 + q] = hi;
+    }
+    __syncthreads();
+    width >>= 1;
   }
 }
 
@@ -219,32 +324,46 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   uint64_t count = n;
   bool leaf_mode = true;
   while (true) {
-    // Levels reducible inside a block of min(count, 1024) nodes.
-    const uint64_t blk = count < kMerkleBlock ? count : kMerkleBlock;
-    // Levels reduced in LDS: while the grid is large, only those at least one
-    // node per thread wide (1024 -> 512 -> 256), so no thread idles; the
-    // narrow top of the tree is finished by small launches.
-    const uint32_t max_extra = count >= (uint64_t)kMerkleBlock * 64 ? 2 : 10;
-    uint32_t extra = 0;
-    while ((blk >> (extra + 1)) >= 1 && extra + 1 <= max_extra && level + extra + 1 <= depth) ++extra;
-    LevelPtrs lp;
-    for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
-    const unsigned grid = (unsigned)((count + kMerkleBlock - 1) / kMerkleBlock);
-    const Digest* below = leaf_mode ? nullptr : nodes + level_offset(n, level - 1);
-    const bool leaf32 = leaf_mode && leaf_len == 32 && (((uintptr_t)d_leaves) & 15) == 0;
-    hipLaunchKernelGGL(leaf32 ? merkle_build_kernel<true> : merkle_build_kernel<false>, dim3(grid), dim3(kMerkleThreads), 0, stream,
-                       leaf_mode ? d_leaves : nullptr, (uint32_t)leaf_len, below, count, extra, lp);
-    STARK_HIP(ctx, hipGetLastError());
-    level += extra;
-    count >>= extra;
+    if (!leaf_mode && count < kTailFrom) {
+      // Narrow pair levels: quad kernel, up to 8 levels per launch.
+      const uint64_t blk = count < kTailBlock ? count : kTailBlock;
+      uint32_t extra = 0;
+      while ((blk >> (extra + 1)) >= 1 && level + extra + 1 <= depth) ++extra;
+      LevelPtrs lp;
+      for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
+      const unsigned grid = (unsigned)((count + kTailBlock - 1) / kTailBlock);
+      hipLaunchKernelGGL(merkle_tail_kernel, dim3(grid), dim3(kTailThreads), 0, stream,
+                         (const Digest*)(nodes + level_offset(n, level - 1)), count, extra, lp);
+      STARK_HIP(ctx, hipGetLastError());
+      level += extra;
+      count >>= extra;
+    } else {
+      // Wide levels: one lane per node, blocks of 1024 nodes reduced by 2
+      // more levels in LDS (1024 -> 512 -> 256, one node per thread).  A
+      // narrow leaf level is hashed alone, one node per thread.
+      const bool narrow_leaf = count < kTailFrom;
+      const uint32_t block = narrow_leaf ? kMerkleThreads : kMerkleBlock;
+      const uint64_t blk = count < block ? count : block;
+      const uint32_t max_extra = narrow_leaf ? 0 : 2;
+      uint32_t extra = 0;
+      while ((blk >> (extra + 1)) >= 1 && extra + 1 <= max_extra && level + extra + 1 <= depth) ++extra;
+      LevelPtrs lp;
+      for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
+      const unsigned grid = (unsigned)((count + block - 1) / block);
+      const Digest* below = leaf_mode ? nullptr : nodes + level_offset(n, level - 1);
+      const bool leaf32 = leaf_mode && leaf_len == 32 && (((uintptr_t)d_leaves) & 15) == 0;
+      hipLaunchKernelGGL(leaf32 ? merkle_build_kernel<true> : merkle_build_kernel<false>, dim3(grid),
+                         dim3(kMerkleThreads), 0, stream, leaf_mode ? d_leaves : nullptr, (uint32_t)leaf_len, below,
+                         count, block, extra, lp);
+      STARK_HIP(ctx, hipGetLastError());
+      level += extra;
+      count >>= extra;
+    }
     if (level == depth) break;
     // Next launch starts by hashing pairs of the current top level.
     ++level;
     count >>= 1;
     leaf_mode = false;
-    if (level == depth && count == 1) {
-      // A single pair remains: handled by a 1-node launch.
-    }
   }
   t->n = n;
   t->leaf_len = leaf_len;
