@@ -7,55 +7,86 @@
 
 namespace stark {
 
-constexpr uint32_t kInvChunk = 32;
-
-// Montgomery constants used below (Montgomery images):
-//   r2 = R^2 mod p  -> montmul(x_canon, r2) = x in Montgomery form
+// Batch inverse kernels.  A canonical input x < p is read as the Montgomery
+// image of x' = x R^-1, so no conversion is needed on the way in: the
+// products and inverses live in the x' Montgomery domain, and inv(x') in
+// Montgomery form is x^-1 R^2, so one montmul by R^-1 (canonical) gives the
+// canonical x^-1 on the way out.
 struct MontConsts {
-  fe r2;   // R^2 mod p as limbs (i.e. Montgomery image of R)
-  fe one;  // Montgomery image of 1 (= R mod p)
+  fe r2;    // R^2 mod p: montmul(x, r2) = Montgomery image of canonical x
+  fe one;   // Montgomery image of 1 (= R mod p)
+  fe rinv;  // R^-1 mod p as plain limbs
 };
 
-// Phase 1: chunk c of kInvChunk elements -> prefix products (Montgomery,
-// zeros skipped) into pref, chunk product into tot[c].  MONT_IN: the input
-// already holds Montgomery images (the chunk products of a lower level).
-template <bool MONT_IN, uint32_t CHUNK>
-__global__ void inv_prefix_kernel(const fe* __restrict__ v, uint64_t n, fe* __restrict__ pref, fe* __restrict__ tot,
-                                  MontConsts mc) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t lo = c * CHUNK;
-  if (lo >= n) return;
-  const uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
-  fe acc = mc.one;
-  for (uint64_t i = lo; i < hi; ++i) {
-    pref[i] = acc;  // product of the non-zero elements before i (exclusive)
-    const fe x = fe_load(v + i);
-    if (!fe_is_zero(x)) acc = fe_mul(acc, MONT_IN ? x : fe_mul(x, mc.r2));
+constexpr uint32_t kInvThreads = 256;
+
+// Hillis-Steele inclusive product scans of the workgroup's 256 values, both
+// directions at once; returns the product of every value but this thread's.
+__device__ __forceinline__ fe wg_others_product(fe t, const fe& one, fe* q, fe* sfx, fe* total) {
+  const uint32_t j = threadIdx.x;
+  fe pq = t, ps = t;
+  q[j] = pq;
+  sfx[j] = ps;
+  __syncthreads();
+  for (uint32_t off = 1; off < kInvThreads; off <<= 1) {
+    const fe a = j >= off ? q[j - off] : one;
+    const fe b = j + off < kInvThreads ? sfx[j + off] : one;
+    __syncthreads();
+    pq = fe_mul(pq, a);
+    ps = fe_mul(ps, b);
+    q[j] = pq;
+    sfx[j] = ps;
+    __syncthreads();
   }
-  tot[c] = acc;
+  *total = q[kInvThreads - 1];
+  const fe before = j ? q[j - 1] : one;
+  const fe after = j + 1 < kInvThreads ? sfx[j + 1] : one;
+  return fe_mul(before, after);
 }
 
-// Phase 3: walk each chunk backwards (poly_utils.rs:55-67 order).  `tot`
-// holds the Montgomery inverse of each chunk product.  Output canonical, or
-// Montgomery when MONT_IN.
-template <bool MONT_IN, uint32_t CHUNK>
-__global__ void inv_back_kernel(const fe* __restrict__ v, uint64_t n, const fe* __restrict__ pref,
-                                const fe* __restrict__ tot, fe* __restrict__ out, MontConsts mc) {
-  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t lo = c * CHUNK;
+// Up pass: thread g owns elements [g*chunk, (g+1)*chunk): exclusive prefix
+// products of its non-zero elements into pref, then the workgroup scan gives
+// others[g] (the product of the other threads' chunks) and wg_tot[block].
+__global__ __launch_bounds__(kInvThreads) void inv_up_kernel(const fe* __restrict__ v, uint64_t n, uint32_t chunk,
+                                                             fe* __restrict__ pref, fe* __restrict__ others,
+                                                             fe* __restrict__ wg_tot, MontConsts mc) {
+  __shared__ fe q[kInvThreads], sfx[kInvThreads];
+  const uint64_t g = (uint64_t)blockIdx.x * kInvThreads + threadIdx.x;
+  const uint64_t lo = g * chunk;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  fe acc = mc.one;
+  for (uint64_t i = lo; i < hi; ++i) {
+    pref[i] = acc;
+    const fe x = fe_load(v + i);
+    if (!fe_is_zero(x)) acc = fe_mul(acc, x);
+  }
+  fe total;
+  others[g] = wg_others_product(acc, mc.one, q, sfx, &total);
+  if (threadIdx.x == 0) wg_tot[blockIdx.x] = total;
+}
+
+// Down pass: wg_inv[block] = inverse of the workgroup total, so the inverse
+// of this thread's chunk product is wg_inv * others; then the chunk is walked
+// backwards (poly_utils.rs:55-67 order).  OUT_CANON: level 0, canonical out.
+template <bool OUT_CANON>
+__global__ __launch_bounds__(kInvThreads) void inv_down_kernel(const fe* __restrict__ v, uint64_t n, uint32_t chunk,
+                                                               const fe* __restrict__ pref,
+                                                               const fe* __restrict__ others,
+                                                               const fe* __restrict__ wg_inv, fe* __restrict__ out,
+                                                               MontConsts mc) {
+  const uint64_t g = (uint64_t)blockIdx.x * kInvThreads + threadIdx.x;
+  const uint64_t lo = g * chunk;
   if (lo >= n) return;
-  const uint64_t hi = lo + CHUNK < n ? lo + CHUNK : n;
-  fe inv = tot[c];  // Montgomery
-  fe unit = fe_zero();
-  unit.w[0] = 1;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  fe inv = fe_mul(wg_inv[blockIdx.x], others[g]);
   for (uint64_t i = hi; i-- > lo;) {
     const fe x = fe_load(v + i);
     if (fe_is_zero(x)) {
       fe_store(out + i, fe_zero());
     } else {
-      const fe r = fe_mul(pref[i], inv);  // Montgomery x^-1
-      fe_store(out + i, MONT_IN ? r : fe_mul(r, unit));
-      inv = fe_mul(inv, MONT_IN ? x : fe_mul(x, mc.r2));
+      const fe r = fe_mul(pref[i], inv);
+      fe_store(out + i, OUT_CANON ? fe_mul(r, mc.rinv) : r);
+      inv = fe_mul(inv, x);
     }
   }
 }
@@ -85,72 +116,109 @@ __global__ void powers_kernel(const fe* __restrict__ lo, const fe* __restrict__ 
 MontConsts mont_consts() {
   const FieldHost& F = FieldHost::get();
   MontConsts mc;
-  // Montgomery image of R is R^2 mod p: from_canonical(R mod p).
+  mc.one = to_dev(F.one());
   uint64_t rmodp[4];
-  HostFp one = F.one();  // Montgomery image of 1 = R mod p (as limbs)
+  const HostFp one = F.one();
   memcpy(rmodp, one.v, 32);
-  mc.r2 = to_dev(F.from_canonical(rmodp));
-  mc.one = to_dev(one);
+  mc.r2 = to_dev(F.from_canonical(rmodp));  // Montgomery image of R
+  // R^-1 mod p: canonical form of inv(Montgomery image of R).
+  uint64_t rinv[4];
+  F.to_canonical(F.inv(F.from_canonical(rmodp)), rinv);
+  HostFp t;
+  memcpy(t.v, rinv, 32);
+  mc.rinv = to_dev(t);
   return mc;
 }
 
-// Batch inverse (0 -> 0), the tree form of multi_inv (poly_utils.rs:38-70):
-// chunk products of 32 inputs, then of 16 chunk products per level until at
-// most 16 remain.  Those few are inverted on the host (one Fermat inversion
-// there takes microseconds; on one GPU lane it is a ~250-product dependent
-// chain, a quarter millisecond), and the inverses flow back down the levels.
-constexpr uint32_t kInvChunkUp = 16;
+// Batch inverse (0 -> 0), the tree form of multi_inv (poly_utils.rs:38-70).
+// Each level turns n_i values into one product per workgroup (chunks of
+// `chunk` per thread, then a product scan over the 256 threads), until at
+// most 16 remain; those are inverted on the host (one Fermat inversion there
+// takes microseconds, on one GPU lane it is a ~250-product dependent chain),
+// and the inverses flow back down.  Small levels use one element per thread
+// so the dependent chain per level is ~10 products; large ones use up to 32
+// per thread so the scan costs < 1 product per element.
 constexpr uint64_t kInvTop = 16;
+
+static uint32_t inv_chunk_for(uint64_t n) {
+  uint32_t c = 1;
+  while (c < 32 && n / c > ((uint64_t)1 << 17)) c <<= 1;
+  return c;
+}
 
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s) {
   if (n == 0) return STARK_OK;
-  // Level sizes: c[0] = ceil(n / 32) chunk products, c[i] = ceil(c[i-1] / 16).
-  std::vector<uint64_t> c{(n + kInvChunk - 1) / kInvChunk};
-  while (c.back() > kInvTop) c.push_back((c.back() + kInvChunkUp - 1) / kInvChunkUp);
-  // Scratch: pref0[n], then per level i: tot_i[c_i], inv_i[c_i], pref_{i+1}[c_i] (for i < top).
-  size_t total = n;
-  for (size_t i = 0; i < c.size(); ++i) total += 3 * c[i];
+  struct Level {
+    uint64_t n;
+    uint32_t chunk, wgs;
+    const fe* in;
+    fe *out, *pref, *others, *tot;
+  };
+  std::vector<Level> lv;
+  uint64_t m = n;
+  size_t total = 0;
+  while (m > kInvTop || lv.empty()) {
+    Level L{};
+    L.n = m;
+    L.chunk = inv_chunk_for(m);
+    const uint64_t threads = (m + L.chunk - 1) / L.chunk;
+    L.wgs = (uint32_t)((threads + kInvThreads - 1) / kInvThreads);
+    total += m + (uint64_t)L.wgs * kInvThreads + 2 * (uint64_t)L.wgs;  // pref, others, tot, out of the next level
+    lv.push_back(L);
+    m = L.wgs;
+  }
   stark_status st = ensure_buf(ctx, ctx->io2, total * sizeof(fe));
   if (st != STARK_OK) return st;
-  fe* pref0 = (fe*)ctx->io2.ptr;
-  std::vector<fe*> tot(c.size()), inv(c.size()), pref(c.size());
-  fe* at = pref0 + n;
-  for (size_t i = 0; i < c.size(); ++i) {
-    tot[i] = at;
-    inv[i] = at + c[i];
-    pref[i] = at + 2 * c[i];  // prefixes of level i+1's chunks over tot[i]
-    at += 3 * c[i];
+  fe* at = (fe*)ctx->io2.ptr;
+  for (size_t i = 0; i < lv.size(); ++i) {
+    Level& L = lv[i];
+    L.in = i ? lv[i - 1].tot : d_in;
+    L.out = i ? nullptr : d_out;
+    L.pref = at;
+    at += L.n;
+    L.others = at;
+    at += (uint64_t)L.wgs * kInvThreads;
+    L.tot = at;
+    at += L.wgs;
   }
+  // out of level i (i >= 1) = inverses of the totals of level i - 1.
+  for (size_t i = 1; i < lv.size(); ++i) {
+    lv[i].out = at;
+    at += lv[i].n;
+  }
+  fe* top_inv = at;  // inverses of the last level's totals
   const MontConsts mc = mont_consts();
-  auto blocks = [](uint64_t chunks) { return (unsigned)((chunks + 255) / 256); };
-  hipLaunchKernelGGL((inv_prefix_kernel<false, kInvChunk>), dim3(blocks(c[0])), dim3(256), 0, s, d_in, n, pref0, tot[0],
-                     mc);
-  for (size_t i = 1; i < c.size(); ++i)
-    hipLaunchKernelGGL((inv_prefix_kernel<true, kInvChunkUp>), dim3(blocks(c[i])), dim3(256), 0, s,
-                       (const fe*)tot[i - 1], c[i - 1], pref[i - 1], tot[i], mc);
+  for (const Level& L : lv)
+    hipLaunchKernelGGL(inv_up_kernel, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk, L.pref, L.others,
+                       L.tot, mc);
   STARK_HIP(ctx, hipGetLastError());
-  // Top level: at most 16 non-zero Montgomery products, inverted on the host.
-  const size_t top = c.size() - 1;
+  // Top: at most 16 non-zero Montgomery products, inverted on the host.
+  const Level& T = lv.back();
   uint8_t* pinned = nullptr;
   st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
   if (st != STARK_OK) return st;
   fe* h_top = (fe*)(pinned + 2560);  // pinned slot 1 layout: [2560, 3072) batch-inverse top level
-  STARK_HIP(ctx, hipMemcpyAsync(h_top, tot[top], c[top] * sizeof(fe), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipMemcpyAsync(h_top, T.tot, T.wgs * sizeof(fe), hipMemcpyDeviceToHost, s));
   STARK_HIP(ctx, hipStreamSynchronize(s));
   {
     const FieldHost& F = FieldHost::get();
-    for (uint64_t i = 0; i < c[top]; ++i) {
+    for (uint32_t i = 0; i < T.wgs; ++i) {
       HostFp x;
       for (int k = 0; k < 4; ++k) x.v[k] = (uint64_t)h_top[i].w[2 * k] | ((uint64_t)h_top[i].w[2 * k + 1] << 32);
       h_top[i] = to_dev(F.inv(x));  // Montgomery in, Montgomery out; products are never zero
     }
   }
-  STARK_HIP(ctx, hipMemcpyAsync(inv[top], h_top, c[top] * sizeof(fe), hipMemcpyHostToDevice, s));
-  for (size_t i = top; i >= 1; --i)
-    hipLaunchKernelGGL((inv_back_kernel<true, kInvChunkUp>), dim3(blocks(c[i])), dim3(256), 0, s,
-                       (const fe*)tot[i - 1], c[i - 1], (const fe*)pref[i - 1], (const fe*)inv[i], inv[i - 1], mc);
-  hipLaunchKernelGGL((inv_back_kernel<false, kInvChunk>), dim3(blocks(c[0])), dim3(256), 0, s, d_in, n,
-                     (const fe*)pref0, (const fe*)inv[0], d_out, mc);
+  STARK_HIP(ctx, hipMemcpyAsync(top_inv, h_top, T.wgs * sizeof(fe), hipMemcpyHostToDevice, s));
+  for (size_t i = lv.size(); i-- > 0;) {
+    const Level& L = lv[i];
+    const fe* wg_inv = i + 1 < lv.size() ? lv[i + 1].out : top_inv;
+    if (i == 0)
+      hipLaunchKernelGGL(inv_down_kernel<true>, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk,
+                         (const fe*)L.pref, (const fe*)L.others, wg_inv, L.out, mc);
+    else
+      hipLaunchKernelGGL(inv_down_kernel<false>, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk,
+                         (const fe*)L.pref, (const fe*)L.others, wg_inv, L.out, mc);
+  }
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
 }

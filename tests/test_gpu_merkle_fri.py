@@ -155,6 +155,21 @@ def test_multi_inv(ctx, oracle):
     assert np.array_equal(ctx.multi_inv(v[:1]), oracle.multi_inv(v[:1]))
 
 
+@pytest.mark.parametrize("n", [2, 16, 17, 255, 256, 257, 4097, (1 << 16) + 1, (1 << 18) + 3, (1 << 22) + 7])
+def test_multi_inv_sizes(ctx, oracle, n):
+    """Every level shape of the workgroup-scan tree: one level straight to the host top, several
+    levels, 1..32 elements per thread, partial workgroups; zeros map to zero (poly_utils.rs:38-70)."""
+    v = O.random_elements(n, 40 + n % 97)
+    v[::7] = 0
+    v[-1] = 0
+    assert np.array_equal(ctx.multi_inv(v), oracle.multi_inv(v))
+
+
+def test_multi_inv_all_zero(ctx, oracle):
+    v = np.zeros((1000, 4), dtype=np.uint64)
+    assert np.array_equal(ctx.multi_inv(v), oracle.multi_inv(v))
+
+
 def test_eval_poly_multi(ctx, oracle):
     poly = O.random_elements(37, 5)
     xs = O.random_elements(5000, 6)
