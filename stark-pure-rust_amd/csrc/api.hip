@@ -42,7 +42,8 @@ stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
     ctx->pinned[slot] = nullptr;
     ctx->pinned_bytes[slot] = 0;
     const size_t want = bytes < 4096 ? 4096 : bytes;
-    STARK_HIP(ctx, hipHostMalloc(&ctx->pinned[slot], want, hipHostMallocDefault));
+    // Coherent: kernels read and write this memory directly (zero-copy gathers).
+    STARK_HIP(ctx, hipHostMalloc(&ctx->pinned[slot], want, hipHostMallocCoherent));
     ctx->pinned_bytes[slot] = want;
   }
   *out = ctx->pinned[slot];
@@ -147,7 +148,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (void* p : ctx->pinned)
     if (p) hipHostFree(p);
   ctx->fri_trees.clear();
-  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->fri_misc, &ctx->gather_dev})
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->fri_misc})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -186,19 +186,20 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
     lv[i].out = at;
     at += lv[i].n;
   }
-  fe* top_inv = at;  // inverses of the last level's totals
+  // Top: at most 16 non-zero Montgomery products, written by the last up
+  // kernel straight into the pinned (coherent) host slot, inverted there on
+  // the host and read back by the first down kernel, with no copies.
+  uint8_t* pinned = nullptr;
+  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
+  if (st != STARK_OK) return st;
+  fe* h_top = (fe*)(pinned + 2560);  // pinned slot 1 layout: [2560, 3072) batch-inverse top level
+  lv.back().tot = h_top;
   const MontConsts mc = mont_consts();
   for (const Level& L : lv)
     hipLaunchKernelGGL(inv_up_kernel, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk, L.pref, L.others,
                        L.tot, mc);
   STARK_HIP(ctx, hipGetLastError());
-  // Top: at most 16 non-zero Montgomery products, inverted on the host.
   const Level& T = lv.back();
-  uint8_t* pinned = nullptr;
-  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
-  if (st != STARK_OK) return st;
-  fe* h_top = (fe*)(pinned + 2560);  // pinned slot 1 layout: [2560, 3072) batch-inverse top level
-  STARK_HIP(ctx, hipMemcpyAsync(h_top, T.tot, T.wgs * sizeof(fe), hipMemcpyDeviceToHost, s));
   STARK_HIP(ctx, hipStreamSynchronize(s));
   {
     const FieldHost& F = FieldHost::get();
@@ -208,10 +209,9 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
       h_top[i] = to_dev(F.inv(x));  // Montgomery in, Montgomery out; products are never zero
     }
   }
-  STARK_HIP(ctx, hipMemcpyAsync(top_inv, h_top, T.wgs * sizeof(fe), hipMemcpyHostToDevice, s));
   for (size_t i = lv.size(); i-- > 0;) {
     const Level& L = lv[i];
-    const fe* wg_inv = i + 1 < lv.size() ? lv[i + 1].out : top_inv;
+    const fe* wg_inv = i + 1 < lv.size() ? lv[i + 1].out : h_top;
     if (i == 0)
       hipLaunchKernelGGL(inv_down_kernel<true>, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk,
                          (const fe*)L.pref, (const fe*)L.others, wg_inv, L.out, mc);

@@ -151,7 +151,6 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   if (st != STARK_OK) return st;
   p->h_roots = pinned + kFriRootsOff;
   fe* d_sx = (fe*)ctx->fri_misc.ptr;
-  uint32_t* d_roots = (uint32_t*)(d_sx + 16);
   while (ctx->fri_trees.size() < layers + 1) {
     stark_merkle_tree* t = nullptr;
     st = stark_merkle_new(ctx, &t);
@@ -193,9 +192,10 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   if (layers) {
     RootPtrs rp;
     for (size_t l = 0; l <= layers; ++l) rp.p[l] = (const uint32_t*)merkle_root_dev(trees[l]);
-    hipLaunchKernelGGL(collect_roots_kernel, dim3(1), dim3(128), 0, s, rp, (uint32_t)(layers + 1), d_roots);
+    // Straight into the pinned (coherent) host slot: no copy behind it.
+    hipLaunchKernelGGL(collect_roots_kernel, dim3(1), dim3(128), 0, s, rp, (uint32_t)(layers + 1),
+                       (uint32_t*)p->h_roots);
     STARK_HIP(ctx, hipGetLastError());
-    STARK_HIP(ctx, hipMemcpyAsync((void*)p->h_roots, d_roots, 32 * (layers + 1), hipMemcpyDeviceToHost, s));
   }
   *out = std::move(p);
   return STARK_OK;

@@ -2,6 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
 
 #include <map>
 #include <memory>
@@ -14,6 +18,35 @@
 #include "fp_host.h"
 
 namespace stark {
+
+// STARK_PROFILE=1: host-side phase timings of a call on stderr (what the
+// host waits on between the device phases; the kernels themselves are timed
+// with rocprofv3).
+struct PhaseClock {
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  explicit PhaseClock(const char* what) : on(enabled()) {
+    if (on) {
+      t0 = last = std::chrono::steady_clock::now();
+      fprintf(stderr, "[stark] %s\n", what);
+    }
+  }
+  static bool enabled() {
+    static const bool e = [] {
+      const char* v = getenv("STARK_PROFILE");
+      return v && v[0] && v[0] != '0';
+    }();
+    return e;
+  }
+  void mark(const char* phase) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[stark]   %-28s %8.1f us (at %8.1f)\n", phase,
+            std::chrono::duration<double, std::micro>(now - last).count(),
+            std::chrono::duration<double, std::micro>(now - t0).count());
+    last = now;
+  }
+};
 
 // Device buffer owned by a context.
 struct DevBuf {
@@ -63,7 +96,6 @@ struct stark_ctx {
   stark::DevBuf fri_misc;                     // per-layer special_x (device transcript)
   void* pinned[2] = {nullptr, nullptr};       // pinned host scratch (ctx_pinned)
   size_t pinned_bytes[2] = {0, 0};
-  stark::DevBuf gather_dev;                   // merkle_gather_batch device region
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
 };

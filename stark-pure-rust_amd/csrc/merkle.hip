@@ -416,10 +416,57 @@ stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* i
   return STARK_OK;
 }
 
-// Many gathers with one upload and one download: the indices go through the
-// context's pinned scratch, every request's leaves and siblings land in one
-// device region, and a single D2H brings all of them back (pageable copies
-// of many small buffers each cost a staged, synchronous round trip).
+// Many gathers in one launch, zero-copy: the kernel reads the indices from
+// and writes every request's leaves and siblings straight into the context's
+// pinned (coherent) host scratch, so the whole opening phase is one launch
+// and one synchronisation (per-request launches and a separate D2H copy cost
+// ~7 us and ~70 us of engine latency each).
+constexpr uint32_t kGatherMaxReq = 64;  // requests per launch (descriptors travel as kernel arguments)
+
+struct GatherDesc {
+  const uint8_t* leaves;
+  const Digest* nodes;
+  uint64_t n;        // leaves
+  uint64_t out_off;  // byte offset of this request's region in the output
+  uint32_t first;    // first proof (block) of this request
+  uint32_t k, leaf_len, depth;
+};
+struct GatherDescs {
+  GatherDesc d[kGatherMaxReq];
+};
+
+// Block p = one proof: leaf bytes then the depth siblings ((idx >> d) ^ 1 at
+// level d, leaf -> root).  Region layout per request: k leaves (padded to 16
+// bytes), then k * depth digests.
+__global__ __launch_bounds__(64) void merkle_gather_multi_kernel(GatherDescs g, uint32_t n_req,
+                                                                  const uint64_t* __restrict__ idx,
+                                                                  uint8_t* __restrict__ out) {
+  const uint32_t p = blockIdx.x;
+  uint32_t r = 0;
+  while (r + 1 < n_req && g.d[r + 1].first <= p) ++r;
+  const GatherDesc& q = g.d[r];
+  const uint32_t i = p - q.first;
+  const uint64_t id = idx[p];
+  uint8_t* region = out + q.out_off;
+  uint8_t* leaf_out = region + (uint64_t)i * q.leaf_len;
+  const uint8_t* leaf_in = q.leaves + id * q.leaf_len;
+  if ((q.leaf_len & 3) == 0 && (((uintptr_t)leaf_in | (uintptr_t)leaf_out) & 3) == 0) {
+    for (uint32_t w = threadIdx.x; w < q.leaf_len / 4; w += blockDim.x)
+      reinterpret_cast<uint32_t*>(leaf_out)[w] = reinterpret_cast<const uint32_t*>(leaf_in)[w];
+  } else {
+    for (uint32_t b = threadIdx.x; b < q.leaf_len; b += blockDim.x) leaf_out[b] = leaf_in[b];
+  }
+  Digest* node_out = reinterpret_cast<Digest*>(region + ((q.k * (uint64_t)q.leaf_len + 15) & ~(uint64_t)15)) +
+                     (uint64_t)i * q.depth;
+  for (uint32_t d = threadIdx.x; d < q.depth; d += blockDim.x) {
+    const uint64_t off = 2 * q.n - 2 * (q.n >> d);  // first node of level d (n a power of two)
+    const uint4* src = reinterpret_cast<const uint4*>(q.nodes + off + ((id >> d) ^ 1));
+    uint4* dst = reinterpret_cast<uint4*>(node_out + d);
+    dst[0] = src[0];
+    dst[1] = src[1];
+  }
+}
+
 stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream) {
   size_t n_idx = 0, out_bytes = 0;
   std::vector<size_t> off(reqs.size());
@@ -432,36 +479,46 @@ stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& r
     out_bytes += ((q.k * q.t->leaf_len + 15) & ~(size_t)15) + q.k * q.t->depth * sizeof(Digest);
   }
   if (n_idx == 0) return STARK_OK;
+  if (n_idx > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
   const size_t idx_bytes = n_idx * sizeof(uint64_t);
-  stark_status st = ensure_buf(ctx, ctx->gather_dev, idx_bytes + out_bytes);
-  if (st != STARK_OK) return st;
   uint8_t* host = nullptr;
-  st = ctx_pinned(ctx, 0, idx_bytes + out_bytes, (void**)&host);
+  stark_status st = ctx_pinned(ctx, 0, idx_bytes + out_bytes, (void**)&host);
   if (st != STARK_OK) return st;
   uint64_t* h_idx = (uint64_t*)host;
   uint8_t* h_out = host + idx_bytes;
-  uint8_t* d_base = (uint8_t*)ctx->gather_dev.ptr;
-  uint64_t* d_idx = (uint64_t*)d_base;
-  uint8_t* d_out = d_base + idx_bytes;
   size_t at = 0;
   for (const GatherReq& q : reqs) {
     for (size_t i = 0; i < q.k; ++i) h_idx[at + i] = q.idx[i];
     at += q.k;
   }
-  STARK_HIP(ctx, hipMemcpyAsync(d_idx, h_idx, idx_bytes, hipMemcpyHostToDevice, stream));
-  at = 0;
-  for (size_t r = 0; r < reqs.size(); ++r) {
-    const GatherReq& q = reqs[r];
-    if (q.k == 0) continue;
-    uint8_t* leaf = d_out + off[r];
-    Digest* node = (Digest*)(leaf + ((q.k * q.t->leaf_len + 15) & ~(size_t)15));
-    hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)q.k), dim3(64), 0, stream, q.t->d_leaves,
-                       (uint32_t)q.t->leaf_len, (const Digest*)q.t->nodes.ptr, (uint64_t)q.t->n, q.t->depth,
-                       (const uint64_t*)(d_idx + at), (uint32_t)q.k, leaf, node);
-    STARK_HIP(ctx, hipGetLastError());
-    at += q.k;
+  // Launches of up to kGatherMaxReq requests; proofs are numbered across the batch.
+  size_t r0 = 0, p0 = 0;
+  while (r0 < reqs.size()) {
+    GatherDescs g;
+    uint32_t m = 0, proofs = 0;
+    size_t r = r0;
+    for (; r < reqs.size() && m < kGatherMaxReq; ++r) {
+      const GatherReq& q = reqs[r];
+      if (q.k == 0) continue;
+      GatherDesc& d = g.d[m++];
+      d.leaves = q.t->d_leaves;
+      d.nodes = (const Digest*)q.t->nodes.ptr;
+      d.n = q.t->n;
+      d.out_off = off[r];
+      d.first = proofs;
+      d.k = (uint32_t)q.k;
+      d.leaf_len = (uint32_t)q.t->leaf_len;
+      d.depth = q.t->depth;
+      proofs += (uint32_t)q.k;
+    }
+    if (m) {
+      hipLaunchKernelGGL(merkle_gather_multi_kernel, dim3(proofs), dim3(64), 0, stream, g, m,
+                         (const uint64_t*)(h_idx + p0), h_out);
+      STARK_HIP(ctx, hipGetLastError());
+    }
+    p0 += proofs;
+    r0 = r;
   }
-  STARK_HIP(ctx, hipMemcpyAsync(h_out, d_out, out_bytes, hipMemcpyDeviceToHost, stream));
   STARK_HIP(ctx, hipStreamSynchronize(stream));
   for (size_t r = 0; r < reqs.size(); ++r) {
     const GatherReq& q = reqs[r];

@@ -528,6 +528,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
                                const uint64_t* flag2, const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
                                stark_r1cs_proof** out) {
+  PhaseClock clk("mk_r1cs_proof");
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
   // prove.rs:30-53
@@ -632,6 +633,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
+  clk.mark("setup + uploads enqueued");
   STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
                      (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
@@ -728,8 +730,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
 
   // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367), enqueued behind the rest.
   FriPendingPtr fri_pending;
+  clk.mark("prover kernels enqueued");
   STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending));
+  clk.mark("FRI kernels enqueued");
   STARK_HIP(ctx, hipStreamSynchronize(s));  // the proof's one wait for the device
+  clk.mark("device wait");
   if (h_tr->err) {
     ctx->last_error = (h_tr->err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
                                       : "invalid B: boundary value mismatch (utils.rs:477-524)";
@@ -757,6 +762,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                   {m_tree, aug.data(), (size_t)4 * kSpotChecks, m_leaves.data(), m_nodes.data()}};
   stark_fri_proof* fri = nullptr;
   STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
+  clk.mark("indices + gather batch");
   std::unique_ptr<stark_fri_proof, void (*)(stark_fri_proof*)> fri_guard(fri, stark_fri_proof_free);
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
   std::string& o = proof->json;
@@ -775,6 +781,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   o += ",\"fri_proof\":";
   fri_proof_json_string(fri, o);
   o += "}";
+  clk.mark("proof JSON");
   *out = proof.release();
   return STARK_OK;
 }

@@ -113,6 +113,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
                                     stark_r1cs_trace** out) {
   if (!r1cs || !wtns || !out) return STARK_ERR_BAD_ARG;
   *out = nullptr;
+  PhaseClock clk("r1cs trace build");
   const FieldHost& F = FieldHost::get();
   // ---- read_r1cs (reader.rs:4-89): header section, then constraints, in that order.
   Cursor c{r1cs, r1cs_len};
@@ -147,6 +148,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
     }
   if (!c.ok || n_wires == 0) return STARK_ERR_BAD_ARG;
 
+  clk.mark("read_r1cs");
   // ---- read_witness (r1cs-stark/src/reader.rs:7-42)
   Cursor w{wtns, wtns_len};
   if (w.u32() != 1936618615u) return STARK_ERR_BAD_ARG;  // "wtns"
@@ -163,6 +165,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   for (uint32_t i = 0; i < n_wit; ++i) witness[i] = F.from_bytes_le(w.raw(field_size), field_size);
   if (n_wit < n_wires || !FieldHost::eq(witness[0], F.one())) return STARK_ERR_BAD_ARG;  // run.rs:358
 
+  clk.mark("read_witness");
   auto t = std::make_unique<stark_r1cs_trace>();
   t->n_constraints = n_constraints;
   t->n_wires = n_wires;
@@ -193,6 +196,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
     F.to_canonical(witness[i], cc);
     memcpy(wcan[i].v, cc, 32);
   }
+  clk.mark("slot bases");
   t->witness_trace.alloc(4 * os);
   t->computational_trace.alloc(4 * os);
   t->coefficients.alloc(4 * os);
@@ -229,6 +233,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
     fill(0, (uint32_t)((uint64_t)n_constraints / nt));
     for (auto& x : th) x.join();
   }
+  clk.mark("slot fill (threads)");
   // ---- calc_flags (run.rs:283-308): flag0 = 1, flag1 = 0 at each constraint's
   // first slot (in all three thirds), flag2 = 1 at its last slot.
   t->flags.assign(3 * os, 0);
@@ -242,6 +247,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
     f1[k] = f1[k + a_len] = f1[k + 2 * a_len] = 0;
   }
   for (uint32_t ci = 0; ci < n_constraints; ++ci) f2[base[ci + 1] - 1] = 1;
+  clk.mark("flags");
   // ---- wire uses in push order (run.rs:160, 195, 230: factor A's slots, then B's, then C's per
   // constraint), as trace positions a_len * factor + slot; counting sort by wire.
   std::vector<uint64_t> use_off((size_t)n_wires + 1, 0);
@@ -259,6 +265,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   for (size_t wi = 0; wi < n_wires; ++wi) use_off[wi + 1] += use_off[wi];
   std::vector<uint64_t> uses(os), cur(use_off.begin(), use_off.end() - 1);
   for_each_use([&](size_t wire, size_t pos) { uses[cur[wire]++] = pos; });
+  clk.mark("wire uses (counting sort)");
   // ---- permuted indices (run.rs:388-401): a cycle through every wire's uses.
   t->permuted_indices.alloc(os);
   for (size_t wi = 0; wi < n_wires; ++wi) {
@@ -276,6 +283,7 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
       t->public_first_indices.push_back(wi);
       t->public_first_indices.push_back(uses[use_off[wi]]);
     }
+  clk.mark("permutation + public firsts");
   *out = t.release();
   return STARK_OK;
 }
