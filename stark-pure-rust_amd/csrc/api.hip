@@ -1,7 +1,11 @@
 // C ABI: contexts, buffers, NTT entry points, Blake2s and the index sampler.
 // Each extern "C" function cites the reference item it replaces in
 // include/stark_hip.h.
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <string.h>
 
 #include "internal.h"
@@ -32,6 +36,77 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   b.bytes = bytes;
   return STARK_OK;
 }
+
+namespace {
+
+class HostWorkers {
+ public:
+  static HostWorkers& get() {
+    static HostWorkers* w = new HostWorkers();  // never destroyed: workers live for the process
+    return *w;
+  }
+  unsigned threads() const { return (unsigned)workers_ + 1; }
+  void run(unsigned n, const std::function<void(unsigned)>& fn) {
+    if (n == 0) return;
+    if (n == 1 || workers_ == 0) {
+      for (unsigned k = 0; k < n; ++k) fn(k);
+      return;
+    }
+    std::lock_guard<std::mutex> serial(call_);  // one parallel call at a time
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &fn;
+      n_ = n;
+      next_.store(1);
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    drain();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  HostWorkers() {
+    unsigned hw = std::thread::hardware_concurrency();
+    hw = hw < 1 ? 1 : (hw > 16 ? 16 : hw);
+    workers_ = hw - 1;
+    for (unsigned i = 0; i < workers_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void drain() {
+    for (unsigned k; (k = next_.fetch_add(1)) < n_;) {
+      (*job_)(k);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  size_t workers_ = 0;
+  std::mutex call_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned n_ = 0, pending_ = 0;
+  std::atomic<unsigned> next_{0};
+  uint64_t gen_ = 0;
+};
+
+}  // namespace
+
+unsigned host_threads() { return HostWorkers::get().threads(); }
+void host_parallel(unsigned n, const std::function<void(unsigned)>& fn) { HostWorkers::get().run(n, fn); }
 
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
   if (ctx->pinned_bytes[slot] < bytes) {

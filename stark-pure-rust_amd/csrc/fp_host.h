@@ -127,19 +127,20 @@ class FieldHost {
     return pow(a, e, 4);
   }
   static bool eq(const HostFp& a, const HostFp& b) { return memcmp(a.v, b.v, 32) == 0; }
-  // from_bytes_le (ff_utils/src/fp.rs:74-76): little-endian integer of up to
-  // 32 bytes, reduced mod p (ff from_str semantics).  Returns Montgomery.
-  // The same value in canonical form (no Montgomery conversion).
+  // from_bytes_le (ff_utils/src/fp.rs:74-76): the little-endian integer of up
+  // to 32 bytes, reduced mod p (ff from_str semantics), in canonical form (no
+  // Montgomery conversion).  The host is little endian, so the bytes are the
+  // limbs.
   HostFp reduce_bytes_le(const uint8_t* b, size_t len) const {
     HostFp a{{0, 0, 0, 0}};
-    for (size_t i = 0; i < len && i < 32; ++i) a.v[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
+    memcpy(a.v, b, len < 32 ? len : 32);
     while (ge_p(a.v)) sub_p_in_place(a.v);
     return a;
   }
+  // The same value as a Montgomery image.
   HostFp from_bytes_le(const uint8_t* b, size_t len) const {
-    uint64_t c[4] = {0, 0, 0, 0};
-    for (size_t i = 0; i < len && i < 32; ++i) c[i / 8] |= (uint64_t)b[i] << (8 * (i % 8));
-    return from_canonical(c);
+    const HostFp c = reduce_bytes_le(b, len);
+    return from_canonical(c.v);
   }
 
  private:

@@ -20,6 +20,9 @@
 #include <array>
 #include <string>
 
+#include <atomic>
+#include <thread>
+
 #include "internal.h"
 #include "blake2s.h"
 
@@ -278,48 +281,104 @@ void json_bytes(std::string& o, const uint8_t* p, size_t n) {
   o.resize((size_t)(w - &o[0]));
 }
 
-// serde_json of Vec<Proof<Vec<u8>, BlakeDigest>> (commitment/src/merkle_tree.rs:14-18).
-void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
-                   const std::vector<uint8_t>& nodes, size_t k, size_t depth) {
-  o.push_back('[');
-  for (size_t i = 0; i < k; ++i) {
+// Proofs [i0, i1) of a serde_json Vec<Proof<Vec<u8>, BlakeDigest>>
+// (commitment/src/merkle_tree.rs:14-18), each preceded by a comma unless it is
+// proof 0; the caller writes the brackets.
+static void json_branch_range(std::string& o, const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes,
+                              size_t i0, size_t i1, size_t depth) {
+  o.reserve(o.size() + (i1 - i0) * (24 + 4 * leaf_len + depth * 130));
+  for (size_t i = i0; i < i1; ++i) {
     if (i) o.push_back(',');
     o += "{\"leaf\":";
-    json_bytes(o, leaves.data() + leaf_len * i, leaf_len);
+    json_bytes(o, leaves + leaf_len * i, leaf_len);
     o += ",\"nodes\":[";
     for (size_t d = 0; d < depth; ++d) {
       if (d) o.push_back(',');
-      json_bytes(o, nodes.data() + (i * depth + d) * 32, 32);
+      json_bytes(o, nodes + (i * depth + d) * 32, 32);
     }
     o += "]}";
   }
+}
+
+void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
+                   const std::vector<uint8_t>& nodes, size_t k, size_t depth) {
+  o.push_back('[');
+  json_branch_range(o, leaves.data(), leaf_len, nodes.data(), 0, k, depth);
   o.push_back(']');
 }
 
-// serde_json of Vec<FriProof<BlakeDigest>> (fri.rs:16-26), appended to o.
-void fri_proof_json_string(const stark_fri_proof* proof, std::string& o) {
-  o.push_back('[');
+void JsonPieces::text(const std::string& s) {
+  fns.push_back([s](std::string& o) { o += s; });
+}
+
+void JsonPieces::bytes(const uint8_t* p, size_t n) {
+  fns.push_back([p, n](std::string& o) { json_bytes(o, p, n); });
+}
+
+void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes,
+                          size_t k, size_t depth) {
+  text("[");
+  const size_t per = 40;  // proofs per piece
+  for (size_t i0 = 0; i0 < k; i0 += per) {
+    const size_t i1 = i0 + per < k ? i0 + per : k;
+    const uint8_t* lp = leaves.data();
+    const uint8_t* np = nodes.data();
+    fns.push_back([=](std::string& o) { json_branch_range(o, lp, leaf_len, np, i0, i1, depth); });
+  }
+  text("]");
+}
+
+void JsonPieces::render(std::string& o) {
+  std::vector<std::string> out(fns.size());
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
+  };
+  unsigned nt = host_threads();
+  if (nt > 8) nt = 8;
+  if (fns.size() < 8) nt = 1;
+  host_parallel(nt, [&](unsigned) { work(); });
+  size_t total = o.size();
+  for (const std::string& x : out) total += x.size();
+  o.reserve(total);
+  for (const std::string& x : out) o += x;
+  fns.clear();
+}
+
+// serde_json of Vec<FriProof<BlakeDigest>> (fri.rs:16-26) as pieces.
+void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j) {
+  j.text("[");
   for (size_t l = 0; l < proof->layers.size(); ++l) {
     const stark_fri_layer& L = proof->layers[l];
-    if (l) o.push_back(',');
+    if (l) j.text(",");
     if (L.last) {
-      o += "{\"Last\":{\"last\":[";
-      for (size_t i = 0; i < L.last_values.size() / 32; ++i) {
-        if (i) o.push_back(',');
-        json_bytes(o, L.last_values.data() + 32 * i, 32);
-      }
-      o += "]}}";
+      j.text("{\"Last\":{\"last\":[");
+      const uint8_t* v = L.last_values.data();
+      const size_t m = L.last_values.size() / 32;
+      j.fns.push_back([v, m](std::string& o) {
+        for (size_t i = 0; i < m; ++i) {
+          if (i) o.push_back(',');
+          json_bytes(o, v + 32 * i, 32);
+        }
+      });
+      j.text("]}}");
     } else {
-      o += "{\"Middle\":{\"root2\":";
-      json_bytes(o, L.root2, 32);
-      o += ",\"column_branches\":";
-      json_branches(o, L.col_leaves, 32, L.col_nodes, L.col_idx.size(), L.col_depth);
-      o += ",\"poly_branches\":";
-      json_branches(o, L.poly_leaves, 32, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
-      o += "}}";
+      j.text("{\"Middle\":{\"root2\":");
+      j.bytes(L.root2, 32);
+      j.text(",\"column_branches\":");
+      j.branches(L.col_leaves, 32, L.col_nodes, L.col_idx.size(), L.col_depth);
+      j.text(",\"poly_branches\":");
+      j.branches(L.poly_leaves, 32, L.poly_nodes, L.poly_idx.size(), L.poly_depth);
+      j.text("}}");
     }
   }
-  o.push_back(']');
+  j.text("]");
+}
+
+void fri_proof_json_string(const stark_fri_proof* proof, std::string& o) {
+  JsonPieces j;
+  fri_proof_json_pieces(proof, j);
+  j.render(o);
 }
 
 }  // namespace stark

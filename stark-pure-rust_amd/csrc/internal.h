@@ -7,6 +7,7 @@
 
 #include <chrono>
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -113,6 +114,13 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
 // Context-owned pinned host scratch of at least `bytes` (async copy target).
 // Slot 0: gather batches; slot 1: transcript values and roots.
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
+
+// Host worker threads shared by the host-side stages (trace build, proof
+// JSON): host_parallel(n, fn) runs fn(0) .. fn(n-1), fn(0) on the caller, the
+// rest on persistent workers (spawning threads per call costs more than the
+// millisecond-scale work it splits).  host_threads() = workers + 1 (<= 16).
+unsigned host_threads();
+void host_parallel(unsigned n, const std::function<void(unsigned)>& fn);
 // Context-owned Merkle tree slot (created on first use).
 stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out);
 hipStream_t pick_stream(stark_ctx* ctx, void* stream);
@@ -142,6 +150,18 @@ struct GatherReq {
 };
 // All requests in one pinned upload, one download, one synchronisation.
 stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream);
+
+// serde_json text rendered in pieces on a few host threads, then
+// concatenated in order (fri.hip).
+struct JsonPieces {
+  std::vector<std::function<void(std::string&)>> fns;
+  void text(const std::string& s);
+  void bytes(const uint8_t* p, size_t n);  // p must outlive render()
+  void branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes, size_t k,
+                size_t depth);
+  void render(std::string& o);
+};
+void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
 
 // FRI prover on device values (fri.hip).  fri_enqueue puts every layer on the
 // context stream with a device-side transcript and queues the roots' download;

@@ -766,21 +766,21 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   std::unique_ptr<stark_fri_proof, void (*)(stark_fri_proof*)> fri_guard(fri, stark_fri_proof_free);
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
   std::string& o = proof->json;
-  o.reserve((size_t)4 * kSpotChecks * (256 + log_prec * 32) * 4 + (size_t)kSpotChecks * (log_prec + 1) * 32 * 4 +
-            ((size_t)3 << 20));
-  o += "{\"m_root\":";
-  json_bytes(o, proof->m_root, 32);
-  o += ",\"l_root\":";
-  json_bytes(o, proof->l_root, 32);
-  o += ",\"a_root\":";
-  json_bytes(o, proof->a_root, 32);
-  o += ",\"main_branches\":";
-  json_branches(o, m_leaves, 256, m_nodes, 4 * kSpotChecks, log_prec);
-  o += ",\"linear_comb_branches\":";
-  json_branches(o, l_leaves, 32, l_nodes, kSpotChecks, log_prec);
-  o += ",\"fri_proof\":";
-  fri_proof_json_string(fri, o);
-  o += "}";
+  JsonPieces j;
+  j.text("{\"m_root\":");
+  j.bytes(proof->m_root, 32);
+  j.text(",\"l_root\":");
+  j.bytes(proof->l_root, 32);
+  j.text(",\"a_root\":");
+  j.bytes(proof->a_root, 32);
+  j.text(",\"main_branches\":");
+  j.branches(m_leaves, 256, m_nodes, 4 * kSpotChecks, log_prec);
+  j.text(",\"linear_comb_branches\":");
+  j.branches(l_leaves, 32, l_nodes, kSpotChecks, log_prec);
+  j.text(",\"fri_proof\":");
+  fri_proof_json_pieces(fri, j);
+  j.text("}");
+  j.render(o);
   clk.mark("proof JSON");
   *out = proof.release();
   return STARK_OK;

@@ -12,20 +12,101 @@
 #include <string.h>
 
 #include <memory>
+#include <mutex>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "internal.h"
 
-// Uninitialised u64 array (every element is written by the builder).
-struct U64Array {
-  std::unique_ptr<uint64_t[]> p;
-  size_t n = 0;
-  void alloc(size_t count) {
-    p.reset(new uint64_t[count ? count : 1]);
-    n = count;
+namespace stark {
+namespace {
+
+// Large host buffers of freed traces are kept for the next build (a few, at
+// most 1 GiB): a fresh multi-MB allocation is mmapped and first-touch page
+// faults cost as much as filling it (milliseconds at 2^20 steps, serialised
+// on the address-space lock across the fill threads).
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool p;
+    return p;
   }
-  uint64_t* data() const { return p.get(); }
+  void* take(size_t bytes, size_t* cap) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      size_t best = free_.size();
+      for (size_t i = 0; i < free_.size(); ++i)
+        if (free_[i].second >= bytes && free_[i].second <= 2 * bytes + (1u << 20) &&
+            (best == free_.size() || free_[i].second < free_[best].second))
+          best = i;
+      if (best != free_.size()) {
+        void* q = free_[best].first;
+        *cap = free_[best].second;
+        cached_ -= *cap;
+        free_.erase(free_.begin() + (long)best);
+        return q;
+      }
+    }
+    *cap = bytes;
+    return malloc(bytes ? bytes : 8);
+  }
+  void give(void* q, size_t cap) {
+    if (!q) return;
+    if (cap < ((size_t)1 << 20)) {
+      free(q);
+      return;
+    }
+    std::lock_guard<std::mutex> g(m_);
+    free_.emplace_back(q, cap);
+    cached_ += cap;
+    while (free_.size() > kMaxBuffers || cached_ > kMaxBytes) {
+      cached_ -= free_.front().second;
+      free(free_.front().first);
+      free_.erase(free_.begin());
+    }
+  }
+
+ private:
+  static constexpr size_t kMaxBuffers = 8;
+  static constexpr size_t kMaxBytes = (size_t)1 << 30;
+  std::mutex m_;
+  std::vector<std::pair<void*, size_t>> free_;
+  size_t cached_ = 0;
+};
+
+// Runs fn(lo, hi) over [0, n) in contiguous ranges on the host workers
+// (inline when n < min_per_thread * 2).
+template <class Fn>
+void parallel_ranges(size_t n, size_t min_per_thread, Fn&& fn) {
+  size_t nt = host_threads();
+  const size_t by_size = n / (min_per_thread ? min_per_thread : 1);
+  if (by_size < nt) nt = by_size;
+  if (nt <= 1) {
+    fn((size_t)0, n);
+    return;
+  }
+  host_parallel((unsigned)nt, [&](unsigned k) { fn(n * k / nt, n * (k + 1) / nt); });
+}
+
+}  // namespace
+}  // namespace stark
+
+// Uninitialised u64 array (every element is written by the builder), from the pool.
+struct U64Array {
+  uint64_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  U64Array() = default;
+  U64Array(const U64Array&) = delete;
+  U64Array& operator=(const U64Array&) = delete;
+  ~U64Array() { stark::HostPool::get().give(p, cap); }
+  bool alloc(size_t count) {
+    stark::HostPool::get().give(p, cap);
+    p = (uint64_t*)stark::HostPool::get().take(count * sizeof(uint64_t), &cap);
+    n = p ? count : 0;
+    return p != nullptr;
+  }
+  uint64_t* data() const { return p; }
   uint64_t& operator[](size_t i) { return p[i]; }
   size_t size() const { return n; }
 };
@@ -130,21 +211,30 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   if (!c.ok || memcmp(prime, kBn254R, 32) != 0) return STARK_ERR_BAD_ARG;  // run.rs:344-350
   if (c.u32() != 2) return STARK_ERR_BAD_ARG;                               // ConstraintSection
   c.u64();
-  std::vector<Coefficient> coefs;                 // all coefficients, in file order
-  coefs.reserve(r1cs_len / 36);
-  std::vector<uint64_t> fac_off((size_t)3 * n_constraints + 1, 0);  // factor k = coefs[fac_off[k], fac_off[k+1])
+  // All coefficients in file order (wire id + pointer to the 32-B value in
+  // the file); factor k = coefs[fac_off[k], fac_off[k+1]).  Pooled buffers:
+  // every entry read is written first.
+  U64Array coef_buf, fac_buf;
+  if (!coef_buf.alloc(2 * (r1cs_len / 36 + 1)) || !fac_buf.alloc((size_t)3 * n_constraints + 1)) return STARK_ERR_OOM;
+  static_assert(sizeof(Coefficient) == 16, "two u64 per coefficient");
+  Coefficient* coefs = reinterpret_cast<Coefficient*>(coef_buf.data());
+  uint64_t* fac_off = fac_buf.data();
+  fac_off[0] = 0;
+  size_t n_coefs = 0;
   for (uint32_t i = 0; i < n_constraints && c.ok; ++i)
     for (int f = 0; f < 3; ++f) {
       const uint32_t nc = c.u32();
       if (nc > c.left / 36) return STARK_ERR_BAD_ARG;
-      for (uint32_t k = 0; k < nc; ++k) {
-        Coefficient cf;
-        cf.wire_id = c.u32();
-        cf.value = c.raw(32);
-        if (cf.wire_id >= n_wires) return STARK_ERR_BAD_ARG;
-        coefs.push_back(cf);
+      const uint8_t* rec = c.raw((size_t)nc * 36);
+      for (uint32_t k = 0; k < nc; ++k, rec += 36) {
+        uint32_t wire;
+        memcpy(&wire, rec, 4);
+        if (wire >= n_wires) return STARK_ERR_BAD_ARG;
+        coefs[n_coefs].wire_id = wire;
+        coefs[n_coefs].value = rec + 4;
+        ++n_coefs;
       }
-      fac_off[(size_t)3 * i + f + 1] = coefs.size();
+      fac_off[(size_t)3 * i + f + 1] = n_coefs;
     }
   if (!c.ok || n_wires == 0) return STARK_ERR_BAD_ARG;
 
@@ -161,8 +251,20 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   w.u32();
   w.u32();
   if (!w.ok || (uint64_t)n_wit * field_size > w.left) return STARK_ERR_BAD_ARG;
-  std::vector<HostFp> witness(n_wit);  // Montgomery; from_bytes_le reduces mod p (run.rs:354-357)
-  for (uint32_t i = 0; i < n_wit; ++i) witness[i] = F.from_bytes_le(w.raw(field_size), field_size);
+  // from_bytes_le reduces mod p (run.rs:354-357): wcan holds the canonical
+  // values (the trace's witness column), witness their Montgomery images (the
+  // products' right operand).
+  const uint8_t* wbytes = w.raw((size_t)n_wit * field_size);
+  U64Array wbuf;
+  if (!wbuf.alloc((size_t)8 * n_wit + 8)) return STARK_ERR_OOM;
+  HostFp* witness = reinterpret_cast<HostFp*>(wbuf.data());
+  HostFp* wcan = witness + n_wit;
+  parallel_ranges(n_wit, 1u << 12, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      wcan[i] = F.reduce_bytes_le(wbytes + i * field_size, field_size);
+      witness[i] = F.from_canonical(wcan[i].v);
+    }
+  });
   if (n_wit < n_wires || !FieldHost::eq(witness[0], F.one())) return STARK_ERR_BAD_ARG;  // run.rs:358
 
   clk.mark("read_witness");
@@ -176,7 +278,10 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   // ---- calc_coefficients_and_witness (run.rs:109-281)
   // Constraint ci owns n_coeff = max(|A|, |B|, |C|) slots starting at base[ci]
   // in each of the three factor thirds of the trace.
-  std::vector<uint64_t> base((size_t)n_constraints + 1, 0);
+  U64Array base_buf;
+  if (!base_buf.alloc((size_t)n_constraints + 1)) return STARK_ERR_OOM;
+  uint64_t* base = base_buf.data();
+  base[0] = 0;
   for (uint32_t ci = 0; ci < n_constraints; ++ci) {
     uint64_t n_coeff = 0;
     for (int f = 0; f < 3; ++f) {
@@ -190,16 +295,9 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   if (a_len == 0) return STARK_ERR_BAD_ARG;
   // Canonical arithmetic: montmul(c_canonical, w_montgomery) = c * w canonical,
   // so each slot costs one modular product and no conversions.
-  std::vector<HostFp> wcan(n_wit);
-  for (uint32_t i = 0; i < n_wit; ++i) {
-    uint64_t cc[4];
-    F.to_canonical(witness[i], cc);
-    memcpy(wcan[i].v, cc, 32);
-  }
   clk.mark("slot bases");
-  t->witness_trace.alloc(4 * os);
-  t->computational_trace.alloc(4 * os);
-  t->coefficients.alloc(4 * os);
+  if (!t->witness_trace.alloc(4 * os) || !t->computational_trace.alloc(4 * os) || !t->coefficients.alloc(4 * os))
+    return STARK_ERR_OOM;
   // Slot filling is independent per constraint: split the constraints over threads.
   auto fill = [&](uint32_t c0, uint32_t c1) {
     for (uint32_t ci = c0; ci < c1; ++ci) {
@@ -223,16 +321,8 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
       }
     }
   };
-  {
-    unsigned nt = std::thread::hardware_concurrency();
-    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
-    if (os < (1u << 16)) nt = 1;
-    std::vector<std::thread> th;
-    for (unsigned k = 1; k < nt; ++k)
-      th.emplace_back(fill, (uint32_t)((uint64_t)n_constraints * k / nt), (uint32_t)((uint64_t)n_constraints * (k + 1) / nt));
-    fill(0, (uint32_t)((uint64_t)n_constraints / nt));
-    for (auto& x : th) x.join();
-  }
+  parallel_ranges(n_constraints, os < (1u << 16) ? n_constraints + 1 : 1u << 12,
+                  [&](size_t lo, size_t hi) { fill((uint32_t)lo, (uint32_t)hi); });
   clk.mark("slot fill (threads)");
   // ---- calc_flags (run.rs:283-308): flag0 = 1, flag1 = 0 at each constraint's
   // first slot (in all three thirds), flag2 = 1 at its last slot.
@@ -250,9 +340,9 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   clk.mark("flags");
   // ---- wire uses in push order (run.rs:160, 195, 230: factor A's slots, then B's, then C's per
   // constraint), as trace positions a_len * factor + slot; counting sort by wire.
-  std::vector<uint64_t> use_off((size_t)n_wires + 1, 0);
-  auto for_each_use = [&](auto&& fn) {
-    for (uint32_t ci = 0; ci < n_constraints; ++ci) {
+  // Uses of constraints [c0, c1) in push order.
+  auto for_each_use = [&](uint32_t c0, uint32_t c1, auto&& fn) {
+    for (uint32_t ci = c0; ci < c1; ++ci) {
       const uint64_t n_coeff = base[ci + 1] - base[ci];
       for (int f = 0; f < 3; ++f) {
         const uint64_t lo = fac_off[(size_t)3 * ci + f], hi = fac_off[(size_t)3 * ci + f + 1];
@@ -261,22 +351,56 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
       }
     }
   };
-  for_each_use([&](size_t wire, size_t) { ++use_off[wire + 1]; });
-  for (size_t wi = 0; wi < n_wires; ++wi) use_off[wi + 1] += use_off[wi];
-  std::vector<uint64_t> uses(os), cur(use_off.begin(), use_off.end() - 1);
-  for_each_use([&](size_t wire, size_t pos) { uses[cur[wire]++] = pos; });
+  // Stable parallel counting sort: thread k owns a contiguous constraint range
+  // (so its uses are contiguous in push order), counts its uses per wire, and
+  // scatters them after wire-major, thread-minor offsets are known.
+  unsigned nt = host_threads();
+  while (nt > 1 && ((uint64_t)n_wires * nt > 4 * (uint64_t)os + (1u << 16) || n_constraints < 1024u * nt)) --nt;
+  std::vector<uint32_t> cut(nt + 1);
+  for (unsigned k = 0; k <= nt; ++k) cut[k] = (uint32_t)((uint64_t)n_constraints * k / nt);
+  U64Array cnt_buf;  // cnt[k * n_wires + wire], zeroed by thread k
+  if (!cnt_buf.alloc((size_t)nt * n_wires + 1)) return STARK_ERR_OOM;
+  uint64_t* cnt = cnt_buf.data();
+  auto run = [&](auto&& body) { host_parallel(nt, [&](unsigned k) { body(k); }); };
+  run([&](unsigned k) {
+    uint64_t* c = cnt + (size_t)k * n_wires;
+    memset(c, 0, (size_t)n_wires * sizeof(uint64_t));
+    for_each_use(cut[k], cut[k + 1], [&](size_t wire, size_t) { ++c[wire]; });
+  });
+  std::vector<uint64_t> use_off((size_t)n_wires + 1, 0);
+  {
+    uint64_t at = 0;
+    for (size_t wi = 0; wi < n_wires; ++wi) {
+      use_off[wi] = at;
+      for (unsigned k = 0; k < nt; ++k) {
+        const uint64_t c = cnt[(size_t)k * n_wires + wi];
+        cnt[(size_t)k * n_wires + wi] = at;  // becomes thread k's cursor for this wire
+        at += c;
+      }
+    }
+    use_off[n_wires] = at;
+  }
+  U64Array uses_buf;
+  if (!uses_buf.alloc(os)) return STARK_ERR_OOM;
+  uint64_t* uses = uses_buf.data();
+  run([&](unsigned k) {
+    uint64_t* cur = cnt + (size_t)k * n_wires;
+    for_each_use(cut[k], cut[k + 1], [&](size_t wire, size_t pos) { uses[cur[wire]++] = pos; });
+  });
   clk.mark("wire uses (counting sort)");
   // ---- permuted indices (run.rs:388-401): a cycle through every wire's uses.
-  t->permuted_indices.alloc(os);
-  for (size_t wi = 0; wi < n_wires; ++wi) {
-    const uint64_t lo = use_off[wi], hi = use_off[wi + 1];
-    if (lo == hi) continue;
-    uint64_t old_w = uses[hi - 1];
-    for (uint64_t j = lo; j < hi; ++j) {
-      t->permuted_indices[uses[j]] = old_w;
-      old_w = uses[j];
+  if (!t->permuted_indices.alloc(os)) return STARK_ERR_OOM;
+  parallel_ranges(n_wires, 1u << 12, [&](size_t w0, size_t w1) {
+    for (size_t wi = w0; wi < w1; ++wi) {
+      const uint64_t lo = use_off[wi], hi = use_off[wi + 1];
+      if (lo == hi) continue;
+      uint64_t old_w = uses[hi - 1];
+      for (uint64_t j = lo; j < hi; ++j) {
+        t->permuted_indices[uses[j]] = old_w;
+        old_w = uses[j];
+      }
     }
-  }
+  });
   // ---- public_first_indices (run.rs:411-419)
   for (size_t wi = 0; wi < n_public && wi < n_wires; ++wi)
     if (use_off[wi] != use_off[wi + 1]) {
