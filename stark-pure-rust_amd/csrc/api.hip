@@ -157,9 +157,23 @@ static stark_status fft_host(stark_ctx* ctx, const uint64_t* in, size_t len, con
   st = ensure_buf(ctx, ctx->io, n * sizeof(fe));
   if (st != STARK_OK) return st;
   fe* d = (fe*)ctx->io.ptr;
-  if (len) STARK_HIP(ctx, hipMemcpyAsync(d, in, len * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
-  if (len < n) STARK_HIP(ctx, hipMemsetAsync(d + len, 0, (n - len) * sizeof(fe), ctx->stream));
-  st = ntt_device(ctx, d, log_n, 1, *tw, inverse, ctx->stream);
+  // A power-of-two input padded by at most the first pass's radix: the pass
+  // reads the len coefficients only (ntt_device_from), no zero fill.
+  uint32_t log_len = 0;
+  while (((size_t)1 << log_len) < len) ++log_len;
+  const bool sparse = len && len < n && ((size_t)1 << log_len) == len && log_n >= 2 &&
+                      log_n - log_len <= ntt_first_log_r(log_n);
+  if (sparse) {
+    st = ensure_buf(ctx, ctx->io2, len * sizeof(fe));
+    if (st != STARK_OK) return st;
+    fe* src = (fe*)ctx->io2.ptr;
+    STARK_HIP(ctx, hipMemcpyAsync(src, in, len * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    st = ntt_device_from(ctx, src, log_n - log_len, d, log_n, 1, *tw, inverse, ctx->stream);
+  } else {
+    if (len) STARK_HIP(ctx, hipMemcpyAsync(d, in, len * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    if (len < n) STARK_HIP(ctx, hipMemsetAsync(d + len, 0, (n - len) * sizeof(fe), ctx->stream));
+    st = ntt_device(ctx, d, log_n, 1, *tw, inverse, ctx->stream);
+  }
   if (st != STARK_OK) return st;
   STARK_HIP(ctx, hipMemcpyAsync(out, d, n * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
   STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -132,6 +132,12 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
 // Device NTT over `batch` contiguous transforms (in place, canonical values).
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
                         bool inverse, hipStream_t stream);
+// Forward/inverse transform of src's batch columns of 2^(log_n - zero_log)
+// elements, zero-extended to 2^log_n, into d_data (zero_log <= the plan's
+// first radix); the zero tail is neither stored nor read.
+uint32_t ntt_first_log_r(uint32_t log_n);  // log2 of the first pass's radix
+stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
+                             uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream);
 
 // Merkle internals (merkle.hip).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,

@@ -35,11 +35,19 @@ struct ColTw {
 // the next tile's 4 elements per thread into registers while it computes the
 // current one, so HBM traffic overlaps the modular arithmetic.
 // T = B*R/4 threads, each owning exactly 4 elements in every phase.
+// First pass of a transform whose input is zero beyond its first n >> zero_log
+// elements (best_fft's zero padding): skip = the number of leading radix-2
+// stages that are plain copies (<= zero_log, matching the pass's stage
+// pairing); log_in = log2 of the compact input's batch stride.
+struct Sparse {
+  uint32_t skip, zero_log, log_in;
+};
+
 template <int LOG_R, bool PERSIST>
 __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
                                                           const fe* __restrict__ small, fe scale, int do_scale,
-                                                          uint32_t log_tiles, uint32_t total_tiles) {
+                                                          uint32_t log_tiles, uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
   fe* sm = lds;          // R/2 small roots w_R^k
@@ -65,12 +73,18 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
   const uint32_t b = tid & (B - 1);
   const uint32_t q = tid >> log_b;  // radix-4 group within the column
 
+  // Sparse first pass (sp.skip > 0): only rows < R >> sp.zero_log are
+  // non-zero (read from a compact input of batch stride 2^sp.log_in), and the
+  // first sp.skip radix-2 stages are copies; rows < R >> sp.skip are loaded.
+  const uint32_t live_rows = R >> sp.skip, nz_rows = R >> sp.zero_log;
+  const uint32_t log_in = sp.zero_log ? sp.log_in : log_n;
   uint32_t tile = blockIdx.x;
   fe v[4];
   if (active && tile < total_tiles) {
-    const fe* src = in + ((size_t)(tile >> log_tiles) << log_n) + ((size_t)(tile & tile_mask) << log_b);
+    const fe* src = in + ((size_t)(tile >> log_tiles) << log_in) + ((size_t)(tile & tile_mask) << log_b);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] = fe_load(src + eb[t] + ((size_t)er[t] << log_cols));
+    for (int t = 0; t < 4; ++t)
+      v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
   }
 
   for (; tile < total_tiles; tile += gridDim.x) {
@@ -103,10 +117,21 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = fe_mul_lazy(v[t], tw[t]);  // v < 4p, tw < p -> [0, 2p)
       }
+      if (sp.skip == 0) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
-        X[(rr << log_b) + eb[t]] = v[t];
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+          X[(rr << log_b) + eb[t]] = v[t];
+        }
+      } else {
+        // Rows >= live_rows are zero, so after sp.skip DIT stages every
+        // position of a group of 2^skip holds the group's one live input.
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (er[t] >= live_rows) continue;
+          const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+          for (uint32_t k = 0; k < (1u << sp.skip); ++k) X[((rr + k) << log_b) + eb[t]] = v[t];
+        }
       }
     }
     __syncthreads();
@@ -114,9 +139,10 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
     // ---- prefetch the next tile while this one is transformed ----
     const uint32_t nt = tile + gridDim.x;
     if (PERSIST && active && nt < total_tiles) {
-      const fe* src = in + ((size_t)(nt >> log_tiles) << log_n) + ((size_t)(nt & tile_mask) << log_b);
+      const fe* src = in + ((size_t)(nt >> log_tiles) << log_in) + ((size_t)(nt & tile_mask) << log_b);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = fe_load(src + eb[t] + ((size_t)er[t] << log_cols));
+      for (int t = 0; t < 4; ++t)
+        v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
     }
 
     // ---- R-point DIT over the bit-reversed image ----
@@ -124,8 +150,8 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
     // left in [0, 2p) and each radix-2 butterfly reduces only its X input
     // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
     // it is the transform's last pass.
-    int s = 0;
-    if (LOG_R & 1) {
+    int s = (int)sp.skip;
+    if ((LOG_R & 1) && sp.skip == 0) {
       if (active) {  // radix-2 stage 0: twiddles are all 1
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -248,11 +274,14 @@ constexpr uint64_t kPersistentGrid = 256 * 2;
 #endif
 constexpr bool kPersistent = STARK_NTT_PERSISTENT != 0;
 
+// The smaller radices lead: a sparse first pass of odd radix can skip 3 copy
+// stages, an even one only 2.  (Every plan of a size has the same last radix,
+// which the cached full last-pass twiddle table depends on.)
 PassPlan plan_passes(uint32_t log_n) {
   PassPlan p;
   p.n_pass = (int)((log_n + kMaxLogR - 1) / kMaxLogR);
   const uint32_t base = log_n / p.n_pass, extra = log_n % p.n_pass;
-  for (int i = 0; i < p.n_pass; ++i) p.log_r[i] = base + ((uint32_t)i < extra ? 1 : 0);
+  for (int i = 0; i < p.n_pass; ++i) p.log_r[i] = base + ((uint32_t)(p.n_pass - 1 - i) < extra ? 1 : 0);
   return p;
 }
 
@@ -266,7 +295,7 @@ uint32_t choose_log_b(uint32_t log_n, uint32_t log_r) {
 }
 
 typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, fe, int, uint32_t,
-                        uint32_t);
+                        uint32_t, Sparse);
 
 pass_fn pass_kernel(uint32_t log_r, bool persist) {
   switch (log_r) {
@@ -421,9 +450,25 @@ static bool full_table_enabled() {
   return on;
 }
 
+uint32_t ntt_first_log_r(uint32_t log_n) { return log_n < 2 ? log_n : plan_passes(log_n).log_r[0]; }
+
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
                         bool inverse, hipStream_t stream) {
+  return ntt_device_from(ctx, nullptr, 0, d_data, log_n, batch, tw, inverse, stream);
+}
+
+// src != nullptr: the input is src (batch columns of 2^(log_n - zero_log)
+// elements, the rest of each column implicitly zero) and the output goes to
+// d_data; the zero tail is never written or read (forward LDE of best_fft's
+// padded coefficients).
+stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
+                             uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream) {
   if (batch == 0) return STARK_OK;
+  if (src && (log_n < 2 || zero_log > plan_passes(log_n).log_r[0])) return STARK_ERR_BAD_ARG;
+  if (src && zero_log == 0) {
+    STARK_HIP(ctx, hipMemcpyAsync(d_data, src, ((size_t)batch << log_n) * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+    src = nullptr;
+  }
   if (((uint64_t)batch << log_n) > ((uint64_t)1 << 34)) return STARK_ERR_BAD_ARG;
   const size_t n = (size_t)1 << log_n;
   const fe scale = to_dev(tw.inv_n);
@@ -437,7 +482,7 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
   stark_status st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
   if (st != STARK_OK) return st;
   fe* scratch = (fe*)ctx->scratch.ptr;
-  fe* cur = d_data;
+  const fe* cur = src ? src : d_data;
   uint32_t log_ns = 0;
   for (int p = 0; p < plan.n_pass; ++p) {
     const uint32_t lr = plan.log_r[p];
@@ -445,6 +490,14 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
     // Passes before the last ping-pong; the last pass (Ns R = n) reads and
     // writes the same positions, so it always lands in d_data.
     fe* dst = last ? d_data : (cur == d_data ? scratch : d_data);
+    Sparse sp{0, 0, log_n};
+    if (p == 0 && src) {
+      // Copy stages the pass's stage pairing can skip: odd radices run a
+      // radix-2 stage 0 then pairs (1,2), (3,4)..; even ones pairs (0,1)..
+      uint32_t k = zero_log < lr ? zero_log : lr;
+      if ((k & 1) != (lr & 1)) --k;
+      sp = Sparse{k, zero_log, log_n - zero_log};
+    }
     const uint32_t lb = choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
@@ -464,7 +517,7 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
     hipLaunchKernelGGL(pass_kernel(lr, persist), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], scale, (inverse && last && !fold) ? 1 : 0, log_tiles,
-                       (uint32_t)total);
+                       (uint32_t)total, sp);
     STARK_HIP(ctx, hipGetLastError());
     cur = dst;
     log_ns += lr;

@@ -189,17 +189,6 @@ __global__ void r1cs_flags_kernel(const uint8_t* __restrict__ fb, uint64_t os, u
   fe_store(dst + f * steps + i, fe_from_u64(fb[g]));
 }
 
-// dst[c][i] = i < steps ? src[c][i] : 0 (best_fft's zero padding, fft.rs:327-357).
-__global__ void r1cs_pad_kernel(const fe* __restrict__ src, fe* __restrict__ dst, uint32_t log_steps,
-                                uint32_t log_prec, uint64_t total) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= total) return;
-  const uint64_t c = g >> log_prec, i = g & (((uint64_t)1 << log_prec) - 1);
-  fe v = fe_zero();
-  if ((i >> log_steps) == 0) v = fe_load(src + (c << log_steps) + i);
-  fe_store(dst + g, v);
-}
-
 // val_nmr / val_dnm of calc_a_mini_evaluations (utils.rs:317-318), written as
 // Montgomery images for the product scans.
 __global__ void r1cs_a_vals_kernel(const fe* __restrict__ ext_idx, const fe* __restrict__ ext_pidx,
@@ -515,11 +504,8 @@ static stark_status product_scan(stark_ctx* ctx, fe* v, uint64_t n, fe* tot, fe*
 static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint32_t log_steps, uint32_t log_prec,
                         const Twiddles& tw_g1_inv, const Twiddles& tw_g2, hipStream_t s) {
   STARK_TRY(ntt_device(ctx, coef, log_steps, batch, tw_g1_inv, true, s));
-  const uint64_t total = (uint64_t)batch << log_prec;
-  hipLaunchKernelGGL(r1cs_pad_kernel, dim3(blocks_for(total)), dim3(256), 0, s, (const fe*)coef, out, log_steps,
-                     log_prec, total);
-  STARK_HIP(ctx, hipGetLastError());
-  return ntt_device(ctx, out, log_prec, batch, tw_g2, false, s);
+  // best_fft's zero padding (fft.rs:327-357) is implicit: the first pass reads the steps coefficients only.
+  return ntt_device_from(ctx, coef, log_prec - log_steps, out, log_prec, batch, tw_g2, false, s);
 }
 
 static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,

@@ -41,6 +41,20 @@ def test_ntt_zero_padding(ctx, oracle, log_n, length):
     assert np.array_equal(ctx.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=8))
 
 
+@pytest.mark.parametrize("log_n,zero_log", [(2, 1), (2, 2), (7, 3), (7, 7), (9, 1), (9, 4), (16, 2), (16, 3),
+                                             (18, 3), (18, 6), (20, 3), (21, 7), (23, 3)])
+def test_ntt_sparse_first_pass(ctx, oracle, log_n, zero_log):
+    """Power-of-two inputs zero-padded by up to the first pass's radix take the sparse first pass
+    (the padding is neither written nor read; the first copy stages are skipped): forward and inverse
+    equal best_fft / inv_best_fft of the padded vector (fft.rs:327-379)."""
+    length = 1 << (log_n - zero_log)
+    c = O.random_elements(length, 900 + log_n * 10 + zero_log)
+    w = O.root_of_unity(log_n)
+    cpus = 16 if log_n >= 20 else 8
+    assert np.array_equal(ctx.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=cpus))
+    assert np.array_equal(ctx.inv_best_fft(c, w, log_n), oracle.inv_best_fft(c, w, log_n, cpus=cpus))
+
+
 def test_ntt_extreme_values(ctx, oracle):
     # p-1 everywhere, zeros, ones: stresses the carry / reduction paths.
     log_n = 12
