@@ -210,6 +210,12 @@ stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, 
  * the cross-rank DFT of the one-exchange distributed NTT. */
 stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
                                    const uint64_t root[4], int inverse, void* stream);
+/* The same, after first scaling d[i + stride*j] by tw_root^(j*(tw_base + i))
+ * (tw_root a primitive 2^log_order-th root): the receiver-side twiddle of the
+ * one-exchange distributed NTT, fused into its cross-rank DFT. */
+stark_status stark_ntt_strided_tw_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
+                                      const uint64_t root[4], int inverse, const uint64_t tw_root[4],
+                                      uint32_t log_order, uint64_t tw_base, void* stream);
 
 /* ---- device memory helpers (for callers without their own allocator) ------ */
 stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);

@@ -50,9 +50,20 @@ struct SmallRoots {
   fe w[8];  // w_G^k, k < G/2 (Montgomery)
 };
 
-template <int LOG_G>
+// Optional input twiddle, applied before the DFT: d[i + stride j] *=
+// w^(j (base + i)) (w from the two-level tables) -- the one-exchange
+// distributed NTT's w^(r k2) factor applied at the receiver, fused here so the
+// sender does not spend a separate pass over HBM on it.
+struct StridedTw {
+  const fe* lo;
+  const fe* hi;
+  uint32_t kb;
+  uint64_t base, mask;  // exponent (base + i) & mask, mask = order - 1
+};
+
+template <int LOG_G, bool TW>
 __global__ __launch_bounds__(256) void strided_ntt_kernel(fe* __restrict__ d, uint64_t stride, SmallRoots rt,
-                                                          fe scale, int do_scale) {
+                                                          fe scale, int do_scale, StridedTw tw) {
   constexpr int G = 1 << LOG_G;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= stride) return;
@@ -63,6 +74,19 @@ __global__ __launch_bounds__(256) void strided_ntt_kernel(fe* __restrict__ d, ui
 #pragma unroll
     for (int b = 0; b < LOG_G; ++b) br |= ((j >> b) & 1) << (LOG_G - 1 - b);
     x[br] = fe_load(d + i + stride * (uint64_t)j);  // bit-reversed order for the in-place DIT
+  }
+  if (TW) {
+    const uint64_t e = (tw.base + i) & tw.mask;
+    const fe step = fe_mul(tw.lo[e & (((uint64_t)1 << tw.kb) - 1)], tw.hi[e >> tw.kb]);  // w^e, Montgomery
+    fe t = step;
+#pragma unroll
+    for (int j = 1; j < G; ++j) {
+      int br = 0;
+#pragma unroll
+      for (int b = 0; b < LOG_G; ++b) br |= ((j >> b) & 1) << (LOG_G - 1 - b);
+      x[br] = fe_mul(x[br], t);  // canonical * Montgomery -> canonical
+      if (j + 1 < G) t = fe_mul(t, step);
+    }
   }
 #pragma unroll
   for (int s = 0; s < LOG_G; ++s) {
@@ -101,8 +125,8 @@ stark_status stark_transpose_dev(stark_ctx* ctx, const uint64_t* d_src, uint64_t
   return STARK_OK;
 }
 
-stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
-                                   const uint64_t root[4], int inverse, void* stream) {
+static stark_status strided(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride, const uint64_t root[4],
+                            int inverse, const uint64_t* tw_root, uint32_t log_order, uint64_t tw_base, void* stream) {
   if (!ctx || !d_data || !root) return STARK_ERR_BAD_ARG;
   if (log_g > 4) return STARK_ERR_BAD_LENGTH;
   if (stride == 0 || log_g == 0) return STARK_OK;
@@ -119,19 +143,47 @@ stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t lo
     rt.w[k] = to_dev(p);
     p = F.mul(p, w);
   }
+  StridedTw tw{nullptr, nullptr, 0, tw_base, 0};
+  if (tw_root) {
+    const Twiddles* t = nullptr;
+    const stark_status st = get_twiddles(ctx, tw_root, log_order, &t);
+    if (st != STARK_OK) return st;
+    tw = StridedTw{t->d_lo, t->d_hi, t->kb, tw_base, ((uint64_t)1 << log_order) - 1};
+  }
   const fe scale = to_dev(F.inv(F.from_u64((uint64_t)1 << log_g)));
   const unsigned grid = (unsigned)((stride + 255) / 256);
   hipStream_t s = pick_stream(ctx, stream);
   fe* d = (fe*)d_data;
   const int sc = inverse ? 1 : 0;
+  const uint64_t st = stride;
+#define STARK_STRIDED(LG)                                                                                      \
+  do {                                                                                                        \
+    if (tw_root)                                                                                              \
+      hipLaunchKernelGGL((strided_ntt_kernel<LG, true>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw);  \
+    else                                                                                                      \
+      hipLaunchKernelGGL((strided_ntt_kernel<LG, false>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw); \
+  } while (0)
   switch (log_g) {
-    case 1: hipLaunchKernelGGL(strided_ntt_kernel<1>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
-    case 2: hipLaunchKernelGGL(strided_ntt_kernel<2>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
-    case 3: hipLaunchKernelGGL(strided_ntt_kernel<3>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
-    default: hipLaunchKernelGGL(strided_ntt_kernel<4>, dim3(grid), dim3(256), 0, s, d, (uint64_t)stride, rt, scale, sc); break;
+    case 1: STARK_STRIDED(1); break;
+    case 2: STARK_STRIDED(2); break;
+    case 3: STARK_STRIDED(3); break;
+    default: STARK_STRIDED(4); break;
   }
+#undef STARK_STRIDED
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
+}
+
+stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
+                                   const uint64_t root[4], int inverse, void* stream) {
+  return strided(ctx, d_data, log_g, stride, root, inverse, nullptr, 0, 0, stream);
+}
+
+stark_status stark_ntt_strided_tw_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
+                                      const uint64_t root[4], int inverse, const uint64_t tw_root[4],
+                                      uint32_t log_order, uint64_t tw_base, void* stream) {
+  if (!tw_root) return STARK_ERR_BAD_ARG;
+  return strided(ctx, d_data, log_g, stride, root, inverse, tw_root, log_order, tw_base, stream);
 }
 
 stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, size_t cols, uint64_t row_base,

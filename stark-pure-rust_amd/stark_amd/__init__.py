@@ -90,6 +90,8 @@ _SIGNATURES = {
     "stark_r1cs_trace_free": ([_vp], None),
     "stark_prove_r1cs_trace": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_ntt_strided_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, ctypes.c_int, _vp], ctypes.c_int),
+    "stark_ntt_strided_tw_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, ctypes.c_int, _u64p,
+                                  ctypes.c_uint32, ctypes.c_uint64, _vp], ctypes.c_int),
     "stark_transpose_dev": ([_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32, _vp], ctypes.c_int),
     "stark_twiddle2d_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _u64p,
                              ctypes.c_uint32, _vp], ctypes.c_int),
@@ -215,6 +217,13 @@ class Context:
         r = _limbs(root)
         self.check(self.lib.stark_ntt_strided_dev(self.h, d_ptr, log_g, stride, _p64(r), 1 if inverse else 0,
                                                   stream or None), "ntt_strided")
+
+    def ntt_strided_tw_dev(self, d_ptr: int, log_g: int, stride: int, root, tw_root, log_order: int, tw_base: int,
+                           inverse: bool = False, stream: int = 0) -> None:
+        """ntt_strided_dev after d[i + stride*j] *= tw_root^(j*(tw_base + i))."""
+        r, t = _limbs(root), _limbs(tw_root)
+        self.check(self.lib.stark_ntt_strided_tw_dev(self.h, d_ptr, log_g, stride, _p64(r), 1 if inverse else 0,
+                                                     _p64(t), log_order, tw_base, stream or None), "ntt_strided_tw")
 
     def transpose_dev(self, d_src: int, d_dst: int, rows: int, cols: int, batch: int = 1, stream: int = 0) -> None:
         self.check(self.lib.stark_transpose_dev(self.h, d_src, d_dst, rows, cols, batch, stream or None), "transpose")

@@ -102,7 +102,21 @@ def cyclic_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = Fals
     local transform overwrite x (no copy); `out` receives the result if given.
     """
     G = dist.get_world_size(group)
-    r = dist.get_rank(group)
+    y = cyclic_ntt_local(x, log_n, root, ops, inverse, group, in_place)
+    if G == 1:
+        return y
+    z = torch.empty_like(y) if out is None else out
+    _exchange(z, y, group)                                          # z[j1][i] = Y_j1[r c + i]
+    cyclic_ntt_finish(z, log_n, root, ops, inverse, group)
+    return z
+
+
+def cyclic_ntt_local(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = False, group=None,
+                     in_place: bool = False) -> torch.Tensor:
+    """cyclic_ntt's first step: this rank's M-point NTT (root w^G), plus the twiddle w^(+-r k2) when
+    the ops cannot fuse it into the last step.  With G == 1 it is the whole transform.  The result is
+    what the exchange sends."""
+    G = dist.get_world_size(group)
     n = 1 << log_n
     M = n // G
     if M * G != n or M % G != 0 or x.shape[0] != M:
@@ -113,14 +127,46 @@ def cyclic_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = Fals
         ops.ntt(y, log_n, 1, w, inverse)
         return y
     log_m = M.bit_length() - 1
-    log_g = G.bit_length() - 1
-    c = M // G
     ops.ntt(y, log_m, 1, pow(w, G, P), inverse)                     # M-point, root w^G
-    ops.twiddle2d(y, 1, M, r, 0, pow(w, P - 2, P) if inverse else w, log_n)   # y[k2] *= w^(+-r k2)
-    z = torch.empty_like(y) if out is None else out
-    _exchange(z, y, group)                                          # z[j1][i] = Y_j1[r c + i]
-    ops.ntt_strided(z, log_g, c, pow(w, M, P), inverse)             # G-point over j1, root w^M
-    return z
+    if not hasattr(ops, "ntt_strided_tw"):
+        ops.twiddle2d(y, 1, M, dist.get_rank(group), 0, pow(w, P - 2, P) if inverse else w, log_n)
+    return y
+
+
+def cyclic_ntt_finish(z: torch.Tensor, log_n: int, root: int, ops, inverse: bool = False, group=None) -> None:
+    """cyclic_ntt's last step on the received chunks z[j1][i] = Y_j1[r c + i]: the twiddle
+    w^(+-j1 (r c + i)) (applied here, fused into the strided kernel, when the ops have
+    ntt_strided_tw) and the G-point DFTs over j1 (root w^M), in place."""
+    G = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    n = 1 << log_n
+    M = n // G
+    c = M // G
+    w = root % P
+    log_g = G.bit_length() - 1
+    if hasattr(ops, "ntt_strided_tw"):
+        ops.ntt_strided_tw(z, log_g, c, pow(w, M, P), inverse, pow(w, P - 2, P) if inverse else w, log_n, r * c)
+    else:
+        ops.ntt_strided(z, log_g, c, pow(w, M, P), inverse)
+
+
+def cyclic_ntt_pipelined(pairs, k: int, log_n: int, root: int, ops, inverse: bool = False, group=None) -> None:
+    """k independent cyclic_ntt transforms with the exchange of transform i overlapping the local NTT
+    of transform i+1: transform i runs on pairs[i % len(pairs)] = (shard, out), the shard transformed
+    in place and the result left in out.  With backend "nccl" the all-to-all runs on RCCL's stream
+    while this stream computes; every transform is complete when the call returns (on the stream)."""
+    pending = None
+    for i in range(k):
+        a, b = pairs[i % len(pairs)]
+        cyclic_ntt_local(a, log_n, root, ops, inverse, group, in_place=True)
+        work = dist.all_to_all_single(b, a, group=group, async_op=True)
+        if pending is not None:
+            pending[0].wait()
+            cyclic_ntt_finish(pending[1], log_n, root, ops, inverse, group)
+        pending = (work, b)
+    if pending is not None:
+        pending[0].wait()
+        cyclic_ntt_finish(pending[1], log_n, root, ops, inverse, group)
 
 
 class GpuOps:
@@ -139,6 +185,11 @@ class GpuOps:
 
     def ntt_strided(self, t: torch.Tensor, log_g: int, stride: int, root: int, inverse: bool) -> None:
         self.ctx.ntt_strided_dev(t.data_ptr(), log_g, stride, root, inverse=inverse, stream=self._stream())
+
+    def ntt_strided_tw(self, t: torch.Tensor, log_g: int, stride: int, root: int, inverse: bool, tw_root: int,
+                       log_order: int, tw_base: int) -> None:
+        self.ctx.ntt_strided_tw_dev(t.data_ptr(), log_g, stride, root, tw_root, log_order, tw_base,
+                                    inverse=inverse, stream=self._stream())
 
     def transpose(self, src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int) -> None:
         self.ctx.transpose_dev(src.data_ptr(), dst.data_ptr(), rows, cols, 1, stream=self._stream())

@@ -45,6 +45,14 @@ class OracleOps:
         for i in range(stride):
             a[:, i] = f(a[:, i].copy(), root, log_g, cpus=1)
 
+    def ntt_strided_tw(self, t, log_g, stride, root, inverse, tw_root, log_order, tw_base):
+        a = self._u64(t).reshape(1 << log_g, stride, 4)
+        mask = (1 << log_order) - 1
+        for j in range(1, 1 << log_g):
+            vals = O.from_limbs(a[j])
+            a[j] = O.to_limbs([v * pow(tw_root, (j * (tw_base + i)) & mask, O.P) % O.P for i, v in enumerate(vals)])
+        self.ntt_strided(t, log_g, stride, root, inverse)
+
     def merkle_commit(self, shard, m, leaf_len):
         self._leaves = bytes(shard.numpy().view(np.uint8)) if hasattr(shard, "numpy") else bytes(shard)
         self._m, self._ll = m, leaf_len
@@ -84,6 +92,54 @@ def _worker(rank, world, port, log_n, inverse, out_q):
     out_q.put((rank, y.numpy().view(np.uint64).copy()))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _worker_pipelined(rank, world, port, log_n, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from stark_amd.distributed import cyclic_ntt, cyclic_ntt_pipelined
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    ops = OracleOps()
+    # Three transforms on two buffer pairs: transform 2 reuses pair 0 after transform 0's exchange.
+    shards = [torch.from_numpy(O.random_elements(n, 500 + 10 * s)[rank::world].copy().view(np.int64))
+              for s in range(2)]
+    want0 = cyclic_ntt(shards[0], log_n, w, ops)
+    want1 = cyclic_ntt(shards[1], log_n, w, ops)
+    want2 = cyclic_ntt(_local_after(shards[0], log_n, w, ops), log_n, w, ops)
+    pairs = [(shards[0].clone(), torch.empty_like(shards[0])), (shards[1].clone(), torch.empty_like(shards[1]))]
+    cyclic_ntt_pipelined(pairs, 2, log_n, w, ops)
+    ok = torch.equal(pairs[0][1], want0) and torch.equal(pairs[1][1], want1)
+    cyclic_ntt_pipelined(pairs, 3, log_n, w, ops)   # 3rd transform: pair 0 again, its shard already local-transformed twice
+    ok = ok and torch.equal(pairs[0][1], want2)
+    out_q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def _local_after(shard, log_n, w, ops):
+    """The shard a third transform on pair 0 sees: cyclic_ntt_local applied twice in place."""
+    from stark_amd.distributed import cyclic_ntt_local
+    y = shard.clone()
+    cyclic_ntt_local(y, log_n, w, ops, in_place=True)
+    cyclic_ntt_local(y, log_n, w, ops, in_place=True)
+    return y
+
+
+@pytest.mark.parametrize("world,log_n", [(2, 8), (4, 10)])
+def test_cyclic_ntt_pipelined_gloo(world, log_n):
+    """bench.py's N > 1 schedule (exchange i overlapping local NTT i+1, two buffer pairs) produces
+    exactly cyclic_ntt's result for every transform."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, log_n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res.values())
 
 
 def _worker_cyclic(rank, world, port, log_n, inverse, out_q):

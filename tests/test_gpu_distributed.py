@@ -90,6 +90,30 @@ def test_ntt_strided(ctx, oracle, log_g, inverse):
         assert np.array_equal(got.reshape(G, stride, 4)[:, i], want[:, i])
 
 
+@pytest.mark.parametrize("log_g,inverse", [(1, False), (3, False), (3, True), (4, True)])
+def test_ntt_strided_tw(ctx, oracle, log_g, inverse):
+    """The receiver-side twiddle fused into the strided DFT: d[i + stride j] *= t^(j (base + i)) first."""
+    G, stride, log_order, base = 1 << log_g, 1000, 20, 123456
+    a = O.random_elements(G * stride, 31 + log_g)
+    t = O.root_of_unity(log_order)
+    d = ctx.alloc(a.nbytes)
+    try:
+        ctx.h2d(d, a)
+        w = O.root_of_unity(log_g)
+        ctx.ntt_strided_tw_dev(d, log_g, stride, w, t, log_order, base, inverse=inverse)
+        got = np.empty_like(a)
+        ctx.d2h(got, d)
+    finally:
+        ctx.free(d)
+    want = a.reshape(G, stride, 4).copy()
+    f = oracle.inv_best_fft if inverse else oracle.best_fft
+    mask = (1 << log_order) - 1
+    for i in range(0, stride, 97):
+        col = [v * pow(t, (j * (base + i)) & mask, O.P) % O.P for j, v in enumerate(O.from_limbs(want[:, i]))]
+        want[:, i] = f(O.to_limbs(col), w, log_g, cpus=1)
+        assert np.array_equal(got.reshape(G, stride, 4)[:, i], want[:, i])
+
+
 def _worker_merkle(rank, world, port, log_m, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
