@@ -80,6 +80,20 @@ stark_status stark_fft_in_place(stark_ctx* ctx, uint64_t* values, const uint64_t
  * semantics.  Asynchronous on `stream` (NULL = context stream). */
 stark_status stark_ntt_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t batch,
                            const uint64_t root[4], int inverse, void* stream);
+/* Low-degree extension, the pattern of r1cs-stark/src/prove.rs:100-101 (and
+ * :160-167, 183-184): inv_best_fft(values, g1, log2 steps) followed by
+ * best_fft(coefficients zero-padded to steps << log_blowup, g2), where g2 is a
+ * primitive (steps << log_blowup)-th root and g1 = g2^(2^log_blowup)
+ * (prove.rs:71-94).  out holds steps << log_blowup elements.  The padding is
+ * never materialised (the first forward pass reads the coefficients only). */
+stark_status stark_lde(stark_ctx* ctx, const uint64_t* values, size_t steps, const uint64_t g1[4],
+                       uint32_t log_blowup, const uint64_t g2[4], uint64_t* out);
+/* Device-resident, batched: `batch` columns of 2^log_steps values at d_values
+ * (overwritten with their coefficients) -> `batch` columns of
+ * 2^(log_steps + log_blowup) evaluations at d_out.  Asynchronous on `stream`. */
+stark_status stark_lde_dev(stark_ctx* ctx, uint64_t* d_values, uint64_t* d_out, uint32_t log_steps,
+                           uint32_t log_blowup, uint32_t batch, const uint64_t g1[4], const uint64_t g2[4],
+                           void* stream);
 /* expand_root_of_unity<T>(root) -> Vec<T> (fft.rs:5-14): writes
  * min(order, cap) powers [1, w, w^2, ...] and stores the order in *count.
  * The order must be a power of two <= 2^28. */
@@ -93,6 +107,23 @@ stark_status stark_multi_inv(stark_ctx* ctx, const uint64_t* values, size_t n, u
  * r1cs-stark/src/prove.rs:216-220): out[i] = sum_k poly[k] * xs[i]^k. */
 stark_status stark_eval_poly_at_multi(stark_ctx* ctx, const uint64_t* poly, size_t deg_plus_1,
                                       const uint64_t* xs, size_t n, uint64_t* out);
+/* multi_interp_4<T>(xsets, ysets) -> Vec<[T; 4]> (poly_utils.rs:449-511): for
+ * each row the coefficients of the cubic through (xs[k], ys[k]), k < 4; rows
+ * x 4 elements in, rows x 4 coefficients out (zero denominators map to zero
+ * through multi_inv, as in the reference). */
+stark_status stark_multi_interp_4(stark_ctx* ctx, const uint64_t* xsets, const uint64_t* ysets, size_t rows,
+                                  uint64_t* out);
+/* eval_quartic<T>(p, x) (poly_utils.rs:442-446) for n (p, x) pairs: polys is
+ * n x 4 coefficients, out[i] = p0 + p1 x + p2 x^2 + p3 x^3. */
+stark_status stark_eval_quartic_multi(stark_ctx* ctx, const uint64_t* polys, const uint64_t* xs, size_t n,
+                                      uint64_t* out);
+/* Field linear combination out[i] = sum_c coeffs[c] * cols[c][i] over n_cols
+ * columns of n elements (the shape of the L combination, prove.rs:287-322). */
+stark_status stark_lincomb(stark_ctx* ctx, const uint64_t* cols, uint32_t n_cols, size_t n, const uint64_t* coeffs,
+                           uint64_t* out);
+/* Device-resident form (columns back to back at d_cols); synchronous. */
+stark_status stark_lincomb_dev(stark_ctx* ctx, const uint64_t* d_cols, uint32_t n_cols, size_t n,
+                               const uint64_t* coeffs, uint64_t* d_out, void* stream);
 
 /* ---- Blake2s + index sampler (packages/fri/src/utils.rs) ------------------ */
 /* blake(message) -> Vec<u8> (fri/src/utils.rs:5-10): Blake2s-256, unkeyed. */

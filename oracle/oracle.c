@@ -403,6 +403,26 @@ void or_multi_interp_4(const fp (*xsets)[4], const fp (*ysets)[4], fp (*out)[4],
   free(eqs); free(inv_targets); free(inv_alls);
 }
 
+/* Canonical-limb entry points of multi_interp_4 and eval_quartic (one quartic per x). */
+void oracle_multi_interp_4(const uint64_t* xsets, const uint64_t* ysets, size_t rows, uint64_t* out) {
+  or_init();
+  fp* x = or_load(xsets, 4 * rows, 4 * rows);
+  fp* y = or_load(ysets, 4 * rows, 4 * rows);
+  fp* o = (fp*)malloc(sizeof(fp) * 4 * (rows ? rows : 1));
+  or_multi_interp_4((const fp (*)[4])x, (const fp (*)[4])y, (fp (*)[4])o, rows);
+  or_store(o, out, 4 * rows);
+  free(x); free(y); free(o);
+}
+
+void oracle_eval_quartic_multi(const uint64_t* polys, const uint64_t* xs, size_t n, uint64_t* out) {
+  or_init();
+  fp* p = or_load(polys, 4 * n, 4 * n);
+  fp* x = or_load(xs, n, n);
+  for (size_t i = 0; i < n; i++) x[i] = eval_quartic(p + 4 * i, x[i]);
+  or_store(x, out, n);
+  free(p); free(x);
+}
+
 /* ------------------------------------------------------------------ */
 /* Blake2s-256 (blake2 0.9.1; RFC 7693), used by fri/src/utils.rs:5-10   */
 /* and commitment/src/utils.rs:5-10.                                   */

@@ -117,6 +117,8 @@ class Oracle:
         L.oracle_root_of_unity.argtypes = [ctypes.c_uint32, u64p]
         L.oracle_multi_inv.argtypes = [u64p, ctypes.c_size_t, u64p]
         L.oracle_eval_poly_multi.argtypes = [u64p, ctypes.c_size_t, u64p, ctypes.c_size_t, u64p]
+        L.oracle_multi_interp_4.argtypes = [u64p, u64p, ctypes.c_size_t, u64p]
+        L.oracle_eval_quartic_multi.argtypes = [u64p, u64p, ctypes.c_size_t, u64p]
         L.oracle_blake2s.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         L.oracle_get_pseudorandom_indices.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
                                                       ctypes.c_size_t, ctypes.c_uint32,
@@ -170,6 +172,23 @@ class Oracle:
         x = np.ascontiguousarray(xs, dtype=np.uint64).reshape(-1, 4)
         out = np.zeros_like(x)
         self.lib.oracle_eval_poly_multi(self._p(p), len(p), self._p(x), len(x), self._p(out))
+        return out
+
+    def multi_interp_4(self, xsets: np.ndarray, ysets: np.ndarray) -> np.ndarray:
+        """poly_utils.rs:449-511: rows x 4 points -> rows x 4 coefficients."""
+        x = np.ascontiguousarray(xsets, dtype=np.uint64).reshape(-1, 4)
+        y = np.ascontiguousarray(ysets, dtype=np.uint64).reshape(-1, 4)
+        rows = len(x) // 4
+        out = np.zeros((4 * rows, 4), dtype=np.uint64)
+        self.lib.oracle_multi_interp_4(self._p(x), self._p(y), rows, self._p(out))
+        return out
+
+    def eval_quartic_multi(self, polys: np.ndarray, xs: np.ndarray) -> np.ndarray:
+        """eval_quartic (poly_utils.rs:442-446) of polys[i] (4 coefficients) at xs[i]."""
+        p = np.ascontiguousarray(polys, dtype=np.uint64).reshape(-1, 4)
+        x = np.ascontiguousarray(xs, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros_like(x)
+        self.lib.oracle_eval_quartic_multi(self._p(p), self._p(x), len(x), self._p(out))
         return out
 
     def blake2s(self, msg: bytes) -> bytes:

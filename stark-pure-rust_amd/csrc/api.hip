@@ -162,7 +162,7 @@ static stark_status fft_host(stark_ctx* ctx, const uint64_t* in, size_t len, con
   uint32_t log_len = 0;
   while (((size_t)1 << log_len) < len) ++log_len;
   const bool sparse = len && len < n && ((size_t)1 << log_len) == len && log_n >= 2 &&
-                      log_n - log_len <= ntt_first_log_r(log_n);
+                      log_n - log_len <= ntt_first_log_r(log_n);  // else zero fill (cheaper than a pad pass)
   if (sparse) {
     st = ensure_buf(ctx, ctx->io2, len * sizeof(fe));
     if (st != STARK_OK) return st;
@@ -275,6 +275,54 @@ stark_status stark_ntt_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uin
   stark_status st = get_twiddles(ctx, use_root, log_n, &tw);
   if (st != STARK_OK) return st;
   return ntt_device(ctx, (fe*)d_data, log_n, batch, *tw, inverse != 0, pick_stream(ctx, stream));
+}
+
+stark_status stark_lde_dev(stark_ctx* ctx, uint64_t* d_values, uint64_t* d_out, uint32_t log_steps,
+                           uint32_t log_blowup, uint32_t batch, const uint64_t g1[4], const uint64_t g2[4],
+                           void* stream) {
+  if (!ctx || !d_values || !d_out || !g1 || !g2 || d_values == d_out) return STARK_ERR_BAD_ARG;
+  if (log_steps + log_blowup > 28) return STARK_ERR_BAD_LENGTH;
+  if (batch == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  // g1 must be g2^(2^log_blowup) (prove.rs:71-94: g1 = g2^extension_factor).
+  const HostFp w2 = F.from_canonical(g2);
+  if (!FieldHost::eq(F.pow_u64(w2, (uint64_t)1 << log_blowup), F.from_canonical(g1))) return STARK_ERR_BAD_ROOT;
+  uint64_t g1_inv[4];
+  F.to_canonical(F.inv(F.from_canonical(g1)), g1_inv);
+  const Twiddles *t1 = nullptr, *t2 = nullptr;
+  stark_status st = get_twiddles(ctx, g1_inv, log_steps, &t1);
+  if (st != STARK_OK) return st;
+  st = get_twiddles(ctx, g2, log_steps + log_blowup, &t2);
+  if (st != STARK_OK) return st;
+  hipStream_t s = pick_stream(ctx, stream);
+  st = ntt_device(ctx, (fe*)d_values, log_steps, batch, *t1, true, s);  // inv_best_fft(values, g1)
+  if (st != STARK_OK) return st;
+  // best_fft(coefficients zero-padded to 2^(log_steps + log_blowup), g2)
+  return ntt_device_from(ctx, (const fe*)d_values, log_blowup, (fe*)d_out, log_steps + log_blowup, batch, *t2, false,
+                         s);
+}
+
+stark_status stark_lde(stark_ctx* ctx, const uint64_t* values, size_t steps, const uint64_t g1[4],
+                       uint32_t log_blowup, const uint64_t g2[4], uint64_t* out) {
+  if (!ctx || !values || !out || !g1 || !g2 || steps == 0 || (steps & (steps - 1))) return STARK_ERR_BAD_ARG;
+  uint32_t log_steps = 0;
+  while (((size_t)1 << log_steps) < steps) ++log_steps;
+  if (log_steps + log_blowup > 28) return STARK_ERR_BAD_LENGTH;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t prec = steps << log_blowup;
+  stark_status st = ensure_buf(ctx, ctx->io, prec * sizeof(fe));
+  if (st != STARK_OK) return st;
+  st = ensure_buf(ctx, ctx->io2, steps * sizeof(fe));
+  if (st != STARK_OK) return st;
+  fe* d_in = (fe*)ctx->io2.ptr;
+  fe* d_out = (fe*)ctx->io.ptr;
+  STARK_HIP(ctx, hipMemcpyAsync(d_in, values, steps * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  st = stark_lde_dev(ctx, (uint64_t*)d_in, (uint64_t*)d_out, log_steps, log_blowup, 1, g1, g2, nullptr);
+  if (st != STARK_OK) return st;
+  STARK_HIP(ctx, hipMemcpyAsync(out, d_out, prec * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
 }
 
 void stark_blake(const uint8_t* msg, size_t len, uint8_t out[32]) { b2s_host(msg, len, out); }

@@ -113,6 +113,92 @@ __global__ void powers_kernel(const fe* __restrict__ lo, const fe* __restrict__ 
   fe_store(out + i, fe_mul(fe_mul(lo[i & (((uint64_t)1 << kb) - 1)], hi[i >> kb]), unit));
 }
 
+// ---- multi_interp_4 / eval_quartic (poly_utils.rs:442-511) ----
+// Row values are taken to Montgomery form on load (montmul by R^2), combined
+// with Montgomery products and returned canonical (montmul by canonical 1).
+
+// The four basis numerators eq_k (coefficients, Montgomery) of the cubic
+// through x0..x3 (poly_utils.rs:458-486).
+__device__ __forceinline__ void interp4_eqs(const fe x[4], const fe& one, fe eq[4][4]) {
+  const fe x01 = fe_mul(x[0], x[1]), x02 = fe_mul(x[0], x[2]), x03 = fe_mul(x[0], x[3]);
+  const fe x12 = fe_mul(x[1], x[2]), x13 = fe_mul(x[1], x[3]), x23 = fe_mul(x[2], x[3]);
+  const fe z = fe_zero();
+  eq[0][0] = fe_sub(z, fe_mul(x12, x[3]));
+  eq[0][1] = fe_add(fe_add(x12, x13), x23);
+  eq[0][2] = fe_sub(fe_sub(fe_sub(z, x[1]), x[2]), x[3]);
+  eq[1][0] = fe_sub(z, fe_mul(x02, x[3]));
+  eq[1][1] = fe_add(fe_add(x02, x03), x23);
+  eq[1][2] = fe_sub(fe_sub(fe_sub(z, x[0]), x[2]), x[3]);
+  eq[2][0] = fe_sub(z, fe_mul(x01, x[3]));
+  eq[2][1] = fe_add(fe_add(x01, x03), x13);
+  eq[2][2] = fe_sub(fe_sub(fe_sub(z, x[0]), x[1]), x[3]);
+  eq[3][0] = fe_sub(z, fe_mul(x01, x[2]));
+  eq[3][1] = fe_add(fe_add(x01, x02), x12);
+  eq[3][2] = fe_sub(fe_sub(fe_sub(z, x[0]), x[1]), x[2]);
+  for (int k = 0; k < 4; ++k) eq[k][3] = one;
+}
+
+// eval_quartic with Montgomery p and x: p0 + p1 x + p2 x^2 + p3 x^3.
+__device__ __forceinline__ fe quartic_m(const fe p[4], const fe& x) {
+  const fe xsq = fe_mul(x, x), xcb = fe_mul(xsq, x);
+  return fe_add(fe_add(fe_add(p[0], fe_mul(p[1], x)), fe_mul(p[2], xsq)), fe_mul(p[3], xcb));
+}
+
+__device__ __forceinline__ fe canon_unit() {
+  fe u = fe_zero();
+  u.w[0] = 1;
+  return u;
+}
+
+// den[4 i + k] = eq_k(x_k) of row i (canonical), the batch inverse's targets.
+__global__ void interp4_den_kernel(const fe* __restrict__ xs, uint64_t rows, fe* __restrict__ den, MontConsts mc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  fe x[4], eq[4][4];
+  for (int k = 0; k < 4; ++k) x[k] = fe_mul(fe_load(xs + 4 * i + k), mc.r2);
+  interp4_eqs(x, mc.one, eq);
+  const fe unit = canon_unit();
+  for (int k = 0; k < 4; ++k) fe_store(den + 4 * i + k, fe_mul(quartic_m(eq[k], x[k]), unit));
+}
+
+// out[i][j] = sum_k eq_k[j] * y_k * inv(den_k) (poly_utils.rs:496-506).
+__global__ void interp4_out_kernel(const fe* __restrict__ xs, const fe* __restrict__ ys, const fe* __restrict__ inv,
+                                   uint64_t rows, fe* __restrict__ out, MontConsts mc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  fe x[4], eq[4][4], iy[4];
+  for (int k = 0; k < 4; ++k) x[k] = fe_mul(fe_load(xs + 4 * i + k), mc.r2);
+  interp4_eqs(x, mc.one, eq);
+  for (int k = 0; k < 4; ++k)  // canonical y times the Montgomery image of inv: canonical y inv
+    iy[k] = fe_mul(fe_load(ys + 4 * i + k), fe_mul(fe_load(inv + 4 * i + k), mc.r2));
+  for (int j = 0; j < 4; ++j) {  // Montgomery eq times canonical y inv: canonical
+    fe acc = fe_mul(eq[0][j], iy[0]);
+    for (int k = 1; k < 4; ++k) acc = fe_add(acc, fe_mul(eq[k][j], iy[k]));
+    fe_store(out + 4 * i + j, acc);
+  }
+}
+
+// out[i] = eval_quartic(polys[i], xs[i]) (poly_utils.rs:442-446), canonical.
+__global__ void eval_quartic_kernel(const fe* __restrict__ polys, const fe* __restrict__ xs, uint64_t n,
+                                    fe* __restrict__ out, MontConsts mc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const fe x = fe_mul(fe_load(xs + i), mc.r2), xsq = fe_mul(x, x), xcb = fe_mul(xsq, x);
+  const fe* p = polys + 4 * i;
+  fe_store(out + i, fe_add(fe_add(fe_add(fe_load(p), fe_mul(fe_load(p + 1), x)), fe_mul(fe_load(p + 2), xsq)),
+                           fe_mul(fe_load(p + 3), xcb)));
+}
+
+// out[i] = sum_c coef[c] * cols[c][i] (coef Montgomery, data canonical).
+__global__ void lincomb_kernel(const fe* __restrict__ cols, uint32_t n_cols, uint64_t n, const fe* __restrict__ coef,
+                               fe* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe acc = fe_zero();
+  for (uint32_t c = 0; c < n_cols; ++c) acc = fe_add(acc, fe_mul(fe_load(cols + (uint64_t)c * n + i), coef[c]));
+  fe_store(out + i, acc);
+}
+
 MontConsts mont_consts() {
   const FieldHost& F = FieldHost::get();
   MontConsts mc;
@@ -262,6 +348,95 @@ stark_status stark_eval_poly_at_multi(stark_ctx* ctx, const uint64_t* poly, size
   hipLaunchKernelGGL(eval_poly_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_poly,
                      (uint64_t)deg_plus_1, d_xs, (uint64_t)n, d_out, mont_consts());
   STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipMemcpyAsync(out, d_out, n * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return STARK_OK;
+}
+
+stark_status stark_multi_interp_4(stark_ctx* ctx, const uint64_t* xsets, const uint64_t* ysets, size_t rows,
+                                  uint64_t* out) {
+  if (!ctx || (rows && (!xsets || !ysets || !out))) return STARK_ERR_BAD_ARG;
+  if (rows == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t m = 4 * rows;
+  stark_status st = ensure_buf(ctx, ctx->io, 5 * m * sizeof(fe));
+  if (st != STARK_OK) return st;
+  fe* d_x = (fe*)ctx->io.ptr;
+  fe* d_y = d_x + m;
+  fe* d_den = d_y + m;
+  fe* d_inv = d_den + m;
+  fe* d_out = d_inv + m;
+  hipStream_t s = ctx->stream;
+  STARK_HIP(ctx, hipMemcpyAsync(d_x, xsets, m * sizeof(fe), hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(d_y, ysets, m * sizeof(fe), hipMemcpyHostToDevice, s));
+  const MontConsts mc = mont_consts();
+  const unsigned grid = (unsigned)((rows + 255) / 256);
+  hipLaunchKernelGGL(interp4_den_kernel, dim3(grid), dim3(256), 0, s, (const fe*)d_x, (uint64_t)rows, d_den, mc);
+  STARK_HIP(ctx, hipGetLastError());
+  st = multi_inv_device(ctx, d_den, d_inv, m, s);  // zero-preserving, like multi_inv (poly_utils.rs:38-70)
+  if (st != STARK_OK) return st;
+  hipLaunchKernelGGL(interp4_out_kernel, dim3(grid), dim3(256), 0, s, (const fe*)d_x, (const fe*)d_y,
+                     (const fe*)d_inv, (uint64_t)rows, d_out, mc);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipMemcpyAsync(out, d_out, m * sizeof(fe), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  return STARK_OK;
+}
+
+stark_status stark_eval_quartic_multi(stark_ctx* ctx, const uint64_t* polys, const uint64_t* xs, size_t n,
+                                      uint64_t* out) {
+  if (!ctx || (n && (!polys || !xs || !out))) return STARK_ERR_BAD_ARG;
+  if (n == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  stark_status st = ensure_buf(ctx, ctx->io, 6 * n * sizeof(fe));
+  if (st != STARK_OK) return st;
+  fe* d_p = (fe*)ctx->io.ptr;
+  fe* d_x = d_p + 4 * n;
+  fe* d_o = d_x + n;
+  hipStream_t s = ctx->stream;
+  STARK_HIP(ctx, hipMemcpyAsync(d_p, polys, 4 * n * sizeof(fe), hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(d_x, xs, n * sizeof(fe), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(eval_quartic_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const fe*)d_p,
+                     (const fe*)d_x, (uint64_t)n, d_o, mont_consts());
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipMemcpyAsync(out, d_o, n * sizeof(fe), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  return STARK_OK;
+}
+
+stark_status stark_lincomb_dev(stark_ctx* ctx, const uint64_t* d_cols, uint32_t n_cols, size_t n,
+                               const uint64_t* coeffs, uint64_t* d_out, void* stream) {
+  if (!ctx || !d_out || (n_cols && (!d_cols || !coeffs))) return STARK_ERR_BAD_ARG;
+  if (n == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  std::vector<fe> h(n_cols ? n_cols : 1);
+  for (uint32_t c = 0; c < n_cols; ++c) h[c] = to_dev(F.from_canonical(coeffs + 4 * c));  // Montgomery
+  stark_status st = ensure_buf(ctx, ctx->io2, h.size() * sizeof(fe));
+  if (st != STARK_OK) return st;
+  hipStream_t s = pick_stream(ctx, stream);
+  STARK_HIP(ctx, hipMemcpyAsync(ctx->io2.ptr, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const fe*)d_cols, n_cols,
+                     (uint64_t)n, (const fe*)ctx->io2.ptr, (fe*)d_out);
+  STARK_HIP(ctx, hipGetLastError());
+  // h is pageable and goes out of scope: the copy must have consumed it.
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  return STARK_OK;
+}
+
+stark_status stark_lincomb(stark_ctx* ctx, const uint64_t* cols, uint32_t n_cols, size_t n, const uint64_t* coeffs,
+                           uint64_t* out) {
+  if (!ctx || (n && !out) || (n && n_cols && (!cols || !coeffs))) return STARK_ERR_BAD_ARG;
+  if (n == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  stark_status st = ensure_buf(ctx, ctx->io, ((size_t)n_cols + 1) * n * sizeof(fe));
+  if (st != STARK_OK) return st;
+  fe* d_cols = (fe*)ctx->io.ptr;
+  fe* d_out = d_cols + (size_t)n_cols * n;
+  if (n_cols)
+    STARK_HIP(ctx, hipMemcpyAsync(d_cols, cols, (size_t)n_cols * n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  st = stark_lincomb_dev(ctx, (const uint64_t*)d_cols, n_cols, n, coeffs, (uint64_t*)d_out, nullptr);
+  if (st != STARK_OK) return st;
   STARK_HIP(ctx, hipMemcpyAsync(out, d_out, n * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
   STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return STARK_OK;

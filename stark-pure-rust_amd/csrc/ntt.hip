@@ -246,6 +246,17 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
   }
 }
 
+// dst[c][i] = i < 2^log_m ? src[c][i] : 0 (best_fft's zero padding, fft.rs:327-357).
+__global__ void pad_kernel(const fe* __restrict__ src, fe* __restrict__ dst, uint32_t log_m, uint32_t log_n,
+                           uint64_t total) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const uint64_t c = g >> log_n, i = g & (((uint64_t)1 << log_n) - 1);
+  fe v = fe_zero();
+  if ((i >> log_m) == 0) v = fe_load(src + (c << log_m) + i);
+  fe_store(dst + g, v);
+}
+
 // n = 2 (best_fft with log_order_of_root = 1): out = (a + b, a - b) [* 1/2].
 __global__ void ntt2_kernel(fe* d, fe scale, int do_scale) {
   const size_t off = (size_t)blockIdx.x * 2;
@@ -464,9 +475,13 @@ stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t bat
 stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
                              uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream) {
   if (batch == 0) return STARK_OK;
-  if (src && (log_n < 2 || zero_log > plan_passes(log_n).log_r[0])) return STARK_ERR_BAD_ARG;
-  if (src && zero_log == 0) {
-    STARK_HIP(ctx, hipMemcpyAsync(d_data, src, ((size_t)batch << log_n) * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+  if (src && zero_log > log_n) return STARK_ERR_BAD_ARG;
+  if (src && (zero_log == 0 || log_n < 2 || zero_log > plan_passes(log_n).log_r[0])) {
+    // Not expressible as a sparse first pass: materialise the padded columns.
+    const uint64_t total = (uint64_t)batch << log_n;
+    hipLaunchKernelGGL(pad_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src, d_data,
+                       log_n - zero_log, log_n, total);
+    STARK_HIP(ctx, hipGetLastError());
     src = nullptr;
   }
   if (((uint64_t)batch << log_n) > ((uint64_t)1 << 34)) return STARK_ERR_BAD_ARG;

@@ -89,6 +89,13 @@ _SIGNATURES = {
     "stark_r1cs_trace_export": ([_vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _szp, _u64p, _szp], ctypes.c_int),
     "stark_r1cs_trace_free": ([_vp], None),
     "stark_prove_r1cs_trace": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_lde": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p, _u64p], ctypes.c_int),
+    "stark_lde_dev": ([_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, _vp],
+                      ctypes.c_int),
+    "stark_multi_interp_4": ([_vp, _u64p, _u64p, ctypes.c_size_t, _u64p], ctypes.c_int),
+    "stark_eval_quartic_multi": ([_vp, _u64p, _u64p, ctypes.c_size_t, _u64p], ctypes.c_int),
+    "stark_lincomb": ([_vp, _u64p, ctypes.c_uint32, ctypes.c_size_t, _u64p, _u64p], ctypes.c_int),
+    "stark_lincomb_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, _vp, _vp], ctypes.c_int),
     "stark_ntt_strided_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, ctypes.c_int, _vp], ctypes.c_int),
     "stark_ntt_strided_tw_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_size_t, _u64p, ctypes.c_int, _u64p,
                                   ctypes.c_uint32, ctypes.c_uint64, _vp], ctypes.c_int),
@@ -261,6 +268,50 @@ class Context:
         self.check(self.lib.stark_eval_poly_at_multi(self.h, _p64(p), len(p), _p64(x), len(x), _p64(out)),
                    "eval_poly_at")
         return out
+
+    def multi_interp_4(self, xsets, ysets) -> np.ndarray:
+        """multi_interp_4 (poly_utils.rs:449-511): rows x 4 points -> rows x 4 coefficients
+        (element arrays of 4 * rows elements, row-major)."""
+        x, y = _elems(xsets), _elems(ysets)
+        if len(x) != len(y) or len(x) % 4:
+            raise ValueError("multi_interp_4: xsets and ysets need 4 elements per row, same row count")
+        out = np.empty_like(x)
+        self.check(self.lib.stark_multi_interp_4(self.h, _p64(x), _p64(y), len(x) // 4, _p64(out)), "multi_interp_4")
+        return out
+
+    def eval_quartic_multi(self, polys, xs) -> np.ndarray:
+        """[eval_quartic(p_i, x_i)] (poly_utils.rs:442-446); polys holds 4 coefficients per x."""
+        p, x = _elems(polys), _elems(xs)
+        if len(p) != 4 * len(x):
+            raise ValueError("eval_quartic_multi: 4 coefficients per point")
+        out = np.empty_like(x)
+        self.check(self.lib.stark_eval_quartic_multi(self.h, _p64(p), _p64(x), len(x), _p64(out)), "eval_quartic")
+        return out
+
+    def lincomb(self, cols, coeffs) -> np.ndarray:
+        """out[i] = sum_c coeffs[c] * cols[c][i]; cols is n_cols x n elements (row-major)."""
+        c = _elems(coeffs)
+        v = _elems(cols)
+        n_cols = len(c)
+        if n_cols == 0 or len(v) % n_cols:
+            raise ValueError("lincomb: cols must hold n_cols equal columns")
+        n = len(v) // n_cols
+        out = np.empty((n, 4), dtype=np.uint64)
+        self.check(self.lib.stark_lincomb(self.h, _p64(v), n_cols, n, _p64(c), _p64(out)), "lincomb")
+        return out
+
+    def lde(self, values, g1, log_blowup: int, g2) -> np.ndarray:
+        """inv_best_fft(values, g1) then best_fft(padded, g2) (prove.rs:100-101)."""
+        v = _elems(values)
+        out = np.empty((len(v) << log_blowup, 4), dtype=np.uint64)
+        self.check(self.lib.stark_lde(self.h, _p64(v), len(v), _p64(_limbs(g1)), log_blowup, _p64(_limbs(g2)),
+                                      _p64(out)), "lde")
+        return out
+
+    def lde_dev(self, d_values: int, d_out: int, log_steps: int, log_blowup: int, batch: int, g1, g2,
+                stream: int = 0) -> None:
+        self.check(self.lib.stark_lde_dev(self.h, d_values, d_out, log_steps, log_blowup, batch, _p64(_limbs(g1)),
+                                          _p64(_limbs(g2)), stream or None), "lde_dev")
 
     # ---- device memory (plumbing) -------------------------------------------
     def alloc(self, nbytes: int) -> int:

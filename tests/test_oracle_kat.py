@@ -178,3 +178,31 @@ def test_random_elements_canonical():
     a = O.from_limbs(O.random_elements(1000, 5))
     assert all(0 <= x < O.P for x in a)
     assert len(set(a)) == 1000
+
+
+def test_multi_interp_4_and_eval_quartic(oracle):
+    """The C multi_interp_4 (poly_utils.rs:449-511) against the Python lagrange_interp on 4 points
+    (poly_utils.rs:409-439), and eval_quartic (:442-446) against direct evaluation: the interpolant
+    passes through every point; a row with a repeated x has a zero denominator, which multi_inv maps
+    to zero (its contributions vanish)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    from stark_verify import lagrange_interp
+    rows = 40
+    xs = O.from_limbs(O.random_elements(4 * rows, 71))
+    ys = O.from_limbs(O.random_elements(4 * rows, 72))
+    xs[4 * 7 + 2] = xs[4 * 7 + 1]  # row 7: duplicate x
+    got = O.from_limbs(oracle.multi_interp_4(O.to_limbs(xs), O.to_limbs(ys)))
+    for r in range(rows):
+        c = got[4 * r:4 * r + 4]
+        if r != 7:
+            assert c == lagrange_interp(xs[4 * r:4 * r + 4], ys[4 * r:4 * r + 4])
+            for k in range(4):
+                x = xs[4 * r + k]
+                assert (c[0] + c[1] * x + c[2] * x * x + c[3] * x ** 3) % O.P == ys[4 * r + k]
+    px = O.from_limbs(O.random_elements(4 * rows, 73))
+    at = O.from_limbs(O.random_elements(rows, 74))
+    q = O.from_limbs(oracle.eval_quartic_multi(O.to_limbs(px), O.to_limbs(at)))
+    for i in range(rows):
+        p, x = px[4 * i:4 * i + 4], at[i]
+        assert q[i] == (p[0] + p[1] * x + p[2] * x * x + p[3] * x ** 3) % O.P
