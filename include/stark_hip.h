@@ -223,6 +223,13 @@ stark_status stark_r1cs_trace_export(const stark_r1cs_trace* trace, uint64_t* wi
 void stark_r1cs_trace_free(stark_r1cs_trace* trace);
 /* prove_with_witness (run.rs:310-452) = stark_mk_r1cs_proof on a built trace. */
 stark_status stark_prove_r1cs_trace(stark_ctx* ctx, const stark_r1cs_trace* trace, stark_r1cs_proof** out);
+/* prove_with_witness (run.rs:310-452) with the trace built on the GPU: the raw
+ * .r1cs / .wtns bytes are parsed (headers and record counts on the host), the
+ * trace columns, flags and permutation are constructed in HBM and proved in
+ * place.  The proof is identical to stark_r1cs_trace_build +
+ * stark_prove_r1cs_trace on the same bytes. */
+stark_status stark_prove_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                                    size_t wtns_len, stark_r1cs_proof** out);
 
 /* ---- multi-GPU four-step NTT building blocks (no reference counterpart;
  * the reference is single-process).  The exchanges are RCCL

@@ -90,6 +90,7 @@ struct stark_ctx {
   stark::DevBuf io2;
   stark::DevBuf fri_cols;    // folded FRI columns (prove_low_degree)
   stark::DevBuf r1cs_arena;  // mk_r1cs_proof working set
+  stark::DevBuf trace_arena;  // device trace builder working set (r1cs_trace_dev.hip)
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -168,6 +169,42 @@ struct JsonPieces {
   void render(std::string& o);
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
+
+// R1CS v1 / wtns v2 headers (circom2bellman_core/src/reader.rs:4-89,
+// r1cs-stark/src/reader.rs:7-42), r1cs_trace.hip.
+struct R1csHeader {
+  uint32_t n_wires, n_pub_out, n_pub_in, n_constraints;
+  size_t cons_off;  // byte offset of the first constraint
+};
+struct WtnsHeader {
+  uint32_t field_size, n_wit;
+  size_t values_off;  // byte offset of witness value 0
+};
+stark_status parse_r1cs_header(const uint8_t* r1cs, size_t len, R1csHeader* h);
+stark_status parse_wtns_header(const uint8_t* wtns, size_t len, WtnsHeader* h);
+
+// The R1CS trace built on the device (r1cs_trace_dev.hip): the host
+// builder's columns (coefficients, witness, computational as canonical
+// elements; flags as bytes; permutation as u64 slots) in ctx->trace_arena,
+// plus the small host-side public inputs.
+struct DevTrace {
+  size_t os = 0, n_constraints = 0, n_wires = 0;
+  fe *coef = nullptr, *wit = nullptr, *comp = nullptr;
+  uint8_t* flags = nullptr;
+  uint64_t* perm = nullptr;
+  std::vector<uint64_t> public_wires;       // canonical limbs, 4 per wire
+  std::vector<size_t> public_first_indices;  // (wire, slot) pairs
+};
+stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                               size_t wtns_len, DevTrace* out);
+// mk_r1cs_proof on trace columns given as host or device pointers, flags as
+// bytes (r1cs.hip).
+stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
+                                      const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                      size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                      const size_t* permuted_indices, const uint64_t* coefficients,
+                                      const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
+                                      stark_r1cs_proof** out);
 
 // FRI prover on device values (fri.hip).  fri_enqueue puts every layer on the
 // context stream with a device-side transcript and queues the roots' download;

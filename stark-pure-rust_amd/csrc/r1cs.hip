@@ -602,22 +602,23 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     }
     STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
   }
-  // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).
+  // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).  The
+  // inputs may be host or device pointers (the device trace builder's columns): hipMemcpyDefault.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
   for (int c = 0; c < 6; ++c) {
     if (!(flag_bytes && c >= 1 && c <= 3))
-      STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyHostToDevice, s));
+      STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyDefault, s));
     if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
   }
   if (flag_bytes) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
     uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel
-    STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyHostToDevice, s));
+    STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyDefault, s));
     hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
                        (uint64_t)os, steps, raw + steps);
     STARK_HIP(ctx, hipGetLastError());
   }
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
-  STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   clk.mark("setup + uploads enqueued");
   STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));

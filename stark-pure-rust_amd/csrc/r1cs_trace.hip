@@ -184,6 +184,45 @@ void push_canon(std::vector<uint64_t>& v, const HostFp& x) {
 }
 
 }  // namespace
+
+stark_status parse_r1cs_header(const uint8_t* r1cs, size_t len, R1csHeader* h) {
+  if (!r1cs || !h) return STARK_ERR_BAD_ARG;
+  Cursor c{r1cs, len};
+  if (c.u32() != 0x73633172u /* "r1cs" */ || c.u32() != 1 || c.u32() != 3 || c.u32() != 1) return STARK_ERR_BAD_ARG;
+  c.u64();
+  c.u32();  // field_size
+  const uint8_t* prime = c.raw(32);
+  h->n_wires = c.u32();
+  h->n_pub_out = c.u32();
+  h->n_pub_in = c.u32();
+  c.u32();  // n_private_inputs
+  c.u64();  // n_labels
+  h->n_constraints = c.u32();
+  if (!c.ok || memcmp(prime, kBn254R, 32) != 0) return STARK_ERR_BAD_ARG;  // run.rs:344-350
+  if (c.u32() != 2) return STARK_ERR_BAD_ARG;                               // ConstraintSection
+  c.u64();
+  if (!c.ok || h->n_wires == 0) return STARK_ERR_BAD_ARG;
+  h->cons_off = len - c.left;
+  return STARK_OK;
+}
+
+stark_status parse_wtns_header(const uint8_t* wtns, size_t len, WtnsHeader* h) {
+  if (!wtns || !h) return STARK_ERR_BAD_ARG;
+  Cursor w{wtns, len};
+  if (w.u32() != 1936618615u) return STARK_ERR_BAD_ARG;  // "wtns"
+  for (int i = 0; i < 5; ++i) w.u32();
+  h->field_size = w.u32();
+  if (h->field_size == 0 || h->field_size > 32 || h->field_size % 4) return STARK_ERR_BAD_ARG;
+  w.raw(h->field_size);
+  h->n_wit = w.u32();
+  w.u32();
+  w.u32();
+  w.u32();
+  if (!w.ok || (uint64_t)h->n_wit * h->field_size > w.left) return STARK_ERR_BAD_ARG;
+  h->values_off = len - w.left;
+  return STARK_OK;
+}
+
 }  // namespace stark
 
 using namespace stark;
@@ -197,20 +236,12 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
   PhaseClock clk("r1cs trace build");
   const FieldHost& F = FieldHost::get();
   // ---- read_r1cs (reader.rs:4-89): header section, then constraints, in that order.
-  Cursor c{r1cs, r1cs_len};
-  if (c.u32() != 0x73633172u /* "r1cs" */ || c.u32() != 1 || c.u32() != 3 || c.u32() != 1) return STARK_ERR_BAD_ARG;
-  c.u64();
-  c.u32();  // field_size
-  const uint8_t* prime = c.raw(32);
-  const uint32_t n_wires = c.u32();
-  const uint32_t n_pub_out = c.u32();
-  const uint32_t n_pub_in = c.u32();
-  c.u32();  // n_private_inputs
-  c.u64();  // n_labels
-  const uint32_t n_constraints = c.u32();
-  if (!c.ok || memcmp(prime, kBn254R, 32) != 0) return STARK_ERR_BAD_ARG;  // run.rs:344-350
-  if (c.u32() != 2) return STARK_ERR_BAD_ARG;                               // ConstraintSection
-  c.u64();
+  R1csHeader hd;
+  stark_status hst = parse_r1cs_header(r1cs, r1cs_len, &hd);
+  if (hst != STARK_OK) return hst;
+  const uint32_t n_wires = hd.n_wires, n_pub_out = hd.n_pub_out, n_pub_in = hd.n_pub_in;
+  const uint32_t n_constraints = hd.n_constraints;
+  Cursor c{r1cs + hd.cons_off, r1cs_len - hd.cons_off};
   // All coefficients in file order (wire id + pointer to the 32-B value in
   // the file); factor k = coefs[fac_off[k], fac_off[k+1]).  Pooled buffers:
   // every entry read is written first.
@@ -240,21 +271,14 @@ stark_status stark_r1cs_trace_build(const uint8_t* r1cs, size_t r1cs_len, const 
 
   clk.mark("read_r1cs");
   // ---- read_witness (r1cs-stark/src/reader.rs:7-42)
-  Cursor w{wtns, wtns_len};
-  if (w.u32() != 1936618615u) return STARK_ERR_BAD_ARG;  // "wtns"
-  for (int i = 0; i < 5; ++i) w.u32();
-  const uint32_t field_size = w.u32();
-  if (field_size == 0 || field_size > 32 || field_size % 4) return STARK_ERR_BAD_ARG;
-  w.raw(field_size);
-  const uint32_t n_wit = w.u32();
-  w.u32();
-  w.u32();
-  w.u32();
-  if (!w.ok || (uint64_t)n_wit * field_size > w.left) return STARK_ERR_BAD_ARG;
+  WtnsHeader wh;
+  hst = parse_wtns_header(wtns, wtns_len, &wh);
+  if (hst != STARK_OK) return hst;
+  const uint32_t field_size = wh.field_size, n_wit = wh.n_wit;
   // from_bytes_le reduces mod p (run.rs:354-357): wcan holds the canonical
   // values (the trace's witness column), witness their Montgomery images (the
   // products' right operand).
-  const uint8_t* wbytes = w.raw((size_t)n_wit * field_size);
+  const uint8_t* wbytes = wtns + wh.values_off;
   U64Array wbuf;
   if (!wbuf.alloc((size_t)8 * n_wit + 8)) return STARK_ERR_OOM;
   HostFp* witness = reinterpret_cast<HostFp*>(wbuf.data());

@@ -1,0 +1,318 @@
+// R1CS trace construction on the GPU: the same trace as the host builder
+// (r1cs_trace.hip, restating run.rs:109-308 and :388-419), built in HBM from
+// the raw .r1cs / .wtns bytes so the prover reads it without a host round trip.
+//
+//   host   header parse + one walk over the constraint records' counts
+//          (factor offsets, the per-constraint slot bases)
+//   GPU    witness decode (from_bytes_le: reduce mod p; canonical + Montgomery)
+//          slot fill: one thread per (constraint, factor) writes its slots'
+//            coefficient, witness and running-sum (computational) values and
+//            the (wire, slot) pair of every use in push order
+//          flags (calc_flags, run.rs:283-308)
+//          stable radix sort of the uses by wire (hipCUB), then the cyclic
+//            permutation of each wire's uses (run.rs:388-401) and the first
+//            use of every public wire (run.rs:411-419)
+//
+// Malformed input (a wire id >= n_wires inside a record) is flagged on the
+// device and reported as STARK_ERR_BAD_ARG, like the host builder.
+#include <string.h>
+
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "internal.h"
+
+namespace stark {
+
+namespace {
+
+__device__ __forceinline__ fe reduce_any(fe v) {  // any 256-bit value < 5.3 p -> canonical
+#pragma unroll
+  for (int t = 0; t < 5; ++t) fe_reduce_once(v);
+  return v;
+}
+
+// from_bytes_le of witness values of `words` 32-bit words (run.rs:354-357).
+__global__ void wit_decode_kernel(const uint32_t* __restrict__ w, uint32_t words, uint64_t n, fe r2,
+                                  fe* __restrict__ wcan, fe* __restrict__ wmont) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe v = fe_zero();
+  for (uint32_t k = 0; k < words; ++k) v.w[k] = w[i * words + k];
+  v = reduce_any(v);
+  fe_store(wcan + i, v);
+  fe_store(wmont + i, fe_mul(v, r2));
+}
+
+struct FillArgs {
+  const uint8_t* cons;      // constraint section (first constraint at offset 0)
+  const uint32_t* fac_rec;  // byte offset of factor k's first record
+  const uint32_t* fac_cnt;  // records of factor k
+  const uint32_t* base;     // first slot of constraint ci (n_constraints + 1 entries)
+  uint32_t n_constraints, n_wires;
+  uint64_t a_len;
+  const fe* wcan;
+  const fe* wmont;
+  fe *coef, *wit, *comp;
+  uint32_t *keys, *vals;
+  uint32_t* err;
+};
+
+// calc_coefficients_and_witness (run.rs:109-281): factor f of constraint ci
+// owns slots base[ci] .. base[ci+1]-1 of third f; a slot past the factor's
+// records is padding (last wire, coefficient 0, running sum unchanged).
+__global__ void slot_fill_kernel(FillArgs a) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * (uint64_t)a.n_constraints) return;
+  const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
+  const uint32_t b0 = a.base[ci], n_coeff = a.base[ci + 1] - b0;
+  const uint32_t cnt = a.fac_cnt[t];
+  const uint8_t* rec = a.cons + a.fac_rec[t];
+  fe tacc = fe_zero();
+  const uint64_t push0 = 3 * (uint64_t)b0 + (uint64_t)f * n_coeff;
+  for (uint32_t i = 0; i < n_coeff; ++i) {
+    const uint64_t slot = (uint64_t)f * a.a_len + b0 + i;
+    uint32_t wire = a.n_wires - 1;
+    fe cf = fe_zero();
+    if (i < cnt) {
+      const uint32_t* r = reinterpret_cast<const uint32_t*>(rec + 36 * (uint64_t)i);
+      wire = r[0];
+      if (wire >= a.n_wires) {
+        atomicOr(a.err, 1u);
+        wire = a.n_wires - 1;
+      }
+      fe v;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v.w[k] = r[1 + k];
+      cf = reduce_any(v);                                       // canonical from_bytes_le
+      tacc = fe_add(tacc, fe_mul(cf, fe_load(a.wmont + wire)));  // canonical * Montgomery
+    }
+    fe_store(a.coef + slot, cf);
+    fe_store(a.wit + slot, fe_load(a.wcan + wire));
+    fe_store(a.comp + slot, tacc);
+    a.keys[push0 + i] = wire;
+    a.vals[push0 + i] = (uint32_t)slot;
+  }
+}
+
+// calc_flags (run.rs:283-308): flag1 = 0 at (last slot + 1) mod a_len in every
+// third, flag2 = 1 at each constraint's last slot (first third).
+__global__ void flags_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
+                             uint8_t* __restrict__ f1, uint8_t* __restrict__ f2) {
+  const uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= n_constraints) return;
+  const uint64_t e = base[ci + 1];
+  const uint64_t k = e % a_len;
+  f1[k] = 0;
+  f1[k + a_len] = 0;
+  f1[k + 2 * a_len] = 0;
+  f2[e - 1] = 1;
+}
+
+__global__ void group_last_kernel(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ last) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t k = keys[j];
+  if (j + 1 == n || keys[j + 1] != k) last[k] = (uint32_t)j;
+}
+
+// Each wire's uses, in push order, form one cycle (run.rs:388-401): a use
+// points at the previous use, the first at the last.  pf[w] = first use of
+// public wire w (run.rs:411-419).
+__global__ void perm_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, uint64_t n,
+                            const uint32_t* __restrict__ last, uint32_t n_public, uint64_t* __restrict__ perm,
+                            uint64_t* __restrict__ pf) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t k = keys[j];
+  const bool start = j == 0 || keys[j - 1] != k;
+  perm[vals[j]] = start ? vals[last[k]] : vals[j - 1];
+  if (start && k < n_public) pf[k] = vals[j];
+}
+
+unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                               size_t wtns_len, DevTrace* out) {
+  PhaseClock clk("r1cs trace build (device)");
+  const FieldHost& F = FieldHost::get();
+  R1csHeader hd;
+  stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
+  if (st != STARK_OK) return st;
+  WtnsHeader wh;
+  st = parse_wtns_header(wtns, wtns_len, &wh);
+  if (st != STARK_OK) return st;
+  const uint32_t n_c = hd.n_constraints, n_wires = hd.n_wires, n_wit = wh.n_wit;
+  const size_t n_public = 1 + (size_t)hd.n_pub_in + hd.n_pub_out;  // run.rs:359-360
+  if (n_wit < n_wires || n_public > n_wit) return STARK_ERR_BAD_ARG;
+  // witness[0] must be 1 (run.rs:358); the public wires are the first n_public values.
+  const uint8_t* wv = wtns + wh.values_off;
+  {
+    const HostFp w0 = F.reduce_bytes_le(wv, wh.field_size);
+    if (!(w0.v[0] == 1 && w0.v[1] == 0 && w0.v[2] == 0 && w0.v[3] == 0)) return STARK_ERR_BAD_ARG;
+  }
+  out->public_wires.resize(4 * n_public);
+  for (size_t i = 0; i < n_public; ++i) {
+    const HostFp v = F.reduce_bytes_le(wv + i * wh.field_size, wh.field_size);
+    memcpy(&out->public_wires[4 * i], v.v, 32);
+  }
+
+  // Host walk: record counts only (the records themselves are read on the GPU).
+  const uint8_t* cons = r1cs + hd.cons_off;
+  const size_t cons_len = r1cs_len - hd.cons_off;
+  if (cons_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  std::vector<uint32_t> fac((size_t)6 * n_c + 1);  // fac_rec[3 n_c] | fac_cnt[3 n_c] | pad
+  std::vector<uint32_t> base((size_t)n_c + 1);
+  uint32_t* fac_rec = fac.data();
+  uint32_t* fac_cnt = fac.data() + (size_t)3 * n_c;
+  {
+    size_t pos = 0;
+    uint64_t b = 0;
+    base[0] = 0;
+    for (uint32_t ci = 0; ci < n_c; ++ci) {
+      uint32_t n_coeff = 0;
+      for (int f = 0; f < 3; ++f) {
+        if (cons_len - pos < 4) return STARK_ERR_BAD_ARG;
+        uint32_t nc;
+        memcpy(&nc, cons + pos, 4);
+        pos += 4;
+        if (nc > (cons_len - pos) / 36) return STARK_ERR_BAD_ARG;
+        fac_rec[3 * (size_t)ci + f] = (uint32_t)pos;
+        fac_cnt[3 * (size_t)ci + f] = nc;
+        pos += (size_t)nc * 36;
+        if (nc > n_coeff) n_coeff = nc;
+      }
+      b += n_coeff;
+      if (b > 0xFFFFFFFFull / 3) return STARK_ERR_BAD_LENGTH;
+      base[ci + 1] = (uint32_t)b;
+    }
+  }
+  const uint64_t a_len = base[n_c];
+  const uint64_t os = 3 * a_len;
+  if (a_len == 0) return STARK_ERR_BAD_ARG;
+  clk.mark("headers + record walk");
+
+  // Device buffers (context-owned arena).
+  uint32_t key_bits = 1;
+  while (key_bits < 32 && (1ull << key_bits) < n_wires) ++key_bits;
+  size_t sort_tmp = 0;
+  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
+                                                   (int)key_bits, ctx->stream));
+  const size_t wbytes = (size_t)n_wit * wh.field_size;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_cons = take(cons_len), o_w = take(wbytes), o_fac = take(fac.size() * 4),
+               o_base = take(base.size() * 4), o_wcan = take((size_t)n_wit * 32), o_wmont = take((size_t)n_wit * 32),
+               o_coef = take(os * 32), o_wit = take(os * 32), o_comp = take(os * 32), o_flags = take(3 * os),
+               o_perm = take(os * 8), o_k = take(os * 4), o_v = take(os * 4), o_k2 = take(os * 4),
+               o_v2 = take(os * 4), o_last = take((size_t)n_wires * 4), o_pf = take(n_public * 8), o_err = take(4),
+               o_tmp = take(sort_tmp);
+  st = ensure_buf(ctx, ctx->trace_arena, off);
+  if (st != STARK_OK) return st;
+  uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
+  hipStream_t s = ctx->stream;
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_cons, cons, cons_len, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_w, wv, wbytes, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac.data(), fac.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base.data(), base.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
+  STARK_HIP(ctx, hipMemsetAsync(A + o_pf, 0xFF, n_public * 8, s));
+  fe* wcan = (fe*)(A + o_wcan);
+  fe* wmont = (fe*)(A + o_wmont);
+  uint32_t* err = (uint32_t*)(A + o_err);
+  {
+    uint64_t one_r[4];  // Montgomery image of R = R^2 mod p
+    memcpy(one_r, F.one().v, 32);
+    hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
+                       wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), wcan, wmont);
+  }
+  FillArgs fa;
+  fa.cons = A + o_cons;
+  fa.fac_rec = (const uint32_t*)(A + o_fac);
+  fa.fac_cnt = (const uint32_t*)(A + o_fac) + (size_t)3 * n_c;
+  fa.base = (const uint32_t*)(A + o_base);
+  fa.n_constraints = n_c;
+  fa.n_wires = n_wires;
+  fa.a_len = a_len;
+  fa.wcan = wcan;
+  fa.wmont = wmont;
+  fa.coef = (fe*)(A + o_coef);
+  fa.wit = (fe*)(A + o_wit);
+  fa.comp = (fe*)(A + o_comp);
+  fa.keys = (uint32_t*)(A + o_k);
+  fa.vals = (uint32_t*)(A + o_v);
+  fa.err = err;
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa);
+  uint8_t* flags = A + o_flags;
+  STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));  // flag0, flag1 = 1
+  STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
+  hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
+                     flags + os, flags + 2 * os);
+  STARK_HIP(ctx, hipGetLastError());
+  size_t tmp_bytes = sort_tmp;
+  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
+                                                   (uint32_t*)(A + o_k2), (const uint32_t*)(A + o_v),
+                                                   (uint32_t*)(A + o_v2), (int)os, 0, (int)key_bits, s));
+  const uint32_t* keys = (const uint32_t*)(A + o_k2);
+  const uint32_t* vals = (const uint32_t*)(A + o_v2);
+  uint32_t* last = (uint32_t*)(A + o_last);
+  hipLaunchKernelGGL(group_last_kernel, dim3(blocks(os)), dim3(256), 0, s, keys, os, last);
+  hipLaunchKernelGGL(perm_kernel, dim3(blocks(os)), dim3(256), 0, s, keys, vals, os, (const uint32_t*)last,
+                     (uint32_t)n_public, (uint64_t*)(A + o_perm), (uint64_t*)(A + o_pf));
+  STARK_HIP(ctx, hipGetLastError());
+  clk.mark("kernels enqueued");
+  // First uses of the public wires and the error flag: the one host read-back.
+  std::vector<uint64_t> pf(n_public);
+  uint32_t h_err = 0;
+  STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  if (h_err) return STARK_ERR_BAD_ARG;  // a wire id >= n_wires (reader.rs:4-89 bounds)
+  out->public_first_indices.clear();
+  for (size_t wi = 0; wi < n_public && wi < n_wires; ++wi)
+    if (pf[wi] != ~0ull) {
+      out->public_first_indices.push_back(wi);
+      out->public_first_indices.push_back((size_t)pf[wi]);
+    }
+  out->os = os;
+  out->n_constraints = n_c;
+  out->n_wires = n_wires;
+  out->coef = fa.coef;
+  out->wit = fa.wit;
+  out->comp = fa.comp;
+  out->flags = flags;
+  out->perm = (uint64_t*)(A + o_perm);
+  clk.mark("device build + read-back");
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+stark_status stark_prove_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                                    size_t wtns_len, stark_r1cs_proof** out) {
+  if (!ctx || !r1cs || !wtns || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  DevTrace dt;
+  const stark_status st = r1cs_trace_device(ctx, r1cs, r1cs_len, wtns, wtns_len, &dt);
+  if (st != STARK_OK) return st;
+  return mk_r1cs_proof_bytes_flags(ctx, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
+                                   dt.public_wires.data(), dt.public_wires.size() / 4,
+                                   dt.public_first_indices.data(), dt.public_first_indices.size() / 2,
+                                   (const size_t*)dt.perm, (const uint64_t*)dt.coef, dt.flags, dt.n_constraints,
+                                   dt.n_wires, out);
+}
+
+}  // extern "C"

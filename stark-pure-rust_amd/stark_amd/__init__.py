@@ -89,6 +89,8 @@ _SIGNATURES = {
     "stark_r1cs_trace_export": ([_vp, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p, _szp, _u64p, _szp], ctypes.c_int),
     "stark_r1cs_trace_free": ([_vp], None),
     "stark_prove_r1cs_trace": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_prove_r1cs_bytes": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_lde": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p, _u64p], ctypes.c_int),
     "stark_lde_dev": ([_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, _vp],
                       ctypes.c_int),

@@ -118,7 +118,15 @@ class R1csTrace:
 
 
 def prove_with_witness(ctx: Context, r1cs: bytes, wtns: bytes) -> StarkProof:
-    """run.rs:310-452."""
+    """run.rs:310-452, the trace built on the GPU (stark_prove_r1cs_bytes)."""
+    h = _vp()
+    ctx.check(ctx.lib.stark_prove_r1cs_bytes(ctx.h, r1cs, len(r1cs), wtns, len(wtns), ctypes.byref(h)),
+              "prove_with_witness")
+    return StarkProof(ctx.lib, h)
+
+
+def prove_with_witness_host_trace(ctx: Context, r1cs: bytes, wtns: bytes) -> StarkProof:
+    """run.rs:310-452 with the host trace builder (R1csTrace) feeding the same prover."""
     tr = R1csTrace(r1cs, wtns)
     h = _vp()
     ctx.check(ctx.lib.stark_prove_r1cs_trace(ctx.h, tr.h, ctypes.byref(h)), "prove_with_witness")

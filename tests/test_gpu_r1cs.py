@@ -118,3 +118,41 @@ def test_synthetic_2_17_steps_matches_oracle_and_verifies(ctx, oracle):
     assert proof == R.mk_r1cs_proof_json(oracle, tr, cpus=16)
     assert verify_r1cs_proof(oracle, proof, tr.public_wires, tr.public_first_indices, tr.permuted_indices,
                              tr.coefficients, tr.flag0, tr.flag1, tr.flag2, tr.n_constraints, tr.n_wires)
+
+
+@pytest.mark.parametrize("name", list(GOLDEN))
+def test_device_trace_equals_host_trace(ctx, name):
+    """stark_prove_r1cs_bytes (trace built on the GPU) and the host trace builder give the same proof."""
+    from stark_amd.r1cs import prove_with_witness, prove_with_witness_host_trace
+    r1, wt = _read(name, "r1cs"), _read(name, "wtns")
+    assert prove_with_witness(ctx, r1, wt).to_json() == prove_with_witness_host_trace(ctx, r1, wt).to_json()
+
+
+def test_device_trace_synthetic_equals_host_trace(ctx):
+    from stark_amd.r1cs import prove_with_witness, prove_with_witness_host_trace
+    r1, wt = _synth(15)
+    assert prove_with_witness(ctx, r1, wt).to_json() == prove_with_witness_host_trace(ctx, r1, wt).to_json()
+
+
+def test_device_trace_rejects_bad_inputs(ctx):
+    """A wire id beyond n_wires inside a record (found on the device) and a witness whose first value
+    is not 1 (run.rs:358) are rejected like the host builder rejects them."""
+    import struct
+    from stark_amd import StarkError
+    from stark_amd.r1cs import prove_with_witness
+    r1, wt = bytearray(_read("compute", "r1cs")), bytearray(_read("compute", "wtns"))
+    n_wires = struct.unpack_from("<I", r1, 4 * 4 + 8 + 4 + 32)[0]
+    cons = 4 * 4 + 8 + 4 + 32 + 4 * 4 + 8 + 4 + 4 + 8   # header section, then the constraint section header
+    bad = bytearray(r1)
+    first_nc = struct.unpack_from("<I", bad, cons)[0]
+    assert first_nc > 0
+    struct.pack_into("<I", bad, cons + 4, n_wires + 5)   # first record's wire id
+    with pytest.raises(StarkError):
+        prove_with_witness(ctx, bytes(bad), bytes(wt))
+    badw = bytearray(wt)
+    n_wit = struct.unpack_from("<I", badw, 4 + 5 * 4 + 4 + 32)[0]  # wtns v2: header section, 32-B prime
+    wval = len(badw) - 32 * n_wit                        # witness value 0
+    assert wval == 4 + 5 * 4 + 4 + 32 + 4 + 3 * 4
+    badw[wval] ^= 2
+    with pytest.raises(StarkError):
+        prove_with_witness(ctx, bytes(r1), bytes(badw))

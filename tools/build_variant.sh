@@ -14,7 +14,7 @@ s = open(p).read()
 s = eval(expr)
 open(p, 'w').write(s)
 PY
-for f in api ntt merkle field_ops fri; do
+for f in $(cd "$TMP" && ls *.hip | sed "s/\.hip$//"); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -I"$ROOT/include" "$@" -c "$TMP/$f.hip" -o "$TMP/$f.o" &
 done
 wait

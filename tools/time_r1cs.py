@@ -40,7 +40,7 @@ def main():
             p = prove_with_witness(ctx, r, w)
             js = p.to_json()
             times.append(time.perf_counter() - t1)
-        print(f"{name}: original_steps={dims['original_steps']} trace_build={t_trace * 1e3:.1f} ms "
+        print(f"{name}: original_steps={dims['original_steps']} host_trace_build={t_trace * 1e3:.1f} ms "
               f"prove first={times[0] * 1e3:.1f} ms best={min(times[1:]) * 1e3:.1f} ms json={len(js)} B",
               flush=True)
     ctx.close()
