@@ -48,6 +48,7 @@ typedef struct stark_merkle_tree stark_merkle_tree;
 typedef struct stark_fri_proof stark_fri_proof;
 typedef struct stark_r1cs_proof stark_r1cs_proof;
 typedef struct stark_r1cs_trace stark_r1cs_trace;
+typedef struct stark_dprove stark_dprove;
 
 /* ---- context ------------------------------------------------------------ */
 /* Replaces commitment::multicore::Worker::new (packages/commitment/src/multicore.rs:43-45):
@@ -254,6 +255,73 @@ stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t lo
 stark_status stark_ntt_strided_tw_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
                                       const uint64_t root[4], int inverse, const uint64_t tw_root[4],
                                       uint32_t log_order, uint64_t tw_base, void* stream);
+
+/* ---- distributed Merkle / FRI / prover building blocks ---------------------
+ * (no reference counterpart: the reference prover is single-process; these let
+ * `world` GPUs share one proof, see stark-pure-rust_amd/stark_amd/dprove.py.)
+ * Vectors are distributed by residue class: rank r holds the points
+ * r, r + world, r + 2 world, ...; world is a power of two <= 8. */
+/* Leaf digests only: d_digests[i] = Blake2s(leaf i) (the level-0 nodes of
+ * merkle_proof_in_place.rs:125-140), n leaves of leaf_len bytes. */
+stark_status stark_merkle_leaf_digests_dev(stark_ctx* ctx, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                                           uint8_t* d_digests, void* stream);
+/* Builds a tree whose level 0 is given: d_digests holds `interleave` chunks of
+ * n/interleave digests (chunk r = the residue class r of the leaves), so leaf
+ * interleave*m + r is chunk r's m-th digest.  gen_proofs then returns the leaf
+ * digest as the leaf bytes. */
+stark_status stark_merkle_update_digests_dev(stark_merkle_tree* tree, const uint8_t* d_digests, size_t n,
+                                             uint32_t interleave, void* stream);
+/* out[i] = the idx[i]-th row (row_bytes) of d_rows, to host memory (openings of leaves held here). */
+stark_status stark_gather_rows_dev(stark_ctx* ctx, const uint8_t* d_rows, size_t row_bytes, const size_t* idx,
+                                   size_t k, uint8_t* out, void* stream);
+/* One FRI fold (fri.rs:135-164) on a residue class: `values` = the layer's n
+ * values at points rank + world j (n/world of them, root = the layer's root of
+ * unity), `column` = the folded column's rows rank + world j (n/(4 world));
+ * special_x = from_bytes_le(m_root).  Requires world | n/4. */
+stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                                const uint64_t root[4], const uint8_t m_root[32], uint32_t world, uint32_t rank,
+                                void* stream);
+/* serde_json of StarkProof (utils.rs:122-130) from its parts. */
+typedef struct stark_branches {
+  const uint8_t* leaves; /* k * leaf_len bytes */
+  const uint8_t* nodes;  /* k * depth * 32 bytes, leaf -> root per proof */
+  size_t k, leaf_len, depth;
+} stark_branches;
+typedef struct stark_fri_layer_parts {
+  const uint8_t* root2; /* 32 bytes */
+  stark_branches column, poly;
+} stark_fri_layer_parts;
+stark_status stark_r1cs_proof_json_from_parts(const uint8_t m_root[32], const uint8_t l_root[32],
+                                              const uint8_t a_root[32], const stark_branches* main_branches,
+                                              const stark_branches* linear_comb_branches,
+                                              const stark_fri_layer_parts* layers, size_t n_layers,
+                                              const uint8_t* last_values, size_t n_last, char* buf, size_t cap,
+                                              size_t* len);
+/* mk_r1cs_proof (prove.rs:14-264) for rank `rank` of `world`: the trace set-up,
+ * accumulator tree and transcript r on every rank, then this rank's residue
+ * class of the precision domain: coset LDEs (no exchange: degree < steps <=
+ * precision/world), A, Zb, the constraint kernel and the 256-B main-tree rows.
+ * Arguments as stark_mk_r1cs_proof; work is enqueued on `stream` (NULL = the
+ * context stream) and finished on return. */
+stark_status stark_dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
+                                const uint64_t* computational_trace, size_t original_steps,
+                                const uint64_t* public_wires, size_t n_public, const size_t* public_first_indices,
+                                size_t n_public_first, const size_t* permuted_indices, const uint64_t* coefficients,
+                                const uint64_t* flag0, const uint64_t* flag1, const uint64_t* flag2,
+                                size_t n_constraints, size_t n_wires, void* stream, stark_dprove** out);
+/* The same from raw .r1cs / .wtns bytes, trace built on this GPU (as stark_prove_r1cs_bytes). */
+stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
+                                      size_t r1cs_len, const uint8_t* wtns, size_t wtns_len, void* stream,
+                                      stark_dprove** out);
+/* Sizes, g2 = 7^((p-1)/precision) (prove.rs:71-82) and a_root; STARK_ERR_CHECK
+ * where the reference's D/B asserts would panic (on this rank's points). */
+stark_status stark_dprove_info(stark_dprove* h, size_t* precision, size_t* n_local, size_t* original_steps,
+                               uint64_t g2[4], uint8_t a_root[32]);
+/* This rank's main-tree rows P|A|S|D1|D2|D3|B2|B3 (n_local x 256 B, device). */
+stark_status stark_dprove_rows(stark_dprove* h, uint8_t** rows_dev);
+/* k from m_root (prove.rs:274-283) and L at this rank's points (prove.rs:287-322). */
+stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uint64_t** l_dev);
+void stark_dprove_free(stark_dprove* h);
 
 /* ---- device memory helpers (for callers without their own allocator) ------ */
 stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);

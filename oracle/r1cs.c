@@ -115,12 +115,15 @@ static void enc(fp v, uint8_t* out) { fp_to_canon(v, (uint64_t*)out); }
  *   2 = a divisibility assert (utils.rs:379-418 D1-D3, :477-524 B2/B3) failed.
  * Elements are canonical LE u64[4]; public_first_indices holds (k, w) pairs.
  */
-char* oracle_mk_r1cs_proof_json(const uint64_t* witness_trace_c, const uint64_t* computational_trace_c,
-                                size_t original_steps, const uint64_t* public_wires_c, size_t n_public,
-                                const size_t* public_first_indices, size_t n_pfi,
-                                const size_t* permuted_indices_in, const uint64_t* coefficients_c,
-                                const uint64_t* flag0_c, const uint64_t* flag1_c, const uint64_t* flag2_c,
-                                size_t n_constraints, size_t n_wires, uint32_t cpus, int* err) {
+/* rows_out != NULL: stop once the main-tree rows exist and hand them (precision x 256 B)
+ * and a_root to the caller (the distributed-prover tests' per-rank slices). */
+static char* mk_proof(const uint64_t* witness_trace_c, const uint64_t* computational_trace_c,
+                      size_t original_steps, const uint64_t* public_wires_c, size_t n_public,
+                      const size_t* public_first_indices, size_t n_pfi,
+                      const size_t* permuted_indices_in, const uint64_t* coefficients_c,
+                      const uint64_t* flag0_c, const uint64_t* flag1_c, const uint64_t* flag2_c,
+                      size_t n_constraints, size_t n_wires, uint32_t cpus, int* err,
+                      uint8_t** rows_out, uint8_t* a_root_out) {
   or_init();
   *err = 0;
   if (!(original_steps <= 3 * n_constraints * n_wires) || original_steps % 3 != 0 || original_steps < 5) {
@@ -318,6 +321,11 @@ char* oracle_mk_r1cs_proof_json(const uint64_t* witness_trace_c, const uint64_t*
       enc(p_ev[i], row); enc(a_ev[i], row + 32); enc(s_ev[i], row + 64); enc(d1[i], row + 96);
       enc(d2[i], row + 128); enc(d3[i], row + 160); enc(b2[i], row + 192); enc(b3[i], row + 224);
     }
+    if (rows_out) {
+      *rows_out = main_leaves;
+      memcpy(a_root_out, a_root, 32);
+      goto done;
+    }
     uint8_t m_root[32];
     oracle_merkle_proofs(main_leaves, precision, 256, NULL, 0, cpus, m_root, NULL);
     /* k (prove.rs:274-283) */
@@ -397,4 +405,30 @@ done:
   free(a_mini); free(a_ev); free(inv_z); free(d1); free(d2); free(d3);
   free(i2_ev); free(i3_ev); free(zb2); free(zb3); free(inv_zb2); free(inv_zb3); free(b2); free(b3);
   return out;
+}
+
+char* oracle_mk_r1cs_proof_json(const uint64_t* witness_trace_c, const uint64_t* computational_trace_c,
+                                size_t original_steps, const uint64_t* public_wires_c, size_t n_public,
+                                const size_t* public_first_indices, size_t n_pfi,
+                                const size_t* permuted_indices_in, const uint64_t* coefficients_c,
+                                const uint64_t* flag0_c, const uint64_t* flag1_c, const uint64_t* flag2_c,
+                                size_t n_constraints, size_t n_wires, uint32_t cpus, int* err) {
+  return mk_proof(witness_trace_c, computational_trace_c, original_steps, public_wires_c, n_public,
+                  public_first_indices, n_pfi, permuted_indices_in, coefficients_c, flag0_c, flag1_c, flag2_c,
+                  n_constraints, n_wires, cpus, err, NULL, NULL);
+}
+
+/* The main-tree rows P|A|S|D1|D2|D3|B2|B3 of every precision point (prove.rs:235-258)
+ * and a_root; free the rows with oracle_free. */
+uint8_t* oracle_r1cs_rows(const uint64_t* witness_trace_c, const uint64_t* computational_trace_c,
+                          size_t original_steps, const uint64_t* public_wires_c, size_t n_public,
+                          const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices_in,
+                          const uint64_t* coefficients_c, const uint64_t* flag0_c, const uint64_t* flag1_c,
+                          const uint64_t* flag2_c, size_t n_constraints, size_t n_wires, uint32_t cpus, int* err,
+                          uint8_t a_root[32]) {
+  uint8_t* rows = NULL;
+  mk_proof(witness_trace_c, computational_trace_c, original_steps, public_wires_c, n_public, public_first_indices,
+           n_pfi, permuted_indices_in, coefficients_c, flag0_c, flag1_c, flag2_c, n_constraints, n_wires, cpus, err,
+           &rows, a_root);
+  return rows;
 }

@@ -273,3 +273,30 @@ def mk_r1cs_proof_json(orc: Oracle, tr: Trace, cpus: int = 8) -> str:
     s = ctypes.string_at(res).decode()
     lib.oracle_free(ctypes.c_void_p(res))
     return s
+
+
+def r1cs_rows(orc: Oracle, tr: Trace, cpus: int = 8):
+    """oracle_r1cs_rows (oracle/r1cs.c): the main-tree rows of every precision point
+    (prove.rs:235-258) and a_root, for checking the distributed prover's per-rank slices."""
+    lib = orc.lib
+    fn = lib.oracle_r1cs_rows
+    fn.restype = ctypes.c_void_p
+    n = len(tr.coefficients)
+    arrs = [to_limbs(v) for v in (tr.witness_trace, tr.computational_trace, tr.public_wires, tr.coefficients,
+                                  tr.flag0, tr.flag1, tr.flag2)]
+    pfi = np.array([x for pair in tr.public_first_indices for x in pair] or [0], dtype=np.uint64)
+    perm = np.array(tr.permuted_indices or [0], dtype=np.uint64)
+    err = ctypes.c_int(0)
+    a_root = ctypes.create_string_buffer(32)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    res = fn(ptr(arrs[0]), ptr(arrs[1]), ctypes.c_size_t(n), ptr(arrs[2]), ctypes.c_size_t(len(tr.public_wires)),
+             ptr(pfi), ctypes.c_size_t(len(tr.public_first_indices)), ptr(perm), ptr(arrs[3]), ptr(arrs[4]),
+             ptr(arrs[5]), ptr(arrs[6]), ctypes.c_size_t(tr.n_constraints), ctypes.c_size_t(tr.n_wires),
+             ctypes.c_uint32(cpus), ctypes.byref(err), a_root)
+    if not res:
+        raise AssertionError(f"oracle r1cs_rows failed (err {err.value})")
+    log_steps = max((n - 1).bit_length(), 3)
+    prec = 8 << log_steps
+    rows = ctypes.string_at(res, 256 * prec)
+    lib.oracle_free(ctypes.c_void_p(res))
+    return rows, a_root.raw

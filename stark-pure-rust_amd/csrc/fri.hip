@@ -56,14 +56,18 @@ __global__ void fri_special_x_kernel(const uint32_t* __restrict__ root, fe* __re
   *s_m = fe_mul(x, r2);
 }
 
+// Row i of q (local rows; global row g_add + (i << log_g) on a distributed
+// prover whose values are the residue class g_add mod 2^log_g, where the four
+// points of a row are local too since n/4 is a multiple of 2^log_g).
 __global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
+                                uint64_t g_add, uint32_t log_g,
                                 const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
                                 const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= q) return;
   const fe s_m = *s_ptr;
   const fe y0 = fe_load(v + i), y1 = fe_load(v + i + q), y2 = fe_load(v + i + 2 * q), y3 = fe_load(v + i + 3 * q);
-  const uint64_t e = i << shift;
+  const uint64_t e = (g_add + (i << log_g)) << shift;
   const fe winv = fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]);  // Montgomery w^-i
   const fe u_m = fe_mul(s_m, winv);                                         // Montgomery special_x * w^-i
   const fe s02 = fe_add(y0, y2), s13 = fe_add(y1, y3);
@@ -179,6 +183,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
     const HostFp zeta = F.pow_u64(w, q);  // w^(n/4)
     const unsigned blocks = (unsigned)((q + 255) / 256);
     hipLaunchKernelGGL(fri_fold_kernel, dim3(blocks), dim3(256), 0, s, cur, next, (uint64_t)q, (uint32_t)(2 * layer),
+                       (uint64_t)0, (uint32_t)0,
                        tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4));
     STARK_HIP(ctx, hipGetLastError());
     st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s);
@@ -409,6 +414,102 @@ stark_status stark_prove_low_degree(stark_ctx* ctx, const uint64_t* values, size
 }
 
 void stark_fri_proof_free(stark_fri_proof* proof) { delete proof; }
+
+// One FRI fold on this GPU's residue class (distributed prover, fri.rs:135-164):
+// `values` holds the layer's values at the points rank + world*j (n/world of
+// them), `column` receives the folded column at the same residue class of the
+// n/4 rows; special_x = from_bytes_le(m_root) (fri.rs:135).
+stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                                const uint64_t root[4], const uint8_t m_root[32], uint32_t world, uint32_t rank,
+                                void* stream) {
+  if (!ctx || !values || !column || !root || !m_root) return STARK_ERR_BAD_ARG;
+  if (world == 0 || (world & (world - 1)) || rank >= world) return STARK_ERR_BAD_ARG;
+  if (n < 4 || (n & (n - 1)) || (n / 4) % world != 0) return STARK_ERR_BAD_LENGTH;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  hipStream_t s = pick_stream(ctx, stream);
+  uint32_t log_n = 0, log_g = 0;
+  while (((size_t)1 << log_n) < n) ++log_n;
+  while ((1u << log_g) < world) ++log_g;
+  uint64_t inv_root[4];
+  F.to_canonical(F.inv(F.from_canonical(root)), inv_root);
+  const Twiddles* tw = nullptr;
+  stark_status st = get_twiddles(ctx, inv_root, log_n, &tw);
+  if (st != STARK_OK) return st;
+  st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
+  if (st != STARK_OK) return st;
+  fe* d_sx = (fe*)ctx->fri_misc.ptr + 15;  // slot 15: unused by prove_low_degree's <= 15 layers
+  const fe sx = to_dev(F.from_bytes_le(m_root, 32));
+  STARK_HIP(ctx, hipMemcpyAsync(d_sx, &sx, sizeof(fe), hipMemcpyHostToDevice, s));
+  const HostFp zeta = F.pow_u64(F.from_canonical(root), n / 4);
+  const size_t q = n / 4 / world;
+  hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, (const fe*)values,
+                     (fe*)column, (uint64_t)q, (uint32_t)0, (uint64_t)rank, log_g, tw->d_lo, tw->d_hi, tw->kb,
+                     (const fe*)d_sx, to_dev(zeta), to_dev(F.inv(F.from_u64(4))));
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipStreamSynchronize(s));  // sx lives on this stack frame
+  return STARK_OK;
+}
+
+// serde_json of a StarkProof (r1cs-stark/src/utils.rs:122-130) from its parts
+// (the distributed prover's rank 0 assembles the openings of every rank).
+stark_status stark_r1cs_proof_json_from_parts(const uint8_t m_root[32], const uint8_t l_root[32],
+                                              const uint8_t a_root[32], const stark_branches* main_branches,
+                                              const stark_branches* linear_comb_branches,
+                                              const stark_fri_layer_parts* layers, size_t n_layers,
+                                              const uint8_t* last_values, size_t n_last, char* buf, size_t cap,
+                                              size_t* len) {
+  if (!m_root || !l_root || !a_root || !main_branches || !linear_comb_branches || !len) return STARK_ERR_BAD_ARG;
+  if ((n_layers && !layers) || (n_last && !last_values)) return STARK_ERR_BAD_ARG;
+  auto vec = [](const uint8_t* p, size_t n) { return std::vector<uint8_t>(p, p + n); };
+  const stark_branches& mb = *main_branches;
+  const stark_branches& lb = *linear_comb_branches;
+  const std::vector<uint8_t> ml = vec(mb.leaves, mb.k * mb.leaf_len), mn = vec(mb.nodes, mb.k * mb.depth * 32);
+  const std::vector<uint8_t> ll = vec(lb.leaves, lb.k * lb.leaf_len), ln = vec(lb.nodes, lb.k * lb.depth * 32);
+  stark_fri_proof fri;
+  for (size_t l = 0; l < n_layers; ++l) {
+    const stark_fri_layer_parts& P = layers[l];
+    stark_fri_layer L;
+    memcpy(L.root2, P.root2, 32);
+    L.col_idx.resize(P.column.k);
+    L.poly_idx.resize(P.poly.k);
+    L.col_depth = P.column.depth;
+    L.poly_depth = P.poly.depth;
+    L.col_leaves = vec(P.column.leaves, P.column.k * 32);
+    L.col_nodes = vec(P.column.nodes, P.column.k * P.column.depth * 32);
+    L.poly_leaves = vec(P.poly.leaves, P.poly.k * 32);
+    L.poly_nodes = vec(P.poly.nodes, P.poly.k * P.poly.depth * 32);
+    fri.layers.push_back(std::move(L));
+  }
+  stark_fri_layer last;
+  last.last = true;
+  last.last_values = vec(last_values, 32 * n_last);
+  fri.layers.push_back(std::move(last));
+  JsonPieces j;
+  j.text("{\"m_root\":");
+  j.bytes(m_root, 32);
+  j.text(",\"l_root\":");
+  j.bytes(l_root, 32);
+  j.text(",\"a_root\":");
+  j.bytes(a_root, 32);
+  j.text(",\"main_branches\":");
+  j.branches(ml, mb.leaf_len, mn, mb.k, mb.depth);
+  j.text(",\"linear_comb_branches\":");
+  j.branches(ll, lb.leaf_len, ln, lb.k, lb.depth);
+  j.text(",\"fri_proof\":");
+  fri_proof_json_pieces(&fri, j);
+  j.text("}");
+  std::string o;
+  j.render(o);
+  *len = o.size();
+  if (buf && cap) {
+    const size_t k = o.size() < cap ? o.size() : cap;
+    memcpy(buf, o.data(), k);
+    if (k < cap) buf[k] = 0;
+  }
+  return STARK_OK;
+}
+
 
 stark_status stark_fri_proof_json(const stark_fri_proof* proof, char* buf, size_t cap, size_t* len) {
   if (!proof || !len) return STARK_ERR_BAD_ARG;

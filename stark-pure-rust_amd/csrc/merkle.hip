@@ -310,7 +310,28 @@ static uint64_t level_offset(uint64_t n, uint32_t level) {
   return off;
 }
 
-// Builds every level of the tree over d_leaves (n leaves of leaf_len bytes).
+// Leaf digests only: out[i] = Blake2s(leaf i) (the level-0 nodes of a tree
+// whose parents another GPU may build, distributed prover).
+__global__ void merkle_leaf_digest_kernel(const uint8_t* __restrict__ leaves, uint32_t leaf_len, uint64_t n,
+                                          Digest* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool l32 = leaf_len == 32 && (((uintptr_t)leaves) & 15) == 0;
+  store_digest(out + i, l32 ? hash_leaf32(leaves + i * 32) : hash_leaf(leaves + i * leaf_len, leaf_len));
+}
+
+// level0[G m + r] = chunks[r][m]: the digests of G ranks' residue classes,
+// received as G contiguous chunks of n/G (one per sender), in leaf order.
+__global__ void merkle_interleave_kernel(const Digest* __restrict__ chunks, uint64_t n, uint32_t log_g,
+                                         Digest* __restrict__ level0) {
+  const uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const uint64_t r = o & ((1u << log_g) - 1), m = o >> log_g;
+  store_digest(level0 + o, load_digest(chunks + r * (n >> log_g) + m));
+}
+
+// Builds every level of the tree over d_leaves (n leaves of leaf_len bytes);
+// with d_leaves == nullptr level 0 (the leaf digests) is already in place.
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
                           hipStream_t stream) {
   if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
@@ -320,10 +341,11 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
   if (st != STARK_OK) return st;
   Digest* nodes = (Digest*)t->nodes.ptr;
-  uint32_t level = 0;
-  uint64_t count = n;
-  bool leaf_mode = true;
-  while (true) {
+  const bool have_level0 = d_leaves == nullptr;
+  uint32_t level = have_level0 ? 1 : 0;
+  uint64_t count = have_level0 ? n / 2 : n;
+  bool leaf_mode = !have_level0;
+  while (depth > 0 || !have_level0) {
     if (!leaf_mode && count < kTailFrom) {
       // Narrow pair levels: quad kernel, up to 8 levels per launch.
       const uint64_t blk = count < kTailBlock ? count : kTailBlock;
@@ -368,7 +390,7 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   t->n = n;
   t->leaf_len = leaf_len;
   t->depth = depth;
-  t->d_leaves = d_leaves;
+  t->d_leaves = have_level0 ? (const uint8_t*)nodes : d_leaves;
   t->built = true;
   return STARK_OK;
 }
@@ -575,6 +597,55 @@ stark_status stark_merkle_update_dev(stark_merkle_tree* t, const uint8_t* d_leav
   stark_ctx* ctx = t->ctx;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   return merkle_build(ctx, t, d_leaves, n, leaf_len, pick_stream(ctx, stream));
+}
+
+stark_status stark_merkle_leaf_digests_dev(stark_ctx* ctx, const uint8_t* d_leaves, size_t n, size_t leaf_len,
+                                           uint8_t* d_digests, void* stream) {
+  if (!ctx || (n && (!d_leaves || !d_digests)) || leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  if (n == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(merkle_leaf_digest_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     pick_stream(ctx, stream), d_leaves, (uint32_t)leaf_len, (uint64_t)n, (Digest*)d_digests);
+  STARK_HIP(ctx, hipGetLastError());
+  return STARK_OK;
+}
+
+stark_status stark_merkle_update_digests_dev(stark_merkle_tree* t, const uint8_t* d_digests, size_t n,
+                                            uint32_t interleave, void* stream) {
+  if (!t || !d_digests || interleave == 0 || (interleave & (interleave - 1))) return STARK_ERR_BAD_ARG;
+  if (n == 0 || (n & (n - 1)) || n % interleave) return STARK_ERR_BAD_LENGTH;
+  stark_ctx* ctx = t->ctx;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = pick_stream(ctx, stream);
+  stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
+  if (st != STARK_OK) return st;
+  uint32_t log_g = 0;
+  while ((1u << log_g) < interleave) ++log_g;
+  hipLaunchKernelGGL(merkle_interleave_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     (const Digest*)d_digests, (uint64_t)n, log_g, (Digest*)t->nodes.ptr);
+  STARK_HIP(ctx, hipGetLastError());
+  return merkle_build(ctx, t, nullptr, n, 32, s);
+}
+
+// out[i] = rows[idx[i]] (row_bytes each): openings of leaves held on this GPU.
+stark_status stark_gather_rows_dev(stark_ctx* ctx, const uint8_t* d_rows, size_t row_bytes, const size_t* idx,
+                                   size_t k, uint8_t* out, void* stream) {
+  if (!ctx || (k && (!d_rows || !idx || !out)) || row_bytes > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  if (k == 0) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = pick_stream(ctx, stream);
+  const size_t idx_bytes = (k * sizeof(uint64_t) + 15) & ~(size_t)15;
+  stark_status st = ensure_buf(ctx, ctx->io2, idx_bytes + k * row_bytes);
+  if (st != STARK_OK) return st;
+  uint8_t* base = (uint8_t*)ctx->io2.ptr;
+  STARK_HIP(ctx, hipMemcpyAsync(base, idx, k * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)k), dim3(64), 0, s, d_rows, (uint32_t)row_bytes,
+                     (const Digest*)nullptr, (uint64_t)0, (uint32_t)0, (const uint64_t*)base, (uint32_t)k,
+                     base + idx_bytes, (Digest*)nullptr);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipMemcpyAsync(out, base + idx_bytes, k * row_bytes, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  return STARK_OK;
 }
 
 size_t stark_merkle_width(const stark_merkle_tree* t) { return t ? t->n : 0; }

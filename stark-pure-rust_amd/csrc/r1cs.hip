@@ -191,15 +191,21 @@ __global__ void r1cs_flags_kernel(const uint8_t* __restrict__ fb, uint64_t os, u
 
 // val_nmr / val_dnm of calc_a_mini_evaluations (utils.rs:317-318), written as
 // Montgomery images for the product scans.
+// ext_idx[8 j] = IDX[j] = j and ext_pidx[8 j] = PIDX[j] (the LDE interpolates the step
+// values); with ext_idx == nullptr (distributed prover: the extended columns are
+// sharded) they are taken from the step-domain permutation instead.
 __global__ void r1cs_a_vals_kernel(const fe* __restrict__ ext_idx, const fe* __restrict__ ext_pidx,
+                                   const uint64_t* __restrict__ perm, uint64_t os,
                                    const fe* __restrict__ w, uint64_t steps, const Transcript* __restrict__ tr, fe mr2,
                                    fe* __restrict__ nmr_m, fe* __restrict__ dnm_m) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= steps) return;
   const fe r0 = tr->r0, r1_m = tr->r1_m, r2_m = tr->r2_m;
   const fe rw = fe_mul(fe_load(w + j), r2_m);
-  const fe vn = fe_add(fe_add(r0, fe_mul(fe_load(ext_idx + j * kExtensionFactor), r1_m)), rw);
-  const fe vd = fe_add(fe_add(r0, fe_mul(fe_load(ext_pidx + j * kExtensionFactor), r1_m)), rw);
+  const fe xi = ext_idx ? fe_load(ext_idx + j * kExtensionFactor) : fe_from_u64(j);
+  const fe xp = ext_idx ? fe_load(ext_pidx + j * kExtensionFactor) : fe_from_u64(j < os ? perm[j] : j);
+  const fe vn = fe_add(fe_add(r0, fe_mul(xi, r1_m)), rw);
+  const fe vd = fe_add(fe_add(r0, fe_mul(xp, r1_m)), rw);
   fe_store(nmr_m + j, fe_mul(vn, mr2));
   fe_store(dnm_m + j, fe_mul(vd, mr2));
 }
@@ -290,12 +296,15 @@ __global__ void r1cs_a_mini_kernel(const fe* __restrict__ nmr_m, const fe* __res
 
 // Zb2(x) = prod_k (x - x_k) (utils.rs:438-455) and Zb3(x) = x - x_last
 // (utils.rs:466-474), canonical, for the batch inverse.
+// Local point i is the global evaluation point g_add + (i << log_g) (a residue
+// class of the precision domain on a distributed prover; g_add = log_g = 0 on one GPU).
 __global__ void r1cs_zb_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint64_t prec,
+                               uint64_t g_add, uint32_t log_g,
                                const fe* __restrict__ xpub_m, uint32_t npub, fe xlast_m, fe unit, fe one_m,
                                fe* __restrict__ zb2, fe* __restrict__ zb3) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= prec) return;
-  const fe x_m = pow_tab(lo, hi, kb, i);
+  const fe x_m = pow_tab(lo, hi, kb, g_add + (i << log_g));
   fe acc = one_m;
   for (uint32_t k = 0; k < npub; ++k) acc = fe_mul(acc, fe_sub(x_m, xpub_m[k]));
   fe_store(zb2 + i, fe_mul(acc, unit));
@@ -311,8 +320,11 @@ struct ConstraintArgs {
   const fe* hi;
   fe* rows;              // precision x 8 elements
   int* err;
-  uint64_t prec;
-  uint64_t shift1, shift2;  // original_steps/3*skips, original_steps/3*2*skips (mod precision)
+  uint64_t prec;            // points on this GPU (a power of two)
+  uint64_t shift1, shift2;  // original_steps/3*skips, original_steps/3*2*skips (mod precision), in local points
+  uint64_t back;            // the -skips shift in local points
+  uint64_t g_add;           // local point i is global point g_add + (i << log_g)
+  uint32_t log_g;
   uint32_t log_prec, kb, n2, n3;
   const Transcript* tr;  // r0, r1, r2 (device transcript)
   fe mr2;
@@ -335,7 +347,8 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe* IDX = Pc + n;
   const fe* PIDX = IDX + n;
   const fe* A = PIDX + n;
-  const uint64_t prev = (i + n - kExtensionFactor) & mask;
+  const uint64_t prev = (i + n - a.back) & mask;
+  const uint64_t gi = a.g_add + (i << a.log_g);  // global evaluation point
   const fe r0 = a.tr->r0, r1_m = a.tr->r1_m, r2_m = a.tr->r2_m;
   const fe p = fe_load(Pc + i), s = fe_load(S + i), av = fe_load(A + i);
   const fe p_prev = fe_load(Pc + prev), a_prev = fe_load(A + prev);
@@ -349,7 +362,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe nmr = fe_add(fe_add(r0, fe_mul(fe_load(IDX + i), r1_m)), rs);
   const fe dnm = fe_add(fe_add(r0, fe_mul(fe_load(PIDX + i), r1_m)), rs);
   const fe q3 = fe_sub(fe_mul(fe_mul(av, a.mr2), dnm), fe_mul(fe_mul(a_prev, a.mr2), nmr));
-  const uint32_t t = (uint32_t)(i & 7);
+  const uint32_t t = (uint32_t)(gi & 7);
   fe iz = a.invz_m[0];
 #pragma unroll
   for (uint32_t k = 1; k < 8; ++k)
@@ -357,7 +370,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   if (t == 0 && !(fe_is_zero(q1) && fe_is_zero(q2) && fe_is_zero(q3))) atomicOr(a.err, 1);
   const fe d1 = fe_mul(q1, iz), d2 = fe_mul(q2, iz), d3 = fe_mul(q3, iz);
   // I2 / I3 at x = g2^i (Horner; the interpolants are canonical).
-  const fe x_m = pow_tab(a.lo, a.hi, a.kb, i);
+  const fe x_m = pow_tab(a.lo, a.hi, a.kb, gi);
   fe i2 = fe_zero();
   for (uint32_t k = a.n2; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
   fe i3 = fe_zero();
@@ -382,6 +395,8 @@ struct LincombArgs {
   const fe* rows;
   fe* out;
   uint64_t prec;
+  uint64_t g_add;        // local point i is global point g_add + (i << log_g)
+  uint32_t log_g;
   const Transcript* tr;  // k (device transcript)
   fe xs_m[8];  // (g2^steps)^t, t = i mod 8 (prove.rs:287-291)
 };
@@ -392,9 +407,10 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.prec) return;
   const fe* row = a.rows + 8 * i;
+  const uint64_t gi = a.g_add + (i << a.log_g);
   const fe p = fe_load(row + 0), av = fe_load(row + 1), s = fe_load(row + 2), d1 = fe_load(row + 3),
            d2 = fe_load(row + 4), d3 = fe_load(row + 5), b2 = fe_load(row + 6), b3 = fe_load(row + 7);
-  const uint32_t t = (uint32_t)(i & 7);
+  const uint32_t t = (uint32_t)(gi & 7);
   fe xs = a.xs_m[0];
 #pragma unroll
   for (uint32_t k = 1; k < 8; ++k)
@@ -641,7 +657,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   fe* ext_idx = cols + 6 * prec;
   fe* ext_pidx = cols + 7 * prec;
   hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
-                     (const fe*)ext_pidx, (const fe*)wcopy, steps, (const Transcript*)d_tr, mc.r2, nmr, dnm);
+                     (const fe*)ext_pidx, (const uint64_t*)nullptr, (uint64_t)0, (const fe*)wcopy, steps,
+                     (const Transcript*)d_tr, mc.r2, nmr, dnm);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
   STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
@@ -652,7 +669,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(lde(ctx, raw, 1, cols + 8 * prec, log_steps, log_prec, *tw1i, *tw2, s));
 
   hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
-                     (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one, zb, zb + prec);
+                     (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one, zb, zb + prec);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * prec, s));
 
@@ -669,6 +686,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.prec = prec;
   ca.shift1 = (os / 3 * skips) % prec;
   ca.shift2 = (os / 3 * 2 * skips) % prec;
+  ca.back = skips;
+  ca.g_add = 0;
+  ca.log_g = 0;
   ca.log_prec = log_prec;
   ca.kb = tw2->kb;
   ca.n2 = (uint32_t)n_pfi;
@@ -696,6 +716,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   la.rows = rows;
   la.out = lvals;
   la.prec = prec;
+  la.g_add = 0;
+  la.log_g = 0;
   la.tr = d_tr;
   {
     const HostFp w8 = F.pow_u64(g2, steps);
@@ -789,6 +811,253 @@ stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_t
   return st;
 }
 
+// ---- distributed prover (one rank of `world` GPUs) -------------------------
+//
+// The precision domain is split by residue class: rank r owns the evaluation
+// points i = r + G j (j < P = precision / G), G | 8.  Then
+//  * the LDE of every column is a coset evaluation with no exchange: the
+//    polynomial has degree < steps <= P, so f(g2^(r + G j)) =
+//    sum_k (c_k g2^(r k)) (g2^G)^(j k) is a P-point NTT of the scaled
+//    coefficients;
+//  * every shifted read of the constraints (-skips, +k skips, +2k skips) is a
+//    multiple of 8, hence of G, and stays inside the residue class;
+//  * the FRI fold's four points i + t n/4 are in the same class while
+//    n/4 >= G, so each layer's column is again residue-class distributed.
+// Only the Merkle trees need other ranks' data; the caller exchanges leaf
+// digests (stark_amd/dprove.py).  The small step-domain work (accumulator
+// tree, transcript r, A's running products) is repeated on every rank.
+struct DProveState {
+  stark_ctx* ctx = nullptr;
+  hipStream_t s = nullptr;
+  uint32_t G = 1, r = 0, log_g = 0;
+  uint64_t steps = 0, prec = 0, P = 0, skips = 0, os = 0;
+  uint32_t log_steps = 0, log_prec = 0;
+  uint64_t g2c[4];
+  DevBuf arena;
+  stark_merkle_tree* acc_tree = nullptr;
+  fe *rows = nullptr, *lvals = nullptr;
+  Transcript* d_tr = nullptr;
+  fe xs_m[8];
+};
+
+}  // namespace stark
+
+struct stark_dprove {
+  stark::DProveState st;
+  ~stark_dprove() {
+    if (st.acc_tree) stark_merkle_free(st.acc_tree);
+    if (st.arena.ptr) hipFree(st.arena.ptr);
+  }
+};
+
+namespace stark {
+
+// coef[c][k] *= g2^(r k) for the batch of step columns (coset shift of the LDE).
+__global__ void coset_scale_kernel(fe* __restrict__ coef, uint32_t log_steps, uint64_t total, const fe* __restrict__ lo,
+                                   const fe* __restrict__ hi, uint32_t kb, uint64_t r, uint64_t prec_mask) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const uint64_t k = g & (((uint64_t)1 << log_steps) - 1);
+  fe_store(coef + g, fe_mul(fe_load(coef + g), pow_tab(lo, hi, kb, (r * k) & prec_mask)));
+}
+
+// Coset LDE of `batch` step columns (coef, destroyed) into out (batch x P).
+static stark_status lde_coset(DProveState& d, fe* coef, uint32_t batch, fe* out, const Twiddles& tw_g1_inv,
+                              const Twiddles& tw_g2, const Twiddles& tw_h) {
+  STARK_TRY(ntt_device(d.ctx, coef, d.log_steps, batch, tw_g1_inv, true, d.s));
+  if (d.r) {
+    const uint64_t total = (uint64_t)batch << d.log_steps;
+    hipLaunchKernelGGL(coset_scale_kernel, dim3(blocks_for(total)), dim3(256), 0, d.s, coef, d.log_steps, total,
+                       tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, (uint64_t)d.r, d.prec - 1);
+    STARK_HIP(d.ctx, hipGetLastError());
+  }
+  const uint32_t log_p = d.log_prec - d.log_g;
+  return ntt_device_from(d.ctx, coef, log_p - d.log_steps, out, log_p, batch, tw_h, false, d.s);
+}
+
+static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
+                                 const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                 size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                 const size_t* permuted_indices, const uint64_t* coefficients, const uint64_t* flag0,
+                                 const uint64_t* flag1, const uint64_t* flag2, const uint8_t* flag_bytes,
+                                 size_t n_constraints, size_t n_wires, hipStream_t s, stark_dprove* h) {
+  const FieldHost& F = FieldHost::get();
+  DProveState& d = h->st;
+  if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
+    return STARK_ERR_BAD_ARG;
+  // prove.rs:30-53 (as prove_r1cs)
+  if (os > 3 * n_constraints * n_wires || os % 3 != 0) return STARK_ERR_BAD_ARG;
+  if (os < 5) return STARK_ERR_BAD_LENGTH;
+  const uint32_t log_steps = log2_ceil_ref(os - 1);
+  const uint32_t log_prec = log_steps + kLogExtensionFactor;
+  if (log_prec >= 24) return STARK_ERR_BAD_LENGTH;
+  d.ctx = ctx;
+  d.s = s;
+  d.G = world;
+  d.r = rank;
+  while ((1u << d.log_g) < world) ++d.log_g;
+  d.log_steps = log_steps;
+  d.log_prec = log_prec;
+  d.steps = (uint64_t)1 << log_steps;
+  d.prec = (uint64_t)1 << log_prec;
+  d.P = d.prec >> d.log_g;
+  d.skips = d.prec / d.steps;
+  d.os = os;
+  const uint64_t steps = d.steps, prec = d.prec, P = d.P, skips = d.skips;
+  for (size_t i = 0; i < n_pfi; ++i)
+    if (public_first_indices[2 * i] >= n_public || public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
+
+  // Roots (prove.rs:71-94); h = g2^G generates this rank's coset of size P.
+  uint64_t pm1[4];
+  memcpy(pm1, FieldHost::kP, 32);
+  pm1[0] -= 1;
+  for (uint32_t k = 0; k < log_prec; ++k)
+    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
+  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
+  const HostFp g1 = F.pow_u64(g2, skips);
+  uint64_t g1ic[4], hc[4];
+  F.to_canonical(g2, d.g2c);
+  F.to_canonical(F.inv(g1), g1ic);
+  F.to_canonical(F.pow_u64(g2, world), hc);
+  const Twiddles *tw2 = nullptr, *tw1i = nullptr, *twh = nullptr;
+  STARK_TRY(get_twiddles(ctx, d.g2c, log_prec, &tw2));
+  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
+  STARK_TRY(get_twiddles(ctx, hc, log_prec - d.log_g, &twh));
+  const Mont mc = mont();
+
+  fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts;
+  uint64_t* perm;
+  uint64_t* acc_leaves;
+  const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
+  Carve cv;
+  cv.add(&raw, 8 * steps);
+  cv.add(&wcopy, steps);
+  cv.add(&perm, steps);
+  cv.add(&acc_leaves, 5 * steps);
+  cv.add(&cols, 9 * P);
+  cv.add(&nmr, steps);
+  cv.add(&dnm, steps);
+  cv.add(&tot, 2 * (size_t)nb);
+  cv.add(&dnm_c, steps);
+  cv.add(&inv_dnm, steps);
+  cv.add(&zb, 2 * P > 3 * os / 32 + 1 ? 2 * P : 3 * os / 32 + 1);
+  cv.add(&inv_zb, 2 * P);
+  cv.add(&consts, 2 * n_pfi + 2);
+  cv.add(&d.rows, 8 * P);
+  cv.add(&d.lvals, P);
+  cv.add(&d.d_tr, 1);
+  STARK_TRY(cv.commit(ctx, d.arena));
+
+  // Interpolants and boundary points (utils.rs:421-474).
+  const HostFp x_last = F.pow_u64(g2, prec - skips);
+  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
+  for (size_t i = 0; i < n_pfi; ++i) {
+    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
+    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
+  }
+  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
+  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
+  std::vector<fe> hc2(2 * n_pfi + 2);
+  auto canon_fe = [&](const HostFp& x) {
+    uint64_t c[4];
+    F.to_canonical(x, c);
+    fe v;
+    for (int k = 0; k < 4; ++k) {
+      v.w[2 * k] = (uint32_t)c[k];
+      v.w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+    }
+    return v;
+  };
+  for (size_t i = 0; i < n_pfi; ++i) {
+    hc2[i] = to_dev(xv[i]);
+    hc2[n_pfi + i] = canon_fe(interp2[i]);
+  }
+  hc2[2 * n_pfi] = canon_fe(interp3[0]);
+  STARK_HIP(ctx, hipMemcpyAsync(consts, hc2.data(), hc2.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+  // Step columns (prove.rs:59-69), host or device sources.
+  const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
+  for (int c = 0; c < 6; ++c) {
+    if (!(flag_bytes && c >= 1 && c <= 3))
+      STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyDefault, s));
+    if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
+  }
+  if (flag_bytes) {
+    uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel (sized for the 3 os flag bytes)
+    STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyDefault, s));
+    hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
+                       (uint64_t)os, steps, raw + steps);
+    STARK_HIP(ctx, hipGetLastError());
+  }
+  STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
+  STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
+  STARK_HIP(ctx, hipMemsetAsync(d.d_tr, 0, sizeof(Transcript), s));
+  hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
+  STARK_HIP(ctx, hipGetLastError());
+  // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
+  STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
+  STARK_TRY(merkle_build(ctx, d.acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
+  STARK_TRY(lde_coset(d, raw, 8, cols, *tw1i, *tw2, *twh));
+  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
+                     (uint32_t)(prec - 1), mc.r2, d.d_tr);
+  STARK_HIP(ctx, hipGetLastError());
+  // A (utils.rs:293-339): step-domain scans on every rank, then this rank's coset.
+  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nullptr,
+                     (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
+                     (const Transcript*)d.d_tr, mc.r2, nmr, dnm);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
+  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
+  STARK_TRY(multi_inv_device(ctx, dnm_c, inv_dnm, steps, s));
+  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
+                     (const fe*)inv_dnm, steps, raw);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(lde_coset(d, raw, 1, cols + 8 * P, *tw1i, *tw2, *twh));
+  // Zb2 / Zb3 at this rank's points and their inverses.
+  hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
+                     (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
+                     zb, zb + P);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
+  ConstraintArgs ca;
+  ca.cols = cols;
+  ca.inv_zb = inv_zb;
+  ca.interp2 = consts + n_pfi;
+  ca.interp3 = consts + 2 * n_pfi;
+  ca.lo = tw2->d_lo;
+  ca.hi = tw2->d_hi;
+  ca.rows = d.rows;
+  ca.err = &d.d_tr->err;
+  ca.prec = P;
+  ca.shift1 = ((os / 3 * skips) % prec) >> d.log_g;  // multiples of 8, hence of G
+  ca.shift2 = ((os / 3 * 2 * skips) % prec) >> d.log_g;
+  ca.back = skips >> d.log_g;
+  ca.g_add = rank;
+  ca.log_g = d.log_g;
+  ca.log_prec = log_prec;
+  ca.kb = tw2->kb;
+  ca.n2 = (uint32_t)n_pfi;
+  ca.n3 = 1;
+  ca.tr = d.d_tr;
+  ca.mr2 = mc.r2;
+  {
+    const HostFp w8 = F.pow_u64(g2, steps);
+    HostFp wt = F.one();
+    for (int t = 0; t < 8; ++t) {
+      const HostFp z = F.sub(wt, F.one());
+      ca.invz_m[t] = FieldHost::eq(z, F.zero()) ? fe_zero_host() : to_dev(F.inv(z));
+      d.xs_m[t] = to_dev(wt);
+      wt = F.mul(wt, w8);
+    }
+  }
+  hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(P)), dim3(256), 0, s, ca);
+  STARK_HIP(ctx, hipGetLastError());
+  // hc2 and the uploads above must outlive the copies: wait here (the caller
+  // reads a_root and the constraint flags next anyway).
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  return STARK_OK;
+}
+
 }  // namespace stark
 
 using namespace stark;
@@ -836,5 +1105,108 @@ stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_roo
 }
 
 void stark_r1cs_proof_free(stark_r1cs_proof* proof) { delete proof; }
+
+stark_status stark_dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
+                                const uint64_t* computational_trace, size_t original_steps,
+                                const uint64_t* public_wires, size_t n_public, const size_t* public_first_indices,
+                                size_t n_public_first, const size_t* permuted_indices, const uint64_t* coefficients,
+                                const uint64_t* flag0, const uint64_t* flag1, const uint64_t* flag2,
+                                size_t n_constraints, size_t n_wires, void* stream, stark_dprove** out) {
+  if (!ctx || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  if (original_steps && (!witness_trace || !computational_trace || !permuted_indices || !coefficients || !flag0 ||
+                         !flag1 || !flag2))
+    return STARK_ERR_BAD_ARG;
+  if ((n_public && !public_wires) || (n_public_first && !public_first_indices)) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  auto h = std::make_unique<stark_dprove>();
+  hipStream_t s = pick_stream(ctx, stream);
+  const stark_status st = dprove_begin(ctx, world, rank, witness_trace, computational_trace, original_steps,
+                                       public_wires, n_public, public_first_indices, n_public_first, permuted_indices,
+                                       coefficients, flag0, flag1, flag2, nullptr, n_constraints, n_wires, s, h.get());
+  if (st != STARK_OK) {
+    hipStreamSynchronize(s);
+    return st;
+  }
+  *out = h.release();
+  return STARK_OK;
+}
+
+stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
+                                      size_t r1cs_len, const uint8_t* wtns, size_t wtns_len, void* stream,
+                                      stark_dprove** out) {
+  if (!ctx || !r1cs || !wtns || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  DevTrace dt;
+  stark_status st = r1cs_trace_device(ctx, r1cs, r1cs_len, wtns, wtns_len, &dt);
+  if (st != STARK_OK) return st;
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the trace builder runs on the context stream
+  auto h = std::make_unique<stark_dprove>();
+  hipStream_t s = pick_stream(ctx, stream);
+  st = dprove_begin(ctx, world, rank, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
+                    dt.public_wires.data(), dt.public_wires.size() / 4, dt.public_first_indices.data(),
+                    dt.public_first_indices.size() / 2, (const size_t*)dt.perm, (const uint64_t*)dt.coef, nullptr,
+                    nullptr, nullptr, dt.flags, dt.n_constraints, dt.n_wires, s, h.get());
+  if (st != STARK_OK) {
+    hipStreamSynchronize(s);
+    return st;
+  }
+  *out = h.release();
+  return STARK_OK;
+}
+
+stark_status stark_dprove_info(stark_dprove* h, size_t* precision, size_t* n_local, size_t* original_steps,
+                               uint64_t g2[4], uint8_t a_root[32]) {
+  if (!h) return STARK_ERR_BAD_ARG;
+  DProveState& d = h->st;
+  if (precision) *precision = d.prec;
+  if (n_local) *n_local = d.P;
+  if (original_steps) *original_steps = d.os;
+  if (g2) memcpy(g2, d.g2c, 32);
+  Transcript t;
+  STARK_HIP(d.ctx, hipMemcpyAsync(&t, d.d_tr, sizeof(Transcript), hipMemcpyDeviceToHost, d.s));
+  STARK_HIP(d.ctx, hipStreamSynchronize(d.s));
+  if (a_root) memcpy(a_root, t.roots[0], 32);
+  if (t.err) {
+    d.ctx->last_error = (t.err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
+                                    : "invalid B: boundary value mismatch (utils.rs:477-524)";
+    return STARK_ERR_CHECK;
+  }
+  return STARK_OK;
+}
+
+stark_status stark_dprove_rows(stark_dprove* h, uint8_t** rows_dev) {
+  if (!h || !rows_dev) return STARK_ERR_BAD_ARG;
+  *rows_dev = (uint8_t*)h->st.rows;
+  return STARK_OK;
+}
+
+stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uint64_t** l_dev) {
+  if (!h || !m_root || !l_dev) return STARK_ERR_BAD_ARG;
+  DProveState& d = h->st;
+  const Mont mc = mont();
+  STARK_HIP(d.ctx, hipSetDevice(d.ctx->device));
+  // k from m_root (prove.rs:274-283) on the device, then L at this rank's points.
+  uint32_t* d_root = d.d_tr->roots[1];
+  STARK_HIP(d.ctx, hipMemcpyAsync(d_root, m_root, 32, hipMemcpyHostToDevice, d.s));
+  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, d.d_tr);
+  STARK_HIP(d.ctx, hipGetLastError());
+  LincombArgs la;
+  la.rows = d.rows;
+  la.out = d.lvals;
+  la.prec = d.P;
+  la.g_add = d.r;
+  la.log_g = d.log_g;
+  la.tr = d.d_tr;
+  for (int t = 0; t < 8; ++t) la.xs_m[t] = d.xs_m[t];
+  hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(d.P)), dim3(256), 0, d.s, la);
+  STARK_HIP(d.ctx, hipGetLastError());
+  STARK_HIP(d.ctx, hipStreamSynchronize(d.s));  // m_root is the caller's (pageable) buffer
+  *l_dev = (uint64_t*)d.lvals;
+  return STARK_OK;
+}
+
+void stark_dprove_free(stark_dprove* h) { delete h; }
 
 }  // extern "C"

@@ -109,6 +109,22 @@ _SIGNATURES = {
     "stark_memcpy_h2d": ([_vp, _vp, _vp, ctypes.c_size_t], ctypes.c_int),
     "stark_memcpy_d2h": ([_vp, _vp, _vp, ctypes.c_size_t], ctypes.c_int),
     "stark_ctx_synchronize": ([_vp], ctypes.c_int),
+    "stark_merkle_leaf_digests_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp, _vp], ctypes.c_int),
+    "stark_merkle_update_digests_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_uint32, _vp], ctypes.c_int),
+    "stark_gather_rows_dev": ([_vp, _vp, ctypes.c_size_t, _szp, ctypes.c_size_t, _u8p, _vp], ctypes.c_int),
+    "stark_fri_fold_dev": ([_vp, _vp, _vp, ctypes.c_size_t, _u64p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _vp],
+                           ctypes.c_int),
+    "stark_r1cs_proof_json_from_parts": ([_u8p, _u8p, _u8p, _vp, _vp, _vp, ctypes.c_size_t, _u8p, ctypes.c_size_t,
+                                          ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
+    "stark_dprove_begin": ([_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, ctypes.c_size_t, _u64p,
+                            ctypes.c_size_t, _szp, ctypes.c_size_t, _szp, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t,
+                            ctypes.c_size_t, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_begin_bytes": ([_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                  ctypes.c_char_p, ctypes.c_size_t, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_info": ([_vp, _szp, _szp, _szp, _u64p, _u8p], ctypes.c_int),
+    "stark_dprove_rows": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_lincomb": ([_vp, _u8p, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_free": ([_vp], None),
 }
 
 _lib = None
@@ -465,6 +481,13 @@ class MerkleProofInPlace:
     def update_dev(self, d_ptr: int, n: int, leaf_len: int, stream: int = 0) -> None:
         self.leaf_len = leaf_len
         self.ctx.check(self.ctx.lib.stark_merkle_update_dev(self.h, d_ptr, n, leaf_len, stream or None), "update")
+
+    def update_digests_dev(self, d_ptr: int, n: int, interleave: int = 1, stream: int = 0) -> None:
+        """Tree over n given leaf digests (device), stored as `interleave` residue-class chunks
+        (stark_merkle_update_digests_dev); proofs return the leaf digest as the leaf."""
+        self.leaf_len = 32
+        self.ctx.check(self.ctx.lib.stark_merkle_update_digests_dev(self.h, d_ptr, n, interleave, stream or None),
+                       "update_digests")
 
     def gen_proofs(self, indices) -> list:
         idx = list(indices)
