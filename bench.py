@@ -106,6 +106,43 @@ def end_to_end(ctx):
     return out
 
 
+def distributed_prove(ctx, world, rank, on_gloo, local):
+    """One StarkProof shared by all ranks (stark_amd/dprove.py: residue-class layout, digest all-to-alls
+    over RCCL): pedersen_test checked bit-exact against the golden digest, and the synthetic 2^20-step
+    circuit (sha256_2_test stand-in) timed, max over ranks."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth_r1cs
+    from stark_amd.dprove import GpuProverOps, prove_distributed
+    ops = GpuProverOps(ctx)
+    fix = os.path.join(ROOT, "tests", "golden", "r1cs")
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
+    out = {}
+    r1 = open(os.path.join(fix, "pedersen_test.r1cs"), "rb").read()
+    wt = open(os.path.join(fix, "pedersen_test.wtns"), "rb").read()
+    js = prove_distributed(ops, r1, wt)
+    if rank == 0:
+        out["prove_pedersen_distributed_bitexact_vs_golden"] = \
+            hashlib.sha256(js.encode()).hexdigest() == golden["pedersen_test"]["json_sha256"]
+
+    def timed(rs, ws, reps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            prove_distributed(ops, rs, ws)
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64,
+                         device="cpu" if on_gloo else f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(float(t.cpu()[0]) * 1000.0, 3)
+
+    out["prove_pedersen_distributed_ms"] = timed(r1, wt, 3)
+    rs, ws = synth_r1cs.for_steps(20)
+    prove_distributed(ops, rs, ws)   # warm: twiddles, arenas
+    out["prove_synth_2^20_steps_distributed_ms"] = timed(rs, ws, 3)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -278,6 +315,7 @@ def main():
                             device="cpu" if on_gloo else f"cuda:{local}")
         dist.all_reduce(same, op=dist.ReduceOp.MIN)
         extras["distributed_schedule_matches_cyclic_ntt"] = bool(float(same.cpu()[0]) == 1.0)
+        extras.update(distributed_prove(ctx, world, rank, on_gloo, local))
 
     # Roofline of the dominant kernel, ntt_pass_kernel: one 2^24 transform is
     # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element

@@ -271,9 +271,20 @@ stark_status stark_merkle_leaf_digests_dev(stark_ctx* ctx, const uint8_t* d_leav
  * digest as the leaf bytes. */
 stark_status stark_merkle_update_digests_dev(stark_merkle_tree* tree, const uint8_t* d_digests, size_t n,
                                              uint32_t interleave, void* stream);
-/* out[i] = the idx[i]-th row (row_bytes) of d_rows, to host memory (openings of leaves held here). */
-stark_status stark_gather_rows_dev(stark_ctx* ctx, const uint8_t* d_rows, size_t row_bytes, const size_t* idx,
-                                   size_t k, uint8_t* out, void* stream);
+/* Many openings in one launch: request i gathers, for its k indices, the leaves
+ * (leaf_len bytes each) and log2(n) sibling digests of `tree`, or, when tree is
+ * NULL, only the rows (row_bytes each) of the device buffer d_rows (n_rows rows).
+ * Either output may be NULL. */
+typedef struct stark_open_req {
+  stark_merkle_tree* tree;
+  const uint8_t* d_rows;
+  size_t row_bytes, n_rows;
+  const size_t* idx;
+  size_t k;
+  uint8_t* leaves_out;
+  uint8_t* nodes_out;
+} stark_open_req;
+stark_status stark_open_batch(stark_ctx* ctx, const stark_open_req* reqs, size_t n_req, void* stream);
 /* One FRI fold (fri.rs:135-164) on a residue class: `values` = the layer's n
  * values at points rank + world j (n/world of them, root = the layer's root of
  * unity), `column` = the folded column's rows rank + world j (n/(4 world));

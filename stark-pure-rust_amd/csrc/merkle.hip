@@ -627,25 +627,34 @@ stark_status stark_merkle_update_digests_dev(stark_merkle_tree* t, const uint8_t
   return merkle_build(ctx, t, nullptr, n, 32, s);
 }
 
-// out[i] = rows[idx[i]] (row_bytes each): openings of leaves held on this GPU.
-stark_status stark_gather_rows_dev(stark_ctx* ctx, const uint8_t* d_rows, size_t row_bytes, const size_t* idx,
-                                   size_t k, uint8_t* out, void* stream) {
-  if (!ctx || (k && (!d_rows || !idx || !out)) || row_bytes > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
-  if (k == 0) return STARK_OK;
+// Every opening of a distributed proof on this rank in one zero-copy gather launch:
+// request i reads paths (and leaf digests) from reqs[i].tree, or, with tree == NULL,
+// leaf bytes from a row buffer.
+stark_status stark_open_batch(stark_ctx* ctx, const stark_open_req* reqs, size_t n_req, void* stream) {
+  if (!ctx || (n_req && !reqs)) return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
-  hipStream_t s = pick_stream(ctx, stream);
-  const size_t idx_bytes = (k * sizeof(uint64_t) + 15) & ~(size_t)15;
-  stark_status st = ensure_buf(ctx, ctx->io2, idx_bytes + k * row_bytes);
-  if (st != STARK_OK) return st;
-  uint8_t* base = (uint8_t*)ctx->io2.ptr;
-  STARK_HIP(ctx, hipMemcpyAsync(base, idx, k * sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)k), dim3(64), 0, s, d_rows, (uint32_t)row_bytes,
-                     (const Digest*)nullptr, (uint64_t)0, (uint32_t)0, (const uint64_t*)base, (uint32_t)k,
-                     base + idx_bytes, (Digest*)nullptr);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_HIP(ctx, hipMemcpyAsync(out, base + idx_bytes, k * row_bytes, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
-  return STARK_OK;
+  std::vector<stark_merkle_tree> views(n_req);  // row buffers seen as depth-0 trees
+  std::vector<GatherReq> g;
+  for (size_t i = 0; i < n_req; ++i) {
+    const stark_open_req& q = reqs[i];
+    if (q.k && (!q.idx || (!q.leaves_out && !q.nodes_out))) return STARK_ERR_BAD_ARG;
+    stark_merkle_tree* t = q.tree;
+    if (!t) {
+      if (!q.d_rows || q.row_bytes > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+      stark_merkle_tree& v = views[i];
+      v.ctx = ctx;
+      v.n = q.n_rows;
+      v.leaf_len = q.row_bytes;
+      v.depth = 0;
+      v.d_leaves = q.d_rows;
+      v.built = true;
+      t = &v;
+    } else if (!t->built) {
+      return STARK_ERR_STATE;
+    }
+    g.push_back({t, q.idx, q.k, q.leaves_out, q.nodes_out});
+  }
+  return merkle_gather_batch(ctx, g, pick_stream(ctx, stream));
 }
 
 size_t stark_merkle_width(const stark_merkle_tree* t) { return t ? t->n : 0; }

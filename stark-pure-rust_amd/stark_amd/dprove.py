@@ -104,33 +104,38 @@ class DistTree:
         self.root = self.top[-1][0]
         return self.root
 
-    def contributions(self, indices) -> tuple:
-        """This rank's parts of the openings: {k: leaf bytes}, {k: lower path}."""
+    def open_plan(self, idx: np.ndarray) -> list:
+        """This rank's gathers for opening leaves idx: (rows request, path request).
+        A leaf comes from its class owner, the lower path from the subtree owner
+        (or rank 0 when the tree is whole on every rank)."""
         G, r, m = self.G, self.r, self.n_local
-        mine_leaf = [(k, i) for k, i in enumerate(indices) if i % G == r]
-        leaves = {}
-        if mine_leaf:
-            got = self.ops.gather(self.leaves, self.leaf_len, [i // G for _, i in mine_leaf])
-            leaves = {k: b for (k, _), b in zip(mine_leaf, got)}
+        leaf_local = idx[idx % G == r] // G
         if self.blocked:
-            mine_path = [(k, i - r * m) for k, i in enumerate(indices) if i // m == r]
+            path_local = idx[idx // m == r] - r * m
         else:
-            mine_path = [(k, i) for k, i in enumerate(indices)] if r == 0 else []
-        paths = {}
-        if mine_path:
-            got = self.tree.open([li for _, li in mine_path])
-            paths = {k: nodes for (k, _), nodes in zip(mine_path, got)}
-        return leaves, paths
+            path_local = idx if r == 0 else idx[:0]
+        return [("rows", self.leaves, self.leaf_len, m, leaf_local), ("tree", self.tree, path_local)]
 
-    def top_path(self, index: int) -> list:
-        if not self.blocked:
-            return []
-        pos = index // self.n_local
-        out = []
-        for lv in self.top[:-1]:
-            out.append(lv[pos ^ 1])
-            pos >>= 1
-        return out
+    def assemble(self, idx: np.ndarray, parts: list) -> tuple:
+        """(k x leaf_len leaves, k x depth x 32 nodes) from every rank's (leaf blob, node blob)."""
+        G, m, k = self.G, self.n_local, len(idx)
+        depth = self.n.bit_length() - 1
+        leaves = np.empty((k, self.leaf_len), dtype=np.uint8)
+        nodes = np.empty((k, depth, 32), dtype=np.uint8)
+        low = (m.bit_length() - 1) if self.blocked else depth
+        for p, (lb, nb) in enumerate(parts):
+            sel = idx % G == p
+            leaves[sel] = np.frombuffer(lb, dtype=np.uint8).reshape(-1, self.leaf_len)
+            psel = (idx // m == p) if self.blocked else np.full(k, p == 0)
+            if psel.any():
+                nodes[psel, :low] = np.frombuffer(nb, dtype=np.uint8).reshape(-1, low, 32)
+        if self.blocked:
+            pos = idx // m
+            for lvl, lv in enumerate(self.top[:-1]):
+                arr = np.frombuffer(b"".join(lv), dtype=np.uint8).reshape(-1, 32)
+                nodes[:, low + lvl] = arr[pos ^ 1]
+                pos = pos >> 1
+        return leaves, nodes
 
 
 def _from_bytes_le(b: bytes) -> int:
@@ -151,32 +156,53 @@ class _FriLayer(ctypes.Structure):
     _fields_ = [("root2", ctypes.c_char_p), ("column", _Branches), ("poly", _Branches)]
 
 
-def _branches(proofs, leaf_len: int, depth: int, keep: list) -> _Branches:
-    lv = b"".join(p[0] for p in proofs)
-    nd = b"".join(b"".join(p[1]) for p in proofs)
+def _branches(opened, keep: list) -> _Branches:
+    leaves, nodes = opened
+    lv, nd = leaves.tobytes(), nodes.tobytes()
     keep += [lv, nd]
-    return _Branches(lv, nd, len(proofs), leaf_len, depth)
+    return _Branches(lv, nd, leaves.shape[0], leaves.shape[1], nodes.shape[1])
 
 
-def render_json(lib, m_root, l_root, a_root, main, main_depth, lcomb, l_depth, layers, last_values) -> str:
-    """stark_r1cs_proof_json_from_parts: serde_json of StarkProof (utils.rs:122-130)."""
+def render_json(lib, m_root, l_root, a_root, main, lcomb, layers, last: bytes) -> str:
+    """stark_r1cs_proof_json_from_parts: serde_json of StarkProof (utils.rs:122-130).
+    main / lcomb / each layer's column and poly: (leaves k x leaf_len, nodes k x depth x 32) arrays."""
     keep = []
-    mb = _branches(main, 256, main_depth, keep)
-    lb = _branches(lcomb, 32, l_depth, keep)
+    mb = _branches(main, keep)
+    lb = _branches(lcomb, keep)
     arr = (_FriLayer * max(len(layers), 1))()
-    for i, (root2, col, cdepth, poly, pdepth) in enumerate(layers):
+    for i, (root2, col, poly) in enumerate(layers):
         keep.append(root2)
-        arr[i] = _FriLayer(root2, _branches(col, 32, cdepth, keep), _branches(poly, 32, pdepth, keep))
-    last = b"".join(last_values)
-    cap = 64 + 4 * (len(b"".join(keep)) + len(last) + 96) + 64 * (len(main) + len(lcomb) + 200 * (len(layers) + 1))
+        arr[i] = _FriLayer(root2, _branches(col, keep), _branches(poly, keep))
+    total = sum(len(x) for x in keep) + len(last) + 96
+    nproofs = main[0].shape[0] + lcomb[0].shape[0] + sum(c[0].shape[0] + q[0].shape[0] for _, c, q in layers)
+    cap = 256 + 4 * total + 32 * nproofs + 64 * len(layers)
     buf = ctypes.create_string_buffer(cap)
     n = ctypes.c_size_t(0)
     rc = lib.stark_r1cs_proof_json_from_parts(m_root, l_root, a_root, ctypes.byref(mb), ctypes.byref(lb),
                                               ctypes.cast(arr, ctypes.c_void_p), len(layers), last,
-                                              len(last_values), buf, cap, ctypes.byref(n))
+                                              len(last) // 32, buf, cap, ctypes.byref(n))
     if rc != 0 or n.value >= cap:
         raise RuntimeError(f"stark_r1cs_proof_json_from_parts failed ({rc}, {n.value} >= {cap})")
     return buf.raw[:n.value].decode()
+
+
+class _Phases:
+    """STARK_PROFILE=1: wall-clock of each phase on this rank (stderr)."""
+
+    def __init__(self, rank: int):
+        import os
+        import time
+        self.on = os.environ.get("STARK_PROFILE", "0") not in ("", "0")
+        self.rank, self.time = rank, time.perf_counter
+        self.t0 = self.last = self.time()
+
+    def mark(self, what: str):
+        if self.on:
+            import sys
+            now = self.time()
+            print(f"[dprove r{self.rank}] {what}: {1e3 * (now - self.last):.3f} ms (total {1e3 * (now - self.t0):.3f})",
+                  file=sys.stderr)
+            self.last = now
 
 
 def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
@@ -184,6 +210,7 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
     Every rank calls it; rank 0 returns the StarkProof JSON, the others None."""
     G = dist.get_world_size(group)
     r = dist.get_rank(group)
+    ph = _Phases(r)
     if G & (G - 1) or G > EXTENSION_FACTOR:
         raise ValueError(f"prove_distributed: world size must be a power of two <= 8 (got {G})")
     h = ops.begin(r1cs, wtns, G, r)
@@ -193,14 +220,17 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
         if any(codes):
             ops.raise_status(next(c for c in codes if c), "prove_distributed")
         prec, n_local, os_, g2, a_root = info
+        ph.mark("trace + LDE + constraints (begin)")
         skips = EXTENSION_FACTOR
         log_prec = prec.bit_length() - 1
         # Main tree over the 256-B rows (prove.rs:235-264) -> k -> L (prove.rs:274-322) -> L tree.
         main = DistTree(ops, group)
         m_root = main.commit(ops.rows(h), n_local, 256)
+        ph.mark("main tree")
         lvals = ops.lincomb(h, m_root, _k_values(m_root))
         ltree = DistTree(ops, group)
         l_root = ltree.commit(lvals, n_local, 32)
+        ph.mark("L + L tree")
         # prove_low_degree(L, g2, precision/4, skips) (prove.rs:367, fri.rs:46-224), layer by layer.
         layers = []
         vals, n, w, deg, mtree, mroot = lvals, prec, g2, prec // 4, ltree, l_root
@@ -214,6 +244,7 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
             layers.append((root2, t2, ys, mtree, poly_idx, (q.bit_length() - 1)))
             vals, n, w, deg, mtree, mroot = col, q, pow(w, 4, P), deg // 4, t2, root2
         last_local = ops.to_host(vals, n // G)
+        ph.mark(f"FRI ({len(layers)} layers)")
         # Spot checks (prove.rs:337-362).
         positions = get_pseudorandom_indices(l_root, prec, SPOT_CHECK_SECURITY_FACTOR, skips)
         aug = []
@@ -222,30 +253,29 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
         reqs = [(main, aug), (ltree, positions)]
         for (_, t2, ys, mt, poly_idx, _) in layers:
             reqs += [(t2, ys), (mt, poly_idx)]
-        parts = [t.contributions(idx) for t, idx in reqs]
-        allparts = _all_gather_object((parts, last_local), G, group)
+        reqs = [(t, np.asarray(idx, dtype=np.uint64)) for t, idx in reqs]
+        plan = [g for t, idx in reqs for g in t.open_plan(idx)]
+        got = ops.open_batch(plan)        # one gather launch for every opening held here
+        mine = [(got[2 * i][0], got[2 * i + 1][1]) for i in range(len(reqs))]
+        allparts = _all_gather_object((mine, last_local), G, group)
+        ph.mark("openings")
         if r != 0:
             return None
-        proofs = []
-        for q_i, (t, idx) in enumerate(reqs):
-            out = []
-            for k, i in enumerate(idx):
-                leaf = next(p[0][q_i][0][k] for p in allparts if k in p[0][q_i][0])
-                lower = next(p[0][q_i][1][k] for p in allparts if k in p[0][q_i][1])
-                out.append((leaf, list(lower) + t.top_path(i)))
-            proofs.append(out)
-        last_values = []
-        chunks = [p[1] for p in allparts]
-        for j in range(n // G):
-            for rr in range(G):
-                last_values.append(chunks[rr][32 * j:32 * (j + 1)])
-        fri_parts = []
-        for li, (root2, t2, ys, mt, poly_idx, log_q) in enumerate(layers):
-            fri_parts.append((root2, proofs[2 + 2 * li], log_q, proofs[3 + 2 * li], log_q + 2))
-        return render_json(ops.lib, m_root, l_root, a_root, proofs[0], log_prec, proofs[1], log_prec, fri_parts,
-                           last_values)
+        opened = [t.assemble(idx, [p[0][i] for p in allparts]) for i, (t, idx) in enumerate(reqs)]
+        chunks = np.stack([np.frombuffer(p[1], dtype=np.uint8).reshape(-1, 32) for p in allparts], axis=1)
+        last = chunks.reshape(-1, 32).tobytes()   # value r + G j is rank r's j-th
+        fri_parts = [(root2, opened[2 + 2 * li], opened[3 + 2 * li]) for li, (root2, *_rest) in enumerate(layers)]
+        js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, last)
+        ph.mark("assembly + JSON")
+        return js
     finally:
         ops.end(h)
+
+
+class _OpenReq(ctypes.Structure):
+    _fields_ = [("tree", ctypes.c_void_p), ("d_rows", ctypes.c_void_p), ("row_bytes", ctypes.c_size_t),
+                ("n_rows", ctypes.c_size_t), ("idx", ctypes.POINTER(ctypes.c_size_t)), ("k", ctypes.c_size_t),
+                ("leaves_out", ctypes.c_void_p), ("nodes_out", ctypes.c_void_p)]
 
 
 class GpuProverOps:
@@ -309,14 +339,31 @@ class GpuProverOps:
     def new_tree(self):
         return _GpuTree(self)
 
-    def gather(self, buf, row_bytes: int, local_indices) -> list:
+    def open_batch(self, plan) -> list:
+        """stark_open_batch over ("rows", buf, row_bytes, n_rows, idx) / ("tree", tree, idx)
+        requests: a list of (leaf blob, node blob) per request."""
         from . import _szp
-        idx = np.ascontiguousarray(np.asarray(local_indices, dtype=np.uint64))
-        out = ctypes.create_string_buffer(len(idx) * row_bytes)
-        self.ctx.check(self.lib.stark_gather_rows_dev(self.ctx.h, self._ptr(buf), row_bytes, idx.ctypes.data_as(_szp),
-                                                      len(idx), out, self._stream()), "gather_rows")
-        raw = out.raw
-        return [raw[i * row_bytes:(i + 1) * row_bytes] for i in range(len(idx))]
+        reqs = (_OpenReq * max(len(plan), 1))()
+        keep, outs = [], []
+        for i, g in enumerate(plan):
+            if g[0] == "rows":
+                _, buf, row_bytes, n_rows, idx = g
+                tree, rows, leaf_len, depth = None, self._ptr(buf), row_bytes, 0
+            else:
+                _, tr, idx = g
+                tree, rows, n_rows, row_bytes = tr.t.h, None, 0, 0
+                leaf_len, depth = 32, max(tr.t.width().bit_length() - 1, 0)
+            idx = np.ascontiguousarray(idx, dtype=np.uint64)
+            lo = ctypes.create_string_buffer(max(len(idx) * leaf_len, 1))
+            no = ctypes.create_string_buffer(max(len(idx) * depth * 32, 1))
+            keep += [idx, lo, no]
+            outs.append((lo, len(idx) * leaf_len, no, len(idx) * depth * 32))
+            reqs[i] = _OpenReq(tree, rows, row_bytes, n_rows, idx.ctypes.data_as(_szp), len(idx),
+                               ctypes.cast(lo, ctypes.c_void_p), ctypes.cast(no, ctypes.c_void_p))
+        torch.cuda.current_stream().synchronize()   # trees were built on this stream
+        self.ctx.check(self.lib.stark_open_batch(self.ctx.h, ctypes.cast(reqs, ctypes.c_void_p), len(plan),
+                                                 self._stream()), "open_batch")
+        return [(lo.raw[:nl], no.raw[:nn]) for lo, nl, no, nn in outs]
 
     def fold(self, vals, n: int, root: int, m_root: bytes, G: int, r: int) -> torch.Tensor:
         from . import _limbs, _p64
@@ -344,6 +391,3 @@ class _GpuTree:
         torch.cuda.current_stream().synchronize()
         self.t.gen_proofs([])      # sets the root (MerkleProofInPlace::get_root semantics)
         return self.t.get_root()
-
-    def open(self, local_indices) -> list:
-        return [p.nodes for p in self.t.gen_proofs(local_indices)]

@@ -110,8 +110,16 @@ class OracleProverOps:
     def new_tree(self):
         return _PyTree()
 
-    def gather(self, buf, row_bytes, idx):
-        return [bytes(buf[row_bytes * i:row_bytes * (i + 1)]) for i in idx]
+    def open_batch(self, plan):
+        out = []
+        for g in plan:
+            if g[0] == "rows":
+                _, buf, row_bytes, _, idx = g
+                out.append((b"".join(bytes(buf[row_bytes * int(i):row_bytes * (int(i) + 1)]) for i in idx), b""))
+            else:
+                _, tree, idx = g
+                out.append((b"", b"".join(b"".join(nodes) for nodes in tree.open([int(i) for i in idx]))))
+        return out
 
     def fold(self, vals, n, root, m_root, G, r):
         """Column rows r + G j: the cubic through (w^(i + t n/4), v[i + t n/4]) at special_x (fri.rs:135-164)."""
