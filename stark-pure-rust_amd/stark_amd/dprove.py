@@ -205,7 +205,14 @@ class _Phases:
             self.last = now
 
 
-def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
+# FRI layers of at most 2^FRI_TAIL_LOG values are not worth a collective each: their
+# values go to rank 0, which proves the rest of the FRI recursion alone (one device-resident
+# prove_low_degree, no per-layer host round trip).  The proof is the same.
+FRI_TAIL_LOG = 16
+_EMPTY_LAST = '{"Last":{"last":[]}}]}'
+
+
+def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: int = FRI_TAIL_LOG):
     """prove_with_witness (run.rs:310-452) over the G ranks of `group`.
     Every rank calls it; rank 0 returns the StarkProof JSON, the others None."""
     G = dist.get_world_size(group)
@@ -234,7 +241,7 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
         # prove_low_degree(L, g2, precision/4, skips) (prove.rs:367, fri.rs:46-224), layer by layer.
         layers = []
         vals, n, w, deg, mtree, mroot = lvals, prec, g2, prec // 4, ltree, l_root
-        while deg > 16:
+        while deg > 16 and n > (1 << fri_tail_log):
             q = n // 4
             col = ops.fold(vals, n, w, mroot, G, r)
             t2 = DistTree(ops, group)
@@ -263,9 +270,17 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None):
             return None
         opened = [t.assemble(idx, [p[0][i] for p in allparts]) for i, (t, idx) in enumerate(reqs)]
         chunks = np.stack([np.frombuffer(p[1], dtype=np.uint8).reshape(-1, 32) for p in allparts], axis=1)
-        last = chunks.reshape(-1, 32).tobytes()   # value r + G j is rank r's j-th
+        values = chunks.reshape(-1, 32).tobytes()   # value r + G j is rank r's j-th
         fri_parts = [(root2, opened[2 + 2 * li], opened[3 + 2 * li]) for li, (root2, *_rest) in enumerate(layers)]
-        js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, last)
+        if deg <= 16:
+            js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, values)
+        else:
+            # The remaining layers [Middle.., Last] of prove_low_degree_rec on this layer's values,
+            # spliced in place of an empty Last.
+            tail = ops.fri_tail(values, n, w, deg, skips)
+            js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, b"")
+            assert js.endswith(_EMPTY_LAST) and tail.startswith("[") and tail.endswith("]")
+            js = js[:-len(_EMPTY_LAST)] + tail[1:] + "}"
         ph.mark("assembly + JSON")
         return js
     finally:
@@ -364,6 +379,11 @@ class GpuProverOps:
         self.ctx.check(self.lib.stark_open_batch(self.ctx.h, ctypes.cast(reqs, ctypes.c_void_p), len(plan),
                                                  self._stream()), "open_batch")
         return [(lo.raw[:nl], no.raw[:nn]) for lo, nl, no, nn in outs]
+
+    def fri_tail(self, values: bytes, n: int, root: int, max_deg_plus_1: int, excl: int) -> str:
+        """prove_low_degree on the full layer (rank 0): its serde JSON."""
+        v = np.frombuffer(values, dtype=np.uint64).reshape(-1, 4)
+        return self.ctx.prove_low_degree(v, root, max_deg_plus_1, excl).to_json()
 
     def fold(self, vals, n: int, root: int, m_root: bytes, G: int, r: int) -> torch.Tensor:
         from . import _limbs, _p64

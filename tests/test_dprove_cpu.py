@@ -143,31 +143,36 @@ class OracleProverOps:
             out.append(acc.to_bytes(32, "little"))
         return b"".join(out)
 
+    def fri_tail(self, values, n, root, max_deg_plus_1, excl):
+        v = np.frombuffer(values, dtype=np.uint64).reshape(-1, 4)
+        return self.o.prove_low_degree_json(v, root, max_deg_plus_1, excl)
+
     def to_host(self, buf, count):
         return bytes(buf[:32 * count])
 
 
-def _worker(rank, world, port, name, out_q):
+def _worker(rank, world, port, name, tail_log, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from stark_amd.dprove import prove_distributed
     r1 = open(os.path.join(FIX, f"{name}.r1cs"), "rb").read()
     wt = open(os.path.join(FIX, f"{name}.wtns"), "rb").read()
-    js = prove_distributed(OracleProverOps(), r1, wt)
+    js = prove_distributed(OracleProverOps(), r1, wt, fri_tail_log=tail_log)
     out_q.put((rank, hashlib.sha256(js.encode()).hexdigest() if js is not None else None))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("compute", 1), ("compute", 2), ("compute", 4), ("compute", 8),
-                                        ("poseidon3_test", 4)])
-def test_prove_distributed_gloo(name, world):
+@pytest.mark.parametrize("name,world,tail_log", [("compute", 1, 0), ("compute", 2, 0), ("compute", 4, 16),
+                                                 ("compute", 8, 0), ("poseidon3_test", 4, 12)])
+def test_prove_distributed_gloo(name, world, tail_log):
+    """tail_log 0: every FRI layer distributed; else layers of <= 2^tail_log values on rank 0."""
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, tail_log, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=600) for _ in range(world))

@@ -27,7 +27,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, name, log_synth, out_q):
+def _worker(rank, world, port, name, log_synth, tail_log, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,7 +45,7 @@ def _worker(rank, world, port, name, log_synth, out_q):
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import synth_r1cs
         r1, wt = synth_r1cs.for_steps(log_synth)
-    js = prove_distributed(GpuProverOps(ctx), r1, wt)
+    js = prove_distributed(GpuProverOps(ctx), r1, wt, fri_tail_log=tail_log)
     single = prove_with_witness(ctx, r1, wt).to_json() if rank == 0 and not name else None
     digest = lambda s: hashlib.sha256(s.encode()).hexdigest() if s is not None else None
     out_q.put((rank, digest(js), digest(single)))
@@ -54,11 +54,11 @@ def _worker(rank, world, port, name, log_synth, out_q):
     dist.destroy_process_group()
 
 
-def _run(world, name, log_synth=0):
+def _run(world, name, log_synth=0, tail_log=16):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, log_synth, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, log_synth, tail_log, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: (a, b) for r, a, b in (q.get(timeout=600) for _ in range(world))}
@@ -69,11 +69,11 @@ def _run(world, name, log_synth=0):
     return res[0]
 
 
-@pytest.mark.parametrize("name,world", [("compute", 2), ("compute", 8), ("poseidon3_test", 4), ("pedersen_test", 2),
-                                        ("pedersen_test", 8), ("bits", 4)])
-def test_prove_distributed_gpu(name, world):
+@pytest.mark.parametrize("name,world,tail_log", [("compute", 2, 0), ("compute", 8, 16), ("poseidon3_test", 4, 0),
+                                                 ("pedersen_test", 2, 16), ("pedersen_test", 8, 12), ("bits", 4, 0)])
+def test_prove_distributed_gpu(name, world, tail_log):
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
-    got, _ = _run(world, name)
+    got, _ = _run(world, name, tail_log=tail_log)
     assert got == golden[name]["json_sha256"]
 
 
