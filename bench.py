@@ -251,6 +251,22 @@ def main():
         ctx.best_fft(hc, w, log_n)
         extras["best_fft_host_2^24_ms_pcie_inclusive"] = round((time.perf_counter() - t_h) * 1000.0, 2)
         del hc
+        # Size sweep 2^20..2^26 (north star: synthetic traces of 2^20-2^26 field elements), forward NTT,
+        # HBM-resident; elements uniform below 2^252 (< p), generated on the device.
+        sweep = {}
+        for ls in (20, 22, 24, 26):
+            g = torch.Generator(device=f"cuda:{local}").manual_seed(ls)
+            t = torch.randint(-2**63, 2**63 - 1, ((1 << ls), 4), dtype=torch.int64, device=f"cuda:{local}",
+                              generator=g)
+            t[:, 3] &= 0x0FFFFFFFFFFFFFFF
+            ws = O.root_of_unity(ls)
+            ctx.ntt_dev(t.data_ptr(), ls, 1, ws, inverse=False, stream=sptr)
+            ms = timed_events(lambda: ctx.ntt_dev(t.data_ptr(), ls, 1, ws, inverse=False, stream=sptr), stream, 5)
+            sweep[f"2^{ls}"] = {"ms": round(ms, 4), "elems_per_s": (1 << ls) / (ms / 1000.0),
+                                "hbm_frac": round(64.0 * (1 << ls) / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)}
+            del t
+        torch.cuda.empty_cache()
+        extras["ntt_sweep"] = sweep
         # inverse 2^24 throughput
         ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr)   # warm: builds the w^-1 tables
         inv_ms = timed_events(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream, 5)

@@ -220,9 +220,15 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
     ph = _Phases(r)
     if G & (G - 1) or G > EXTENSION_FACTOR:
         raise ValueError(f"prove_distributed: world size must be a power of two <= 8 (got {G})")
-    h = ops.begin(r1cs, wtns, G, r)
+    # A rank that fails must not leave the others blocked in a collective: every rank
+    # reports its status first and all of them raise together.
+    h, status, info = None, 0, None
     try:
+        h = ops.begin(r1cs, wtns, G, r)
         status, info = ops.info(h)
+    except Exception as e:  # noqa: BLE001 - re-raised below on every rank
+        status = getattr(e, "code", -1) or -1
+    try:
         codes = _all_gather_object(status, G, group)
         if any(codes):
             ops.raise_status(next(c for c in codes if c), "prove_distributed")
@@ -284,7 +290,8 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
         ph.mark("assembly + JSON")
         return js
     finally:
-        ops.end(h)
+        if h is not None:
+            ops.end(h)
 
 
 class _OpenReq(ctypes.Structure):

@@ -2,6 +2,7 @@
 libstark_hip's per-rank steps).  On the one-GPU test box the ranks share GPU 0
 and exchange through gloo; the 8-GPU bench runs the same code over RCCL.
 The proof must equal the single-GPU / oracle proof byte for byte."""
+import datetime
 import hashlib
 import json
 import os
@@ -28,9 +29,11 @@ def _free_port():
 
 
 def _worker(rank, world, port, name, log_synth, tail_log, out_q):
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)   # a stuck rank prints its stack and exits
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=80))
     import stark_amd as S
     from stark_amd.dprove import GpuProverOps, prove_distributed
     from stark_amd.r1cs import prove_with_witness
@@ -61,9 +64,11 @@ def _run(world, name, log_synth=0, tail_log=16):
     procs = [ctx.Process(target=_worker, args=(r, world, port, name, log_synth, tail_log, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = {r: (a, b) for r, a, b in (q.get(timeout=600) for _ in range(world))}
+    res = {r: (a, b) for r, a, b in (q.get(timeout=110) for _ in range(world))}
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
         assert p.exitcode == 0
     assert all(res[r][0] is None for r in range(1, world))
     return res[0]
