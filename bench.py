@@ -37,6 +37,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARC
 MODMUL_PEAK = 1024 * 2.4e9 * 64 / (256 * 4)
 LOG_N = 24
 PROFILE = os.path.join(ROOT, "profiles", "r01_summary.json")
+SQ_PROFILE = os.path.join(ROOT, "profiles", "r01_ntt_sq_counters.json")
 
 
 def parse():
@@ -371,6 +372,18 @@ def main():
     valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
     valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
+    try:
+        # VALU issue occupancy of the same kernel (committed rocprofv3 SQ counters): wave64 VALU
+        # instructions per launch x ~4.5 cycles each (the half-rate mad/carry ops that are ~90 % of the
+        # mix, tools/microbench/isa_lat.hip) over the SIMD-cycles of the measured launch.
+        sq = json.load(open(SQ_PROFILE))["kernels"]["stark::ntt_pass_kernel<8, false>"]
+        if log_n == 24:
+            simd_cycles = 1024 * 2.4e9 * (ev_ms / passes) / 1000.0
+            valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
+            valu["issue_busy_frac_est"] = round(sq["SQ_INSTS_VALU"] * 4.5 / simd_cycles, 3)
+            valu["sq_profile"] = os.path.relpath(SQ_PROFILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        pass
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
