@@ -181,3 +181,37 @@ def test_prove_distributed_gloo(name, world, tail_log):
         assert p.exitcode == 0
     assert res[0] == golden[name]["json_sha256"]
     assert all(res[r] is None for r in range(1, world))
+
+
+def _worker_bad(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from stark_amd.dprove import prove_distributed
+    r1 = open(os.path.join(FIX, "compute.r1cs"), "rb").read()
+    wt = open(os.path.join(FIX, "compute.wtns"), "rb").read()
+    if rank == 1:
+        wt = wt[:len(wt) // 2]          # one rank gets a truncated witness
+    try:
+        prove_distributed(OracleProverOps(), r1, wt)
+        out_q.put((rank, "no error"))
+    except Exception as e:  # noqa: BLE001
+        out_q.put((rank, type(e).__name__))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_prove_distributed_failure_raises_on_every_rank():
+    """A rank whose set-up fails must not leave the others blocked in a collective."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_bad, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(v != "no error" for v in res.values()), res
