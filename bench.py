@@ -104,6 +104,27 @@ def end_to_end(ctx):
         ts.append(time.perf_counter() - t0)
     out["prove_pedersen_ms"] = round(min(ts) * 1000.0, 3)
     out["prove_synth_2^20_steps_ms"] = round(synth_ms(3) * 1000.0, 3)
+    # The same proofs from a prepared circuit (R1csCircuit: the .r1cs-only work, including the LDEs of
+    # K, F0-F2, IDX, PIDX, done once outside the timed region): a prover serving many witnesses of
+    # one circuit.  Labelled separately; the lines above are the cold prove_with_witness.
+    from stark_amd.r1cs import R1csCircuit
+
+    def prepared_ms(r1b, wtb, reps):
+        c = R1csCircuit(ctx, r1b)
+        c.prove(wtb).to_json()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            c.prove(wtb).to_json()
+            ts.append(time.perf_counter() - t0)
+        return round(min(ts) * 1000.0, 3), c
+    out["prove_pedersen_prepared_circuit_ms"], c = prepared_ms(r1, wt, 5)
+    out["prove_pedersen_prepared_circuit_bitexact"] = \
+        hashlib.sha256(c.prove(wt).to_json().encode()).hexdigest() == golden["pedersen_test"]["json_sha256"]
+    del c
+    rs, ws = synth_r1cs.for_steps(20)
+    out["prove_synth_2^20_steps_prepared_circuit_ms"], c = prepared_ms(rs, ws, 3)
+    del c
     return out
 
 

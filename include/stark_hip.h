@@ -49,6 +49,7 @@ typedef struct stark_fri_proof stark_fri_proof;
 typedef struct stark_r1cs_proof stark_r1cs_proof;
 typedef struct stark_r1cs_trace stark_r1cs_trace;
 typedef struct stark_dprove stark_dprove;
+typedef struct stark_r1cs_circuit stark_r1cs_circuit;
 
 /* ---- context ------------------------------------------------------------ */
 /* Replaces commitment::multicore::Worker::new (packages/commitment/src/multicore.rs:43-45):
@@ -231,6 +232,17 @@ stark_status stark_prove_r1cs_trace(stark_ctx* ctx, const stark_r1cs_trace* trac
  * stark_prove_r1cs_trace on the same bytes. */
 stark_status stark_prove_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
                                     size_t wtns_len, stark_r1cs_proof** out);
+
+/* Prove many witnesses of one circuit: stark_r1cs_circuit_new does, once, all of
+ * prove_with_witness that depends on the .r1cs alone (slot layout, coefficients,
+ * flags, permutation, public first uses, and the LDEs of K, F0-F2, IDX, PIDX);
+ * stark_prove_r1cs_circuit then builds the witness columns and extends only S, P
+ * and A.  The proof equals stark_prove_r1cs_bytes on the same bytes.  A circuit
+ * is bound to the context that prepared it. */
+stark_status stark_r1cs_circuit_new(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, stark_r1cs_circuit** out);
+void stark_r1cs_circuit_free(stark_r1cs_circuit* circuit);
+stark_status stark_prove_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit, const uint8_t* wtns,
+                                      size_t wtns_len, stark_r1cs_proof** out);
 
 /* ---- multi-GPU four-step NTT building blocks (no reference counterpart;
  * the reference is single-process).  The exchanges are RCCL

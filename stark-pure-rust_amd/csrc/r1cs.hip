@@ -312,7 +312,7 @@ __global__ void r1cs_zb_kernel(const fe* __restrict__ lo, const fe* __restrict__
 }
 
 struct ConstraintArgs {
-  const fe* cols;        // K F0 F1 F2 S P IDX PIDX A, precision each
+  const fe* col[9];      // K F0 F1 F2 S P IDX PIDX A, precision (local points) each
   const fe* inv_zb;      // inv Zb2 (precision) then inv Zb3 (precision)
   const fe* interp2;     // canonical coefficients, low degree first
   const fe* interp3;
@@ -338,15 +338,15 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.prec) return;
   const uint64_t n = a.prec, mask = n - 1;
-  const fe* K = a.cols;
-  const fe* F0 = K + n;
-  const fe* F1 = F0 + n;
-  const fe* F2 = F1 + n;
-  const fe* S = F2 + n;
-  const fe* Pc = S + n;
-  const fe* IDX = Pc + n;
-  const fe* PIDX = IDX + n;
-  const fe* A = PIDX + n;
+  const fe* K = a.col[0];
+  const fe* F0 = a.col[1];
+  const fe* F1 = a.col[2];
+  const fe* F2 = a.col[3];
+  const fe* S = a.col[4];
+  const fe* Pc = a.col[5];
+  const fe* IDX = a.col[6];
+  const fe* PIDX = a.col[7];
+  const fe* A = a.col[8];
   const uint64_t prev = (i + n - a.back) & mask;
   const uint64_t gi = a.g_add + (i << a.log_g);  // global evaluation point
   const fe r0 = a.tr->r0, r1_m = a.tr->r1_m, r2_m = a.tr->r2_m;
@@ -529,7 +529,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
                                const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
                                const uint64_t* flag2, const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
-                               stark_r1cs_proof** out) {
+                               stark_r1cs_proof** out, const fe* pre = nullptr) {
+  // pre != nullptr: the circuit's LDE columns K F0 F1 F2 IDX PIDX (precision each), prepared
+  // once per circuit (stark_r1cs_circuit_new); only S, P and A are extended here.
   PhaseClock clk("mk_r1cs_proof");
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
@@ -621,12 +623,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).  The
   // inputs may be host or device pointers (the device trace builder's columns): hipMemcpyDefault.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
-  for (int c = 0; c < 6; ++c) {
+  for (int c = pre ? 4 : 0; c < 6; ++c) {
     if (!(flag_bytes && c >= 1 && c <= 3))
       STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyDefault, s));
     if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
   }
-  if (flag_bytes) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
+  if (flag_bytes && !pre) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
     uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel
     STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyDefault, s));
     hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
@@ -649,13 +651,16 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(ctx_tree(ctx, 3, &m_tree));
   STARK_TRY(ctx_tree(ctx, 4, &l_tree));
   STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
-  STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
+  if (pre)  // S and P only: K, the flags, IDX and PIDX are the circuit's
+    STARK_TRY(lde(ctx, raw + 4 * steps, 2, cols + 4 * prec, log_steps, log_prec, *tw1i, *tw2, s));
+  else
+    STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(acc_tree),
                      (uint32_t)(prec - 1), mc.r2, d_tr);
   STARK_HIP(ctx, hipGetLastError());
   // A (utils.rs:293-339, prove.rs:183-184).
-  fe* ext_idx = cols + 6 * prec;
-  fe* ext_pidx = cols + 7 * prec;
+  const fe* ext_idx = pre ? pre + 4 * prec : cols + 6 * prec;
+  const fe* ext_pidx = pre ? pre + 5 * prec : cols + 7 * prec;
   hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
                      (const fe*)ext_pidx, (const uint64_t*)nullptr, (uint64_t)0, (const fe*)wcopy, steps,
                      (const Transcript*)d_tr, mc.r2, nmr, dnm);
@@ -675,7 +680,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
 
   // Constraint kernel.
   ConstraintArgs ca;
-  ca.cols = cols;
+  for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * prec;
+  if (pre) {
+    for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * prec;
+    ca.col[6] = pre + 4 * prec;
+    ca.col[7] = pre + 5 * prec;
+  }
   ca.inv_zb = inv_zb;
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
@@ -793,6 +803,72 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   clk.mark("proof JSON");
   *out = proof.release();
   return STARK_OK;
+}
+
+// IDX / PIDX step columns only (the circuit's part of r1cs_index_kernel).
+__global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, uint64_t steps, fe* __restrict__ idx,
+                                fe* __restrict__ pidx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= steps) return;
+  fe_store(idx + i, fe_from_u64(i));
+  fe_store(pidx + i, fe_from_u64(i < os ? perm[i] : i));
+}
+
+// The LDE columns of a circuit that no witness changes: K, F0, F1, F2, IDX, PIDX
+// (prove.rs:100-124, 160-167), 6 x precision into `out`.  coef / flag bytes / perm
+// are the device trace builder's circuit columns (os slots).
+stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
+                         DevBuf& out, hipStream_t s) {
+  const FieldHost& F = FieldHost::get();
+  if (os < 5 || os % 3 != 0) return STARK_ERR_BAD_LENGTH;
+  const uint32_t log_steps = log2_ceil_ref(os - 1);
+  const uint32_t log_prec = log_steps + kLogExtensionFactor;
+  if (log_prec >= 24) return STARK_ERR_BAD_LENGTH;
+  const uint64_t steps = (uint64_t)1 << log_steps, prec = (uint64_t)1 << log_prec;
+  uint64_t pm1[4];
+  memcpy(pm1, FieldHost::kP, 32);
+  pm1[0] -= 1;
+  for (uint32_t k = 0; k < log_prec; ++k)
+    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
+  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
+  uint64_t g2c[4], g1ic[4];
+  F.to_canonical(g2, g2c);
+  F.to_canonical(F.inv(F.pow_u64(g2, prec / steps)), g1ic);
+  const Twiddles *tw2 = nullptr, *tw1i = nullptr;
+  STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
+  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
+  DevBuf tmp;
+  STARK_TRY(ensure_buf(ctx, tmp, 6 * steps * sizeof(fe)));
+  stark_status st = ensure_buf(ctx, out, 6 * prec * sizeof(fe));
+  if (st == STARK_OK) {
+    fe* raw = (fe*)tmp.ptr;
+    hipMemsetAsync(raw, 0, 6 * steps * sizeof(fe), s);
+    hipMemcpyAsync(raw, coef, os * sizeof(fe), hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, flag_bytes, (uint64_t)os, steps,
+                       raw + steps);
+    hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
+                       raw + 4 * steps, raw + 5 * steps);
+    st = lde(ctx, raw, 6, (fe*)out.ptr, log_steps, log_prec, *tw1i, *tw2, s);
+    if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
+  }
+  hipStreamSynchronize(s);
+  hipFree(tmp.ptr);
+  return st;
+}
+
+stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
+                                    size_t os, const uint64_t* public_wires, size_t n_public,
+                                    const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
+                                    const uint64_t* coefficients, const uint8_t* flag_bytes, size_t n_constraints,
+                                    size_t n_wires, const fe* pre, stark_r1cs_proof** out) {
+  if (!ctx || !out || !pre) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const stark_status st = prove_r1cs(ctx, witness_trace, computational_trace, os, public_wires, n_public,
+                                     public_first_indices, n_pfi, permuted_indices, coefficients, nullptr, nullptr,
+                                     nullptr, flag_bytes, n_constraints, n_wires, out, pre);
+  hipStreamSynchronize(ctx->stream);
+  return st;
 }
 
 stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
@@ -1020,7 +1096,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
   ConstraintArgs ca;
-  ca.cols = cols;
+  for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * P;
   ca.inv_zb = inv_zb;
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;

@@ -56,6 +56,7 @@ struct FillArgs {
   const fe* wmont;
   fe *coef, *wit, *comp;
   uint32_t *keys, *vals;
+  uint32_t* slot_wire;  // optional: the wire of every slot (prepared circuits)
   uint32_t* err;
 };
 
@@ -86,11 +87,14 @@ __global__ void slot_fill_kernel(FillArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v.w[k] = r[1 + k];
       cf = reduce_any(v);                                       // canonical from_bytes_le
-      tacc = fe_add(tacc, fe_mul(cf, fe_load(a.wmont + wire)));  // canonical * Montgomery
+      if (a.wmont) tacc = fe_add(tacc, fe_mul(cf, fe_load(a.wmont + wire)));  // canonical * Montgomery
     }
     fe_store(a.coef + slot, cf);
-    fe_store(a.wit + slot, fe_load(a.wcan + wire));
-    fe_store(a.comp + slot, tacc);
+    if (a.wmont) {  // no witness: circuit columns only
+      fe_store(a.wit + slot, fe_load(a.wcan + wire));
+      fe_store(a.comp + slot, tacc);
+    }
+    if (a.slot_wire) a.slot_wire[slot] = wire;
     a.keys[push0 + i] = wire;
     a.vals[push0 + i] = (uint32_t)slot;
   }
@@ -131,7 +135,59 @@ __global__ void perm_kernel(const uint32_t* __restrict__ keys, const uint32_t* _
   if (start && k < n_public) pf[k] = vals[j];
 }
 
+// The witness columns of a prepared circuit: the slot fill's witness / running-sum
+// part (run.rs:109-281) from the stored slot wires and coefficients.
+__global__ void wit_fill_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
+                                const uint32_t* __restrict__ slot_wire, const fe* __restrict__ coef,
+                                const fe* __restrict__ wcan, const fe* __restrict__ wmont, fe* __restrict__ wit,
+                                fe* __restrict__ comp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * (uint64_t)n_constraints) return;
+  const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
+  const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
+  fe tacc = fe_zero();
+  for (uint32_t i = 0; i < n_coeff; ++i) {
+    const uint64_t slot = (uint64_t)f * a_len + b0 + i;
+    const uint32_t wire = slot_wire[slot];
+    tacc = fe_add(tacc, fe_mul(fe_load(coef + slot), fe_load(wmont + wire)));  // padding slots: coefficient 0
+    fe_store(wit + slot, fe_load(wcan + wire));
+    fe_store(comp + slot, tacc);
+  }
+}
+
 unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// One host pass over the constraint records' counts: fac = fac_rec[3 n_c] (byte
+// offset of each factor's first record) | fac_cnt[3 n_c] | pad, and base[ci] = the
+// first slot of constraint ci (n_c + 1 entries; run.rs:109-137 slot counts).
+stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, std::vector<uint32_t>& fac,
+                          std::vector<uint32_t>& base) {
+  if (cons_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  fac.assign((size_t)6 * n_c + 1, 0);
+  base.assign((size_t)n_c + 1, 0);
+  uint32_t* fac_rec = fac.data();
+  uint32_t* fac_cnt = fac.data() + (size_t)3 * n_c;
+  size_t pos = 0;
+  uint64_t b = 0;
+  for (uint32_t ci = 0; ci < n_c; ++ci) {
+    uint32_t n_coeff = 0;
+    for (int f = 0; f < 3; ++f) {
+      if (cons_len - pos < 4) return STARK_ERR_BAD_ARG;
+      uint32_t nc;
+      memcpy(&nc, cons + pos, 4);
+      pos += 4;
+      if (nc > (cons_len - pos) / 36) return STARK_ERR_BAD_ARG;
+      fac_rec[3 * (size_t)ci + f] = (uint32_t)pos;
+      fac_cnt[3 * (size_t)ci + f] = nc;
+      pos += (size_t)nc * 36;
+      if (nc > n_coeff) n_coeff = nc;
+    }
+    b += n_coeff;
+    if (b > 0xFFFFFFFFull / 3) return STARK_ERR_BAD_LENGTH;
+    base[ci + 1] = (uint32_t)b;
+  }
+  return STARK_OK;
+}
 
 }  // namespace
 
@@ -163,33 +219,9 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   // Host walk: record counts only (the records themselves are read on the GPU).
   const uint8_t* cons = r1cs + hd.cons_off;
   const size_t cons_len = r1cs_len - hd.cons_off;
-  if (cons_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
-  std::vector<uint32_t> fac((size_t)6 * n_c + 1);  // fac_rec[3 n_c] | fac_cnt[3 n_c] | pad
-  std::vector<uint32_t> base((size_t)n_c + 1);
-  uint32_t* fac_rec = fac.data();
-  uint32_t* fac_cnt = fac.data() + (size_t)3 * n_c;
-  {
-    size_t pos = 0;
-    uint64_t b = 0;
-    base[0] = 0;
-    for (uint32_t ci = 0; ci < n_c; ++ci) {
-      uint32_t n_coeff = 0;
-      for (int f = 0; f < 3; ++f) {
-        if (cons_len - pos < 4) return STARK_ERR_BAD_ARG;
-        uint32_t nc;
-        memcpy(&nc, cons + pos, 4);
-        pos += 4;
-        if (nc > (cons_len - pos) / 36) return STARK_ERR_BAD_ARG;
-        fac_rec[3 * (size_t)ci + f] = (uint32_t)pos;
-        fac_cnt[3 * (size_t)ci + f] = nc;
-        pos += (size_t)nc * 36;
-        if (nc > n_coeff) n_coeff = nc;
-      }
-      b += n_coeff;
-      if (b > 0xFFFFFFFFull / 3) return STARK_ERR_BAD_LENGTH;
-      base[ci + 1] = (uint32_t)b;
-    }
-  }
+  std::vector<uint32_t> fac, base;
+  st = walk_records(cons, cons_len, n_c, fac, base);
+  if (st != STARK_OK) return st;
   const uint64_t a_len = base[n_c];
   const uint64_t os = 3 * a_len;
   if (a_len == 0) return STARK_ERR_BAD_ARG;
@@ -249,6 +281,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   fa.comp = (fe*)(A + o_comp);
   fa.keys = (uint32_t*)(A + o_k);
   fa.vals = (uint32_t*)(A + o_v);
+  fa.slot_wire = nullptr;
   fa.err = err;
   hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa);
   uint8_t* flags = A + o_flags;
@@ -294,6 +327,190 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   return STARK_OK;
 }
 
+// ---- prepared circuits --------------------------------------------------------
+//
+// Everything of a proof that depends on the .r1cs alone, built once: the slot
+// layout (and each slot's wire), the coefficient and flag columns, the
+// permutation, the public wires' first uses, and the LDEs of K, F0, F1, F2, IDX
+// and PIDX.  A proof for a new witness then builds S and P (wit_fill_kernel) and
+// extends only S, P and A: 3 of the 9 LDE columns.
+struct PreparedCircuit {
+  DevBuf arena, lde;
+  size_t os = 0, n_wires = 0, n_public = 0;
+  uint32_t n_c = 0;
+  uint64_t a_len = 0;
+  std::vector<size_t> pfi;
+  const uint32_t* base = nullptr;
+  const fe* coef = nullptr;
+  const uint8_t* flags = nullptr;
+  const uint64_t* perm = nullptr;
+  const uint32_t* slot_wire = nullptr;
+};
+
+static stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c) {
+  R1csHeader hd;
+  stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
+  if (st != STARK_OK) return st;
+  const uint32_t n_c = hd.n_constraints, n_wires = hd.n_wires;
+  const size_t n_public = 1 + (size_t)hd.n_pub_in + hd.n_pub_out;  // run.rs:359-360
+  if (n_wires == 0 || n_public > n_wires) return STARK_ERR_BAD_ARG;
+  const uint8_t* cons = r1cs + hd.cons_off;
+  const size_t cons_len = r1cs_len - hd.cons_off;
+  std::vector<uint32_t> fac, base;
+  st = walk_records(cons, cons_len, n_c, fac, base);
+  if (st != STARK_OK) return st;
+  const uint64_t a_len = base[n_c];
+  const uint64_t os = 3 * a_len;
+  if (a_len == 0) return STARK_ERR_BAD_ARG;
+  uint32_t key_bits = 1;
+  while (key_bits < 32 && (1ull << key_bits) < n_wires) ++key_bits;
+  hipStream_t s = ctx->stream;
+  size_t sort_tmp = 0;
+  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
+                                                   (int)key_bits, s));
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  // Kept: base, coef, flags, perm, slot wires.  Scratch (the circuit's own arena, so a
+  // prepared circuit never aliases the context's trace arena): records, sort buffers.
+  const size_t o_base = take(base.size() * 4), o_coef = take(os * 32), o_flags = take(3 * os),
+               o_perm = take(os * 8), o_sw = take(os * 4), o_cons = take(cons_len), o_fac = take(fac.size() * 4),
+               o_k = take(os * 4), o_v = take(os * 4), o_k2 = take(os * 4), o_v2 = take(os * 4),
+               o_last = take((size_t)n_wires * 4), o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp);
+  st = ensure_buf(ctx, c.arena, off);
+  if (st != STARK_OK) return st;
+  uint8_t* A = (uint8_t*)c.arena.ptr;
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_cons, cons, cons_len, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac.data(), fac.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base.data(), base.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
+  STARK_HIP(ctx, hipMemsetAsync(A + o_pf, 0xFF, n_public * 8, s));
+  FillArgs fa;
+  fa.cons = A + o_cons;
+  fa.fac_rec = (const uint32_t*)(A + o_fac);
+  fa.fac_cnt = (const uint32_t*)(A + o_fac) + (size_t)3 * n_c;
+  fa.base = (const uint32_t*)(A + o_base);
+  fa.n_constraints = n_c;
+  fa.n_wires = n_wires;
+  fa.a_len = a_len;
+  fa.wcan = nullptr;
+  fa.wmont = nullptr;  // circuit columns only
+  fa.coef = (fe*)(A + o_coef);
+  fa.wit = nullptr;
+  fa.comp = nullptr;
+  fa.keys = (uint32_t*)(A + o_k);
+  fa.vals = (uint32_t*)(A + o_v);
+  fa.slot_wire = (uint32_t*)(A + o_sw);
+  fa.err = (uint32_t*)(A + o_err);
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa);
+  uint8_t* flags = A + o_flags;
+  STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));
+  STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
+  hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
+                     flags + os, flags + 2 * os);
+  STARK_HIP(ctx, hipGetLastError());
+  size_t tmp_bytes = sort_tmp;
+  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
+                                                   (uint32_t*)(A + o_k2), (const uint32_t*)(A + o_v),
+                                                   (uint32_t*)(A + o_v2), (int)os, 0, (int)key_bits, s));
+  hipLaunchKernelGGL(group_last_kernel, dim3(blocks(os)), dim3(256), 0, s, (const uint32_t*)(A + o_k2), os,
+                     (uint32_t*)(A + o_last));
+  hipLaunchKernelGGL(perm_kernel, dim3(blocks(os)), dim3(256), 0, s, (const uint32_t*)(A + o_k2),
+                     (const uint32_t*)(A + o_v2), os, (const uint32_t*)(A + o_last), (uint32_t)n_public,
+                     (uint64_t*)(A + o_perm), (uint64_t*)(A + o_pf));
+  STARK_HIP(ctx, hipGetLastError());
+  std::vector<uint64_t> pf(n_public);
+  uint32_t h_err = 0;
+  STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipMemcpyAsync(&h_err, A + o_err, 4, hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  if (h_err) return STARK_ERR_BAD_ARG;
+  c.pfi.clear();
+  for (size_t wi = 0; wi < n_public; ++wi)
+    if (pf[wi] != ~0ull) {
+      c.pfi.push_back(wi);
+      c.pfi.push_back((size_t)pf[wi]);
+    }
+  c.os = os;
+  c.n_c = n_c;
+  c.n_wires = n_wires;
+  c.n_public = n_public;
+  c.a_len = a_len;
+  c.base = (const uint32_t*)(A + o_base);
+  c.coef = (const fe*)(A + o_coef);
+  c.flags = flags;
+  c.perm = (const uint64_t*)(A + o_perm);
+  c.slot_wire = (const uint32_t*)(A + o_sw);
+  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.lde, s);
+}
+
+// The witness of one proof: decode, then S and P from the circuit's slot wires.
+static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, const uint8_t* wtns, size_t wtns_len,
+                                    DevTrace* out) {
+  const FieldHost& F = FieldHost::get();
+  WtnsHeader wh;
+  stark_status st = parse_wtns_header(wtns, wtns_len, &wh);
+  if (st != STARK_OK) return st;
+  const uint32_t n_wit = wh.n_wit;
+  if (n_wit < c.n_wires || c.n_public > n_wit) return STARK_ERR_BAD_ARG;
+  const uint8_t* wv = wtns + wh.values_off;
+  {
+    const HostFp w0 = F.reduce_bytes_le(wv, wh.field_size);  // witness[0] == 1 (run.rs:358)
+    if (!(w0.v[0] == 1 && w0.v[1] == 0 && w0.v[2] == 0 && w0.v[3] == 0)) return STARK_ERR_BAD_ARG;
+  }
+  out->public_wires.resize(4 * c.n_public);
+  for (size_t i = 0; i < c.n_public; ++i) {
+    const HostFp v = F.reduce_bytes_le(wv + i * wh.field_size, wh.field_size);
+    memcpy(&out->public_wires[4 * i], v.v, 32);
+  }
+  const size_t wbytes = (size_t)n_wit * wh.field_size;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  };
+  const size_t o_w = take(wbytes), o_wcan = take((size_t)n_wit * 32), o_wmont = take((size_t)n_wit * 32),
+               o_wit = take(c.os * 32), o_comp = take(c.os * 32);
+  st = ensure_buf(ctx, ctx->trace_arena, off);
+  if (st != STARK_OK) return st;
+  uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
+  hipStream_t s = ctx->stream;
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_w, wv, wbytes, hipMemcpyHostToDevice, s));
+  uint64_t one_r[4];
+  memcpy(one_r, F.one().v, 32);
+  hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
+                     wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), (fe*)(A + o_wcan),
+                     (fe*)(A + o_wmont));
+  hipLaunchKernelGGL(wit_fill_kernel, dim3(blocks(3 * (uint64_t)c.n_c)), dim3(256), 0, s, c.base, c.n_c, c.a_len,
+                     c.slot_wire, c.coef, (const fe*)(A + o_wcan), (const fe*)(A + o_wmont), (fe*)(A + o_wit),
+                     (fe*)(A + o_comp));
+  STARK_HIP(ctx, hipGetLastError());
+  out->os = c.os;
+  out->n_constraints = c.n_c;
+  out->n_wires = c.n_wires;
+  out->wit = (fe*)(A + o_wit);
+  out->comp = (fe*)(A + o_comp);
+  out->public_first_indices = c.pfi;
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+struct stark_r1cs_circuit {
+  stark_ctx* ctx = nullptr;
+  stark::PreparedCircuit c;
+  ~stark_r1cs_circuit() {
+    if (c.arena.ptr) hipFree(c.arena.ptr);
+    if (c.lde.ptr) hipFree(c.lde.ptr);
+  }
+};
+
+namespace stark {
 }  // namespace stark
 
 using namespace stark;
@@ -313,6 +530,36 @@ stark_status stark_prove_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t 
                                    dt.public_first_indices.data(), dt.public_first_indices.size() / 2,
                                    (const size_t*)dt.perm, (const uint64_t*)dt.coef, dt.flags, dt.n_constraints,
                                    dt.n_wires, out);
+}
+
+
+stark_status stark_r1cs_circuit_new(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, stark_r1cs_circuit** out) {
+  if (!ctx || !r1cs || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  auto h = std::make_unique<stark_r1cs_circuit>();
+  h->ctx = ctx;
+  const stark_status st = circuit_build(ctx, r1cs, r1cs_len, h->c);
+  hipStreamSynchronize(ctx->stream);
+  if (st != STARK_OK) return st;
+  *out = h.release();
+  return STARK_OK;
+}
+
+void stark_r1cs_circuit_free(stark_r1cs_circuit* c) { delete c; }
+
+stark_status stark_prove_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit, const uint8_t* wtns,
+                                      size_t wtns_len, stark_r1cs_proof** out) {
+  if (!ctx || !circuit || !wtns || !out || circuit->ctx != ctx) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const PreparedCircuit& c = circuit->c;
+  DevTrace dt;
+  const stark_status st = circuit_witness(ctx, c, wtns, wtns_len, &dt);
+  if (st != STARK_OK) return st;
+  return mk_r1cs_proof_prepared(ctx, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, c.os, dt.public_wires.data(),
+                                dt.public_wires.size() / 4, c.pfi.data(), c.pfi.size() / 2, (const size_t*)c.perm,
+                                (const uint64_t*)c.coef, c.flags, c.n_c, c.n_wires, (const fe*)c.lde.ptr, out);
 }
 
 }  // extern "C"

@@ -4,6 +4,7 @@
     R1csTrace.build(r1cs, wtns)        read_r1cs + read_witness + run.rs:310-437
     prove_with_witness(ctx, r1cs, wtns)   run.rs:310-452
     prove_with_file_path(ctx, ...)     run.rs:528-554 (writes the proof JSON)
+    R1csCircuit(ctx, r1cs).prove(wtns) the same proofs, circuit-only work done once
     StarkProof                         utils.rs:122-130 (serde_json text + roots)
 
 Everything runs in libstark_hip.so; there is no CPU fallback.
@@ -131,6 +132,31 @@ def prove_with_witness_host_trace(ctx: Context, r1cs: bytes, wtns: bytes) -> Sta
     h = _vp()
     ctx.check(ctx.lib.stark_prove_r1cs_trace(ctx.h, tr.h, ctypes.byref(h)), "prove_with_witness")
     return StarkProof(ctx.lib, h)
+
+
+class R1csCircuit:
+    """A circuit prepared once for many proofs (stark_r1cs_circuit_new): everything of
+    prove_with_witness (run.rs:310-452) that depends on the .r1cs alone, including the
+    LDEs of K, F0-F2, IDX and PIDX, stays in HBM; prove(wtns) extends only S, P and A.
+    The proofs equal prove_with_witness(ctx, r1cs, wtns)."""
+
+    def __init__(self, ctx: Context, r1cs: bytes):
+        self.ctx = ctx
+        self.h = _vp()
+        ctx.check(ctx.lib.stark_r1cs_circuit_new(ctx.h, r1cs, len(r1cs), ctypes.byref(self.h)), "r1cs_circuit_new")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.ctx.lib.stark_r1cs_circuit_free(self.h)
+        except Exception:
+            pass
+
+    def prove(self, wtns: bytes) -> StarkProof:
+        h = _vp()
+        self.ctx.check(self.ctx.lib.stark_prove_r1cs_circuit(self.ctx.h, self.h, wtns, len(wtns), ctypes.byref(h)),
+                       "prove_r1cs_circuit")
+        return StarkProof(self.ctx.lib, h)
 
 
 def prove_with_file_path(ctx: Context, r1cs_file_path: str, witness_file_path: str, proof_json_path: str) -> None:

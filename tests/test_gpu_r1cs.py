@@ -156,3 +156,46 @@ def test_device_trace_rejects_bad_inputs(ctx):
     badw[wval] ^= 2
     with pytest.raises(StarkError):
         prove_with_witness(ctx, bytes(r1), bytes(badw))
+
+
+@pytest.mark.parametrize("name", list(GOLDEN))
+def test_prepared_circuit_matches_golden(ctx, name):
+    """R1csCircuit (circuit-only work and LDE columns prepared once) gives the golden proof, twice."""
+    from stark_amd.r1cs import R1csCircuit
+    c = R1csCircuit(ctx, _read(name, "r1cs"))
+    wt = _read(name, "wtns")
+    for _ in range(2):
+        assert hashlib.sha256(c.prove(wt).to_json().encode()).hexdigest() == GOLDEN[name]["json_sha256"]
+
+
+def test_prepared_circuit_new_witnesses(ctx):
+    """One prepared synthetic circuit, three witnesses: each proof equals prove_with_witness's."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    import synth_r1cs
+    from stark_amd.r1cs import R1csCircuit, prove_with_witness
+    r1, _ = synth_r1cs.for_steps(14)
+    c = R1csCircuit(ctx, r1)
+    for inputs in [(11, 22), (3, 5), (R.P - 1, 7)]:
+        r1b, wt = synth_r1cs.for_steps(14, inputs=inputs)
+        assert r1b == r1
+        assert c.prove(wt).to_json() == prove_with_witness(ctx, r1, wt).to_json()
+
+
+def test_prepared_circuit_rejects_bad_inputs(ctx):
+    """A witness for a different circuit size, a first value other than 1 and an unsatisfying witness."""
+    from stark_amd import StarkError
+    from stark_amd.r1cs import R1csCircuit
+    c = R1csCircuit(ctx, _read("pedersen_test", "r1cs"))
+    with pytest.raises(StarkError):
+        c.prove(_read("compute", "wtns"))          # fewer witness values than the circuit's wires
+    wt = bytearray(_read("pedersen_test", "wtns"))
+    bad = bytearray(wt)
+    bad[-32 * 1997] ^= 1                                # witness[0] != 1 (n_wit = 1997 for pedersen_test)
+    with pytest.raises(StarkError):
+        c.prove(bytes(bad))
+    bad = bytearray(wt)
+    bad[-32 * 100] ^= 1                                 # some wire value: constraints fail
+    with pytest.raises(StarkError) as e:
+        c.prove(bytes(bad))
+    assert e.value.code == 8

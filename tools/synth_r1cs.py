@@ -24,8 +24,9 @@ def _fe(x: int) -> bytes:
     return (x % P).to_bytes(32, "little")
 
 
-def synth(n_constraints: int, seed: int = 1):
-    """Returns (r1cs_bytes, wtns_bytes)."""
+def synth(n_constraints: int, seed: int = 1, inputs=None):
+    """Returns (r1cs_bytes, wtns_bytes).  inputs = (public output, public input) overrides
+    the seeded ones: the same circuit (identical .r1cs) with another witness."""
     import random
     rnd = random.Random(seed)
     n_chain = n_constraints - 1
@@ -48,6 +49,9 @@ def synth(n_constraints: int, seed: int = 1):
     # choose the public output as the final chain value; constraints reference it, so compute forward
     # with w[1] unknown: solve sequentially treating w[1] as fixed random public output.
     w[1] = rnd.randrange(P)
+    if inputs is not None:
+        w[1], w[2] = inputs[0] % P, inputs[1] % P
+        w[3] = w[2]
     out = []
     for (cur, a, p1), (_, b, p2), (nxt, c), _, _ in cons:
         av = (w[cur] + a * w[p1] + 1) % P
@@ -80,8 +84,8 @@ def synth(n_constraints: int, seed: int = 1):
     return bytes(r1cs), bytes(wt)
 
 
-def for_steps(log_steps: int, seed: int = 1):
+def for_steps(log_steps: int, seed: int = 1, inputs=None):
     """A circuit whose padded trace length is 2^log_steps (original_steps = 9 n_constraints)."""
     target = 1 << log_steps
     n = (target // 2) // 9 + 1            # original_steps in (2^(k-1), 2^k]
-    return synth(n, seed)
+    return synth(n, seed, inputs)
