@@ -199,9 +199,10 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
                                size_t wtns_len, DevTrace* out);
 // mk_r1cs_proof on trace columns given as host or device pointers, flags as
 // bytes (r1cs.hip).
-// The witness-independent LDE columns K F0 F1 F2 IDX PIDX of a circuit (6 x precision).
+// The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the
+// inverses of Zb2, Zb3 (8 x precision).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
-                         DevBuf& out, hipStream_t s);
+                         const size_t* public_first_indices, size_t n_pfi, DevBuf& out, hipStream_t s);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                     size_t os, const uint64_t* public_wires, size_t n_public,

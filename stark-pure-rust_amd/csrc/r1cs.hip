@@ -530,8 +530,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
                                const uint64_t* flag2, const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
                                stark_r1cs_proof** out, const fe* pre = nullptr) {
-  // pre != nullptr: the circuit's LDE columns K F0 F1 F2 IDX PIDX (precision each), prepared
-  // once per circuit (stark_r1cs_circuit_new); only S, P and A are extended here.
+  // pre != nullptr: the circuit's LDE columns K F0 F1 F2 IDX PIDX (precision each) and the
+  // inverses of Zb2, Zb3 (2 x precision), prepared once per circuit (stark_r1cs_circuit_new);
+  // only S, P and A are extended here.
   PhaseClock clk("mk_r1cs_proof");
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
@@ -673,10 +674,13 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(lde(ctx, raw, 1, cols + 8 * prec, log_steps, log_prec, *tw1i, *tw2, s));
 
-  hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
-                     (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one, zb, zb + prec);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * prec, s));
+  if (!pre) {  // prepared circuits carry these (they depend on the public wires' positions only)
+    hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
+                       (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
+                       zb, zb + prec);
+    STARK_HIP(ctx, hipGetLastError());
+    STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * prec, s));
+  }
 
   // Constraint kernel.
   ConstraintArgs ca;
@@ -686,7 +690,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     ca.col[6] = pre + 4 * prec;
     ca.col[7] = pre + 5 * prec;
   }
-  ca.inv_zb = inv_zb;
+  ca.inv_zb = pre ? pre + 6 * prec : inv_zb;
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
   ca.lo = tw2->d_lo;
@@ -818,7 +822,7 @@ __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, 
 // (prove.rs:100-124, 160-167), 6 x precision into `out`.  coef / flag bytes / perm
 // are the device trace builder's circuit columns (os slots).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
-                         DevBuf& out, hipStream_t s) {
+                         const size_t* public_first_indices, size_t n_pfi, DevBuf& out, hipStream_t s) {
   const FieldHost& F = FieldHost::get();
   if (os < 5 || os % 3 != 0) return STARK_ERR_BAD_LENGTH;
   const uint32_t log_steps = log2_ceil_ref(os - 1);
@@ -837,9 +841,11 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
   const Twiddles *tw2 = nullptr, *tw1i = nullptr;
   STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
   STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
-  DevBuf tmp;
-  STARK_TRY(ensure_buf(ctx, tmp, 6 * steps * sizeof(fe)));
-  stark_status st = ensure_buf(ctx, out, 6 * prec * sizeof(fe));
+  for (size_t i = 0; i < n_pfi; ++i)
+    if (public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
+  DevBuf tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 precision + n_pfi)
+  STARK_TRY(ensure_buf(ctx, tmp, (6 * steps + 2 * prec + n_pfi + 1) * sizeof(fe)));
+  stark_status st = ensure_buf(ctx, out, 8 * prec * sizeof(fe));
   if (st == STARK_OK) {
     fe* raw = (fe*)tmp.ptr;
     hipMemsetAsync(raw, 0, 6 * steps * sizeof(fe), s);
@@ -849,6 +855,22 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
     st = lde(ctx, raw, 6, (fe*)out.ptr, log_steps, log_prec, *tw1i, *tw2, s);
+    // Zb2 = prod_k (x - x_k), Zb3 = x - x_last (utils.rs:438-474) and their inverses (0 -> 0).
+    const uint64_t skips = prec / steps;
+    std::vector<fe> xk(n_pfi + 1);
+    for (size_t i = 0; i < n_pfi; ++i) xk[i] = to_dev(F.pow_u64(g2, skips * public_first_indices[2 * i + 1]));
+    fe* zb = raw + 6 * steps;
+    fe* d_xk = zb + 2 * prec;
+    const Mont mc = mont();
+    if (st == STARK_OK && n_pfi &&
+        hipMemcpyAsync(d_xk, xk.data(), n_pfi * sizeof(fe), hipMemcpyHostToDevice, s) != hipSuccess)
+      st = STARK_ERR_HIP;
+    if (st == STARK_OK) {
+      hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
+                         (uint64_t)0, (uint32_t)0, (const fe*)d_xk, (uint32_t)n_pfi,
+                         to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + prec);
+      st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * prec, 2 * prec, s);
+    }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
   }
   hipStreamSynchronize(s);
