@@ -99,6 +99,7 @@ struct FriPending {
   uint32_t excl = 0;
   std::vector<size_t> qs;
   const fe* last_dev = nullptr;  // the last layer's values (device)
+  std::vector<stark_merkle_tree*> trees;  // trees[l] commits layer l's values
   const uint8_t* h_roots = nullptr;  // pinned: roots of trees[0..layers]
 };
 
@@ -109,7 +110,7 @@ struct FriPending {
 void FriPendingDeleter::operator()(FriPending* p) const { delete p; }
 
 stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
-                         uint32_t excl, FriPendingPtr* out) {
+                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0) {
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
   FriPendingPtr p(new FriPending());
@@ -164,7 +165,11 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
     if (st != STARK_OK) return st;
     ctx->fri_trees.push_back(t);
   }
-  std::vector<stark_merkle_tree*>& trees = ctx->fri_trees;  // trees[l] commits layer l's values
+  // trees[l] commits layer l's values; tree0, when given, is the caller's tree of d_values (the
+  // prover's L tree: the same leaves, so layer 0's tree is not built twice).
+  p->trees.assign(ctx->fri_trees.begin(), ctx->fri_trees.begin() + layers + 1);
+  if (tree0) p->trees[0] = tree0;
+  std::vector<stark_merkle_tree*>& trees = p->trees;
 
   const fe* cur = d_values;
   fe* next = (fe*)ctx->fri_cols.ptr;
@@ -173,7 +178,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   const HostFp inv4 = F.inv(F.from_u64(4));
   const fe r2 = to_dev(F.from_canonical(F.one().v));  // Montgomery image of R
   for (size_t layer = 0; layer < layers; ++layer) {
-    if (layer == 0) {
+    if (layer == 0 && !tree0) {
       st = merkle_build(ctx, trees[0], (const uint8_t*)cur, m, 32, s);
       if (st != STARK_OK) return st;
     }
@@ -215,7 +220,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
 stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out) {
   hipStream_t s = ctx->stream;
   STARK_HIP(ctx, hipStreamSynchronize(s));
-  std::vector<stark_merkle_tree*>& trees = ctx->fri_trees;
+  std::vector<stark_merkle_tree*>& trees = p->trees;
   stark_fri_proof* proof = p->proof.get();
   proof->layers.resize(p->layers);
   std::vector<GatherReq> reqs = extra;

@@ -226,7 +226,7 @@ struct FriPendingDeleter {
 };
 using FriPendingPtr = std::unique_ptr<FriPending, FriPendingDeleter>;
 stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
-                         uint32_t excl, FriPendingPtr* out);
+                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0 = nullptr);
 stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out);
 stark_status fri_prove_device(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
                               size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out);

@@ -754,7 +754,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367), enqueued behind the rest.
   FriPendingPtr fri_pending;
   clk.mark("prover kernels enqueued");
-  STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending));
+  STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending, l_tree));
   clk.mark("FRI kernels enqueued");
   STARK_HIP(ctx, hipStreamSynchronize(s));  // the proof's one wait for the device
   clk.mark("device wait");
