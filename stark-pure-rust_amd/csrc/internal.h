@@ -200,7 +200,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // mk_r1cs_proof on trace columns given as host or device pointers, flags as
 // bytes (r1cs.hip).
 // The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the
-// inverses of Zb2, Zb3 (8 x precision).
+// inverses of Zb2, Zb3 (8 x precision; K, F0-F2 and the inverses as Montgomery images).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, DevBuf& out, hipStream_t s);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).

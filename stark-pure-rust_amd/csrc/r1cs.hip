@@ -84,6 +84,7 @@ struct Transcript {
   fe r1_m;     // Montgomery r[1], r[2]
   fe r2_m;
   fe k_m[11];  // Montgomery k[0..10]
+  fe kx_m[8][3];  // Montgomery k3 + k4 xs_t, k5 + k6 xs_t, k7 + k8 xs_t (t = i mod 8)
   uint32_t roots[3][8];  // a_root, m_root, l_root (LE words = the digest bytes)
   int err;
 };
@@ -133,25 +134,41 @@ __global__ void r1cs_r_kernel(const uint32_t* __restrict__ a_root, uint32_t prec
   for (int i = 0; i < 8; ++i) tr->roots[0][i] = a_root[i];
 }
 
+// (g2^steps)^t, t < 8: the x^steps factor of L at the points i = t mod 8 (prove.rs:287-291).
+struct XsPowers {
+  fe v[8];
+};
+
 // k_0 = 1, k_i = from_str(mk_seed([m_root, [i]])) = BE integer of
-// Blake2s(m_root || i) mod p (prove.rs:274-283, utils.rs:25-27, 51-57).
-__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, Transcript* __restrict__ tr) {
+// Blake2s(m_root || i) mod p (prove.rs:274-283, utils.rs:25-27, 51-57); then the
+// three per-residue coefficients of L, kx[t] = (k3 + k4 xs_t, k5 + k6 xs_t,
+// k7 + k8 xs_t), so the L kernel needs 8 products per point instead of 14.
+__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, XsPowers xs,
+                              Transcript* __restrict__ tr) {
+  __shared__ fe ks[11];
   const uint32_t i = threadIdx.x;
-  if (i > 10) return;
   if (i == 0) {
+    ks[0] = one_m;
     tr->k_m[0] = one_m;
 #pragma unroll
     for (int j = 0; j < 8; ++j) tr->roots[1][j] = m_root[j];
-    return;
+  } else if (i <= 10) {
+    uint32_t h[8];
+    b2s_short(m_root, i, 33, h);
+    fe k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k.w[j] = bswap32(h[7 - j]);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) fe_reduce_once(k);
+    ks[i] = fe_mul(k, r2);
+    tr->k_m[i] = ks[i];
   }
-  uint32_t h[8];
-  b2s_short(m_root, i, 33, h);
-  fe k;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) k.w[j] = bswap32(h[7 - j]);
-#pragma unroll
-  for (int t = 0; t < 5; ++t) fe_reduce_once(k);
-  tr->k_m[i] = fe_mul(k, r2);
+  __syncthreads();
+  if (i < 8) {
+    tr->kx_m[i][0] = fe_add(ks[3], fe_mul(ks[4], xs.v[i]));
+    tr->kx_m[i][1] = fe_add(ks[5], fe_mul(ks[6], xs.v[i]));
+    tr->kx_m[i][2] = fe_add(ks[7], fe_mul(ks[8], xs.v[i]));
+  }
 }
 
 __global__ void r1cs_l_root_kernel(const uint32_t* __restrict__ l_root, Transcript* __restrict__ tr) {
@@ -328,7 +345,11 @@ struct ConstraintArgs {
   uint32_t log_prec, kb, n2, n3;
   const Transcript* tr;  // r0, r1, r2 (device transcript)
   fe mr2;
-  fe invz_m[8];          // Montgomery inv(w8^t - 1), 0 for t = 0 (multi_inv of Z, prove.rs:203)
+  // inv(Z) at the points t = i mod 8 (multi_inv of Z, prove.rs:203; 0 for t = 0) as the
+  // Montgomery images of inv(Z) R^k, k = 0, 1, 2: the constraint kernel forms some Q's scaled by
+  // R^-k (one product fewer per conversion it skips) and undoes the scale in D = Q inv(Z).
+  fe invz_m[3][8];
+  int mont_cols;         // K, F0-F2 and inv Zb2/Zb3 are Montgomery images (prepared circuits)
 };
 
 // Q1/Q2/Q3 (utils.rs:181-248, 344-376) -> D1..D3 (utils.rs:379-418), I2/I3
@@ -353,22 +374,30 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe p = fe_load(Pc + i), s = fe_load(S + i), av = fe_load(A + i);
   const fe p_prev = fe_load(Pc + prev), a_prev = fe_load(A + prev);
   const fe p2 = fe_load(Pc + ((i + a.shift1) & mask)), p3 = fe_load(Pc + ((i + a.shift2) & mask));
-  // Data x data products: one operand to Montgomery form first.
-  const fe s_m = fe_mul(s, a.mr2);
-  const fe q1 = fe_mul(fe_mul(fe_load(F0 + i), a.mr2),
-                       fe_sub(fe_sub(p, fe_mul(fe_mul(fe_load(F1 + i), a.mr2), p_prev)), fe_mul(fe_load(K + i), s_m)));
-  const fe q2 = fe_mul(fe_mul(fe_load(F2 + i), a.mr2), fe_sub(p3, fe_mul(fe_mul(p, a.mr2), p2)));
+  // Data x data products: a Montgomery product of two canonical values is x y R^-1, so each Q is
+  // formed at a scale R^-k and D = Q inv(Z) takes the inv(Z) R^k constant (zero tests are
+  // scale-free).  Prepared circuits hold K, F0-F2 as Montgomery images: their products are exact.
+  const bool mc = a.mont_cols != 0;
+  fe unit = fe_zero();
+  unit.w[0] = 1;                                  // canonical 1: fe_mul(x, unit) = x R^-1
+  const fe k_s = fe_mul(fe_load(K + i), s), f1_p = fe_mul(fe_load(F1 + i), p_prev);
+  const fe q1 = fe_mul(fe_load(F0 + i), fe_sub(fe_sub(mc ? p : fe_mul(p, unit), f1_p), k_s));  // R^-(mc ? 0 : 2)
+  const fe q2 = fe_mul(fe_load(F2 + i), fe_sub(fe_mul(p3, unit), fe_mul(p, p2)));            // R^-(mc ? 1 : 2)
   const fe rs = fe_mul(s, r2_m);
   const fe nmr = fe_add(fe_add(r0, fe_mul(fe_load(IDX + i), r1_m)), rs);
   const fe dnm = fe_add(fe_add(r0, fe_mul(fe_load(PIDX + i), r1_m)), rs);
-  const fe q3 = fe_sub(fe_mul(fe_mul(av, a.mr2), dnm), fe_mul(fe_mul(a_prev, a.mr2), nmr));
+  const fe q3 = fe_sub(fe_mul(av, dnm), fe_mul(a_prev, nmr));                                // R^-1
   const uint32_t t = (uint32_t)(gi & 7);
-  fe iz = a.invz_m[0];
+  fe iz0 = a.invz_m[0][0], iz1 = a.invz_m[1][0], iz2 = a.invz_m[2][0];
 #pragma unroll
   for (uint32_t k = 1; k < 8; ++k)
-    if (t == k) iz = a.invz_m[k];
+    if (t == k) {
+      iz0 = a.invz_m[0][k];
+      iz1 = a.invz_m[1][k];
+      iz2 = a.invz_m[2][k];
+    }
   if (t == 0 && !(fe_is_zero(q1) && fe_is_zero(q2) && fe_is_zero(q3))) atomicOr(a.err, 1);
-  const fe d1 = fe_mul(q1, iz), d2 = fe_mul(q2, iz), d3 = fe_mul(q3, iz);
+  const fe d1 = fe_mul(q1, mc ? iz0 : iz2), d2 = fe_mul(q2, mc ? iz1 : iz2), d3 = fe_mul(q3, iz1);
   // I2 / I3 at x = g2^i (Horner; the interpolants are canonical).
   const fe x_m = pow_tab(a.lo, a.hi, a.kb, gi);
   fe i2 = fe_zero();
@@ -379,7 +408,8 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe e2 = fe_sub(s, i2), e3 = fe_sub(av, i3);
   if (fe_is_zero(izb2) && !fe_is_zero(e2)) atomicOr(a.err, 2);
   if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
-  const fe b2 = fe_mul(fe_mul(e2, a.mr2), izb2), b3 = fe_mul(fe_mul(e3, a.mr2), izb3);
+  const fe b2 = mc ? fe_mul(e2, izb2) : fe_mul(fe_mul(e2, a.mr2), izb2);
+  const fe b3 = mc ? fe_mul(e3, izb3) : fe_mul(fe_mul(e3, a.mr2), izb3);
   fe* row = a.rows + 8 * i;
   fe_store(row + 0, p);
   fe_store(row + 1, av);
@@ -397,8 +427,7 @@ struct LincombArgs {
   uint64_t prec;
   uint64_t g_add;        // local point i is global point g_add + (i << log_g)
   uint32_t log_g;
-  const Transcript* tr;  // k (device transcript)
-  fe xs_m[8];  // (g2^steps)^t, t = i mod 8 (prove.rs:287-291)
+  const Transcript* tr;  // k and kx (device transcript)
 };
 
 // L = k0 D1 + k1 D2 + k2 D3 + k3 P + k4 P x^steps + k5 B2 + k6 B2 x^steps +
@@ -411,26 +440,38 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
   const fe p = fe_load(row + 0), av = fe_load(row + 1), s = fe_load(row + 2), d1 = fe_load(row + 3),
            d2 = fe_load(row + 4), d3 = fe_load(row + 5), b2 = fe_load(row + 6), b3 = fe_load(row + 7);
   const uint32_t t = (uint32_t)(gi & 7);
-  fe xs = a.xs_m[0];
-#pragma unroll
-  for (uint32_t k = 1; k < 8; ++k)
-    if (t == k) xs = a.xs_m[k];
   const fe* k_m = a.tr->k_m;
+  const fe* kx = a.tr->kx_m[t];
   fe acc = fe_mul(d1, k_m[0]);
   acc = fe_add(acc, fe_mul(d2, k_m[1]));
   acc = fe_add(acc, fe_mul(d3, k_m[2]));
-  acc = fe_add(acc, fe_mul(p, k_m[3]));
-  acc = fe_add(acc, fe_mul(fe_mul(p, k_m[4]), xs));
-  acc = fe_add(acc, fe_mul(b2, k_m[5]));
-  acc = fe_add(acc, fe_mul(fe_mul(b2, k_m[6]), xs));
-  acc = fe_add(acc, fe_mul(b3, k_m[7]));
-  acc = fe_add(acc, fe_mul(fe_mul(b3, k_m[8]), xs));
+  acc = fe_add(acc, fe_mul(p, kx[0]));    // (k3 + k4 x^steps) P
+  acc = fe_add(acc, fe_mul(b2, kx[1]));   // (k5 + k6 x^steps) B2
+  acc = fe_add(acc, fe_mul(b3, kx[2]));   // (k7 + k8 x^steps) B3
   acc = fe_add(acc, fe_mul(av, k_m[9]));
   acc = fe_add(acc, fe_mul(s, k_m[10]));
   fe_store(a.out + i, acc);
 }
 
 // ---- host helpers -----------------------------------------------------------
+
+// Z(g2^i) = (g2^steps)^(i mod 8) - 1; its inverse with 0 -> 0 (prove.rs:128-129, 203), times
+// R^k for the kernel's R^-k-scaled Q's.
+static void set_inv_z(ConstraintArgs& ca, const HostFp& g2, uint64_t steps) {
+  const FieldHost& F = FieldHost::get();
+  const HostFp rv = F.from_canonical(F.one().v);  // the field element R = 2^256 mod p
+  const HostFp w8 = F.pow_u64(g2, steps);
+  HostFp wt = F.one();
+  for (int t = 0; t < 8; ++t) {
+    const HostFp z = F.sub(wt, F.one());
+    HostFp iz = FieldHost::eq(z, F.zero()) ? F.zero() : F.inv(z);
+    for (int k = 0; k < 3; ++k) {
+      ca.invz_m[k][t] = to_dev(iz);
+      iz = F.mul(iz, rv);
+    }
+    wt = F.mul(wt, w8);
+  }
+}
 
 // log2_ceil, utils.rs:14-23.
 static uint32_t log2_ceil_ref(size_t v) {
@@ -709,23 +750,24 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.n3 = 1;
   ca.tr = d_tr;
   ca.mr2 = mc.r2;
-  {
-    // Z(g2^i) = (g2^steps)^(i mod 8) - 1; inverse with 0 -> 0 (prove.rs:128-129, 203).
-    const HostFp w8 = F.pow_u64(g2, steps);
-    HostFp wt = F.one();
-    for (int t = 0; t < 8; ++t) {
-      const HostFp z = F.sub(wt, F.one());
-      ca.invz_m[t] = FieldHost::eq(z, F.zero()) ? fe_zero_host() : to_dev(F.inv(z));
-      wt = F.mul(wt, w8);
-    }
-  }
+  set_inv_z(ca, g2, steps);
+  ca.mont_cols = pre ? 1 : 0;
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
   // Main tree over the 256-B rows (prove.rs:261-264).
   STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s));
-  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(m_tree), mc.r2, mc.one,
-                     d_tr);
-  STARK_HIP(ctx, hipGetLastError());
+  {
+    XsPowers xs;
+    const HostFp w8 = F.pow_u64(g2, steps);
+    HostFp wt = F.one();
+    for (int t = 0; t < 8; ++t) {
+      xs.v[t] = to_dev(wt);
+      wt = F.mul(wt, w8);
+    }
+    hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(m_tree), mc.r2,
+                       mc.one, xs, d_tr);
+    STARK_HIP(ctx, hipGetLastError());
+  }
   LincombArgs la;
   la.rows = rows;
   la.out = lvals;
@@ -733,14 +775,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   la.g_add = 0;
   la.log_g = 0;
   la.tr = d_tr;
-  {
-    const HostFp w8 = F.pow_u64(g2, steps);
-    HostFp wt = F.one();
-    for (int t = 0; t < 8; ++t) {
-      la.xs_m[t] = to_dev(wt);
-      wt = F.mul(wt, w8);
-    }
-  }
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s));
@@ -809,6 +843,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   return STARK_OK;
 }
 
+// v[i] <- Montgomery image of v[i] (canonical in).
+__global__ void to_mont_kernel(fe* __restrict__ v, uint64_t n, fe r2) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fe_store(v + i, fe_mul(fe_load(v + i), r2));
+}
+
 // IDX / PIDX step columns only (the circuit's part of r1cs_index_kernel).
 __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, uint64_t steps, fe* __restrict__ idx,
                                 fe* __restrict__ pidx) {
@@ -870,6 +910,12 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                          (uint64_t)0, (uint32_t)0, (const fe*)d_xk, (uint32_t)n_pfi,
                          to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + prec);
       st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * prec, 2 * prec, s);
+    }
+    if (st == STARK_OK) {  // K, F0-F2 and the Zb inverses as Montgomery images (ConstraintArgs::mont_cols)
+      fe* o = (fe*)out.ptr;
+      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * prec)), dim3(256), 0, s, o, 4 * prec, mc.r2);
+      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * prec)), dim3(256), 0, s, o + 6 * prec, 2 * prec, mc.r2);
+      if (hipGetLastError() != hipSuccess) st = STARK_ERR_HIP;
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
   }
@@ -1138,12 +1184,12 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   ca.n3 = 1;
   ca.tr = d.d_tr;
   ca.mr2 = mc.r2;
+  set_inv_z(ca, g2, steps);
+  ca.mont_cols = 0;
   {
     const HostFp w8 = F.pow_u64(g2, steps);
     HostFp wt = F.one();
     for (int t = 0; t < 8; ++t) {
-      const HostFp z = F.sub(wt, F.one());
-      ca.invz_m[t] = FieldHost::eq(z, F.zero()) ? fe_zero_host() : to_dev(F.inv(z));
       d.xs_m[t] = to_dev(wt);
       wt = F.mul(wt, w8);
     }
@@ -1288,7 +1334,9 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
   // k from m_root (prove.rs:274-283) on the device, then L at this rank's points.
   uint32_t* d_root = d.d_tr->roots[1];
   STARK_HIP(d.ctx, hipMemcpyAsync(d_root, m_root, 32, hipMemcpyHostToDevice, d.s));
-  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, d.d_tr);
+  XsPowers xs;
+  for (int t = 0; t < 8; ++t) xs.v[t] = d.xs_m[t];
+  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs, d.d_tr);
   STARK_HIP(d.ctx, hipGetLastError());
   LincombArgs la;
   la.rows = d.rows;
@@ -1297,7 +1345,6 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
   la.g_add = d.r;
   la.log_g = d.log_g;
   la.tr = d.d_tr;
-  for (int t = 0; t < 8; ++t) la.xs_m[t] = d.xs_m[t];
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(d.P)), dim3(256), 0, d.s, la);
   STARK_HIP(d.ctx, hipGetLastError());
   STARK_HIP(d.ctx, hipStreamSynchronize(d.s));  // m_root is the caller's (pageable) buffer

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "stark-pure-rust_amd"), os.path.join(ROOT, "tools")]
 
 import stark_amd as S  # noqa: E402
-from stark_amd.r1cs import R1csTrace, prove_with_witness  # noqa: E402
+from stark_amd.r1cs import R1csCircuit, R1csTrace, prove_with_witness  # noqa: E402
 import synth_r1cs  # noqa: E402
 
 
@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--synth", default="16,18,20")
     ap.add_argument("--fixtures", default="poseidon3_test,pedersen_test")
+    ap.add_argument("--prepared", action="store_true", help="prove through R1csCircuit (prepared once)")
     a = ap.parse_args()
     ctx = S.Context(0)
     cases = []
@@ -35,9 +36,10 @@ def main():
         t_trace = time.perf_counter() - t0
         dims = tr.dims()
         times = []
+        circ = R1csCircuit(ctx, r) if a.prepared else None
         for i in range(a.reps + 1):
             t1 = time.perf_counter()
-            p = prove_with_witness(ctx, r, w)
+            p = circ.prove(w) if circ else prove_with_witness(ctx, r, w)
             js = p.to_json()
             times.append(time.perf_counter() - t1)
         print(f"{name}: original_steps={dims['original_steps']} host_trace_build={t_trace * 1e3:.1f} ms "
