@@ -147,11 +147,11 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
         out["prove_pedersen_distributed_bitexact_vs_golden"] = \
             hashlib.sha256(js.encode()).hexdigest() == golden["pedersen_test"]["json_sha256"]
 
-    def timed(rs, ws, reps):
+    def timed(rs, ws, reps, circuit=None):
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
-            prove_distributed(ops, rs, ws)
+            prove_distributed(ops, rs, ws, circuit=circuit)
         dist.barrier()
         t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64,
                          device="cpu" if on_gloo else f"cuda:{local}")
@@ -162,6 +162,12 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
     rs, ws = synth_r1cs.for_steps(20)
     prove_distributed(ops, rs, ws)   # warm: twiddles, arenas
     out["prove_synth_2^20_steps_distributed_ms"] = timed(rs, ws, 3)
+    # Prepared circuit per rank (DistCircuit: the .r1cs-only work outside the timed region), labelled.
+    from stark_amd.dprove import DistCircuit
+    circ = DistCircuit(ctx, rs)
+    prove_distributed(ops, None, ws, circuit=circ)
+    out["prove_synth_2^20_steps_distributed_prepared_circuit_ms"] = timed(None, ws, 3, circ)
+    del circ
     return out
 
 
@@ -398,7 +404,7 @@ def main():
         # instructions per launch x ~4.5 cycles each (the half-rate mad/carry ops that are ~90 % of the
         # mix, tools/microbench/isa_lat.hip) over the SIMD-cycles of the measured launch.
         sq = json.load(open(SQ_PROFILE))["kernels"]["stark::ntt_pass_kernel<8, false>"]
-        if log_n == 24:
+        if log_n == 24 and world == 1:
             simd_cycles = 1024 * 2.4e9 * (ev_ms / passes) / 1000.0
             valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
             valu["issue_busy_frac_est"] = round(sq["SQ_INSTS_VALU"] * 4.5 / simd_cycles, 3)

@@ -336,6 +336,13 @@ stark_status stark_dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, c
 stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
                                       size_t r1cs_len, const uint8_t* wtns, size_t wtns_len, void* stream,
                                       stark_dprove** out);
+/* A circuit prepared for rank `rank` of `world` (as stark_r1cs_circuit_new, with this rank's
+ * coset LDEs and Zb inverses), and the distributed proof of one witness with it.  The proofs
+ * equal stark_dprove_begin_bytes' on the same bytes. */
+stark_status stark_dprove_circuit_new(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
+                                      size_t r1cs_len, stark_r1cs_circuit** out);
+stark_status stark_dprove_begin_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit, const uint8_t* wtns,
+                                        size_t wtns_len, void* stream, stark_dprove** out);
 /* Sizes, g2 = 7^((p-1)/precision) (prove.rs:71-82) and a_root; STARK_ERR_CHECK
  * where the reference's D/B asserts would panic (on this rank's points). */
 stark_status stark_dprove_info(stark_dprove* h, size_t* precision, size_t* n_local, size_t* original_steps,

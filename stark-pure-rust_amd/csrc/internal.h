@@ -200,15 +200,24 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // mk_r1cs_proof on trace columns given as host or device pointers, flags as
 // bytes (r1cs.hip).
 // The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the
-// inverses of Zb2, Zb3 (8 x precision; K, F0-F2 and the inverses as Montgomery images).
+// inverses of Zb2, Zb3 at the points rank + world j (8 x precision/world; K, F0-F2 and the
+// inverses as Montgomery images).  world = 1: the whole domain.
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
-                         const size_t* public_first_indices, size_t n_pfi, DevBuf& out, hipStream_t s);
+                         const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
+                         hipStream_t s);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                     size_t os, const uint64_t* public_wires, size_t n_public,
                                     const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
                                     const uint64_t* coefficients, const uint8_t* flag_bytes, size_t n_constraints,
                                     size_t n_wires, const fe* pre, stark_r1cs_proof** out);
+// dprove_begin (r1cs.hip) with a prepared circuit's columns for this rank.
+stark_status dprove_begin_prepared(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
+                                   const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                   size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                   const size_t* permuted_indices, const uint64_t* coefficients,
+                                   const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires, const fe* pre,
+                                   void* stream, stark_dprove** out);
 stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
                                       const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,

@@ -558,11 +558,37 @@ static stark_status product_scan(stark_ctx* ctx, fe* v, uint64_t n, fe* tot, fe*
 
 // LDE of `batch` step columns (in place in `coef`, destroyed) into `out`
 // (batch x precision): inv_best_fft(., g1) then best_fft(., g2) (prove.rs:100-101).
+// coef[c][k] *= g2^(r k) for the batch of step columns (coset shift of the LDE).
+__global__ void coset_scale_kernel(fe* __restrict__ coef, uint32_t log_steps, uint64_t total, const fe* __restrict__ lo,
+                                   const fe* __restrict__ hi, uint32_t kb, uint64_t r, uint64_t prec_mask) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total) return;
+  const uint64_t k = g & (((uint64_t)1 << log_steps) - 1);
+  fe_store(coef + g, fe_mul(fe_load(coef + g), pow_tab(lo, hi, kb, (r * k) & prec_mask)));
+}
+
+// The values of the step columns' polynomials at the points r + 2^log_g j of the precision
+// domain (j < P = precision >> log_g): iNTT(steps, g1), coefficients scaled by g2^(r k), then a
+// P-point NTT with root h = g2^(2^log_g) over the zero-padded coefficients (degree < steps <= P).
+// log_g = r = 0 is the plain LDE of prove.rs:100-101.  coef is destroyed.
+static stark_status coset_lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint32_t log_steps,
+                              uint32_t log_prec, uint32_t log_g, uint32_t r, const Twiddles& tw_g1_inv,
+                              const Twiddles& tw_g2, const Twiddles& tw_h, hipStream_t s) {
+  STARK_TRY(ntt_device(ctx, coef, log_steps, batch, tw_g1_inv, true, s));
+  if (r) {
+    const uint64_t total = (uint64_t)batch << log_steps;
+    hipLaunchKernelGGL(coset_scale_kernel, dim3(blocks_for(total)), dim3(256), 0, s, coef, log_steps, total,
+                       tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, (uint64_t)r, ((uint64_t)1 << log_prec) - 1);
+    STARK_HIP(ctx, hipGetLastError());
+  }
+  // best_fft's zero padding (fft.rs:327-357) is implicit: the first pass reads the steps coefficients only.
+  const uint32_t log_p = log_prec - log_g;
+  return ntt_device_from(ctx, coef, log_p - log_steps, out, log_p, batch, tw_h, false, s);
+}
+
 static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint32_t log_steps, uint32_t log_prec,
                         const Twiddles& tw_g1_inv, const Twiddles& tw_g2, hipStream_t s) {
-  STARK_TRY(ntt_device(ctx, coef, log_steps, batch, tw_g1_inv, true, s));
-  // best_fft's zero padding (fft.rs:327-357) is implicit: the first pass reads the steps coefficients only.
-  return ntt_device_from(ctx, coef, log_prec - log_steps, out, log_prec, batch, tw_g2, false, s);
+  return coset_lde(ctx, coef, batch, out, log_steps, log_prec, 0, 0, tw_g1_inv, tw_g2, tw_g2, s);
 }
 
 static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
@@ -862,30 +888,38 @@ __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, 
 // (prove.rs:100-124, 160-167), 6 x precision into `out`.  coef / flag bytes / perm
 // are the device trace builder's circuit columns (os slots).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
-                         const size_t* public_first_indices, size_t n_pfi, DevBuf& out, hipStream_t s) {
+                         const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
+                         hipStream_t s) {
   const FieldHost& F = FieldHost::get();
+  if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
+    return STARK_ERR_BAD_ARG;
+  uint32_t log_g = 0;
+  while ((1u << log_g) < world) ++log_g;
   if (os < 5 || os % 3 != 0) return STARK_ERR_BAD_LENGTH;
   const uint32_t log_steps = log2_ceil_ref(os - 1);
   const uint32_t log_prec = log_steps + kLogExtensionFactor;
   if (log_prec >= 24) return STARK_ERR_BAD_LENGTH;
   const uint64_t steps = (uint64_t)1 << log_steps, prec = (uint64_t)1 << log_prec;
+  const uint64_t P = prec >> log_g;  // this rank's points r + world j
   uint64_t pm1[4];
   memcpy(pm1, FieldHost::kP, 32);
   pm1[0] -= 1;
   for (uint32_t k = 0; k < log_prec; ++k)
     for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
   const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
-  uint64_t g2c[4], g1ic[4];
+  uint64_t g2c[4], g1ic[4], hc[4];
   F.to_canonical(g2, g2c);
   F.to_canonical(F.inv(F.pow_u64(g2, prec / steps)), g1ic);
-  const Twiddles *tw2 = nullptr, *tw1i = nullptr;
+  F.to_canonical(F.pow_u64(g2, world), hc);
+  const Twiddles *tw2 = nullptr, *tw1i = nullptr, *twh = nullptr;
   STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
   STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
+  STARK_TRY(get_twiddles(ctx, hc, log_prec - log_g, &twh));
   for (size_t i = 0; i < n_pfi; ++i)
     if (public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
-  DevBuf tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 precision + n_pfi)
-  STARK_TRY(ensure_buf(ctx, tmp, (6 * steps + 2 * prec + n_pfi + 1) * sizeof(fe)));
-  stark_status st = ensure_buf(ctx, out, 8 * prec * sizeof(fe));
+  DevBuf tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 P + n_pfi)
+  STARK_TRY(ensure_buf(ctx, tmp, (6 * steps + 2 * P + n_pfi + 1) * sizeof(fe)));
+  stark_status st = ensure_buf(ctx, out, 8 * P * sizeof(fe));
   if (st == STARK_OK) {
     fe* raw = (fe*)tmp.ptr;
     hipMemsetAsync(raw, 0, 6 * steps * sizeof(fe), s);
@@ -894,27 +928,27 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                        raw + steps);
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
-    st = lde(ctx, raw, 6, (fe*)out.ptr, log_steps, log_prec, *tw1i, *tw2, s);
+    st = coset_lde(ctx, raw, 6, (fe*)out.ptr, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
     // Zb2 = prod_k (x - x_k), Zb3 = x - x_last (utils.rs:438-474) and their inverses (0 -> 0).
     const uint64_t skips = prec / steps;
     std::vector<fe> xk(n_pfi + 1);
     for (size_t i = 0; i < n_pfi; ++i) xk[i] = to_dev(F.pow_u64(g2, skips * public_first_indices[2 * i + 1]));
     fe* zb = raw + 6 * steps;
-    fe* d_xk = zb + 2 * prec;
+    fe* d_xk = zb + 2 * P;
     const Mont mc = mont();
     if (st == STARK_OK && n_pfi &&
         hipMemcpyAsync(d_xk, xk.data(), n_pfi * sizeof(fe), hipMemcpyHostToDevice, s) != hipSuccess)
       st = STARK_ERR_HIP;
     if (st == STARK_OK) {
-      hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
-                         (uint64_t)0, (uint32_t)0, (const fe*)d_xk, (uint32_t)n_pfi,
-                         to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + prec);
-      st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * prec, 2 * prec, s);
+      hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
+                         (uint64_t)rank, log_g, (const fe*)d_xk, (uint32_t)n_pfi,
+                         to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + P);
+      st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * P, 2 * P, s);
     }
     if (st == STARK_OK) {  // K, F0-F2 and the Zb inverses as Montgomery images (ConstraintArgs::mont_cols)
       fe* o = (fe*)out.ptr;
-      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * prec)), dim3(256), 0, s, o, 4 * prec, mc.r2);
-      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * prec)), dim3(256), 0, s, o + 6 * prec, 2 * prec, mc.r2);
+      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * P)), dim3(256), 0, s, o, 4 * P, mc.r2);
+      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * P)), dim3(256), 0, s, o + 6 * P, 2 * P, mc.r2);
       if (hipGetLastError() != hipSuccess) st = STARK_ERR_HIP;
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
@@ -996,27 +1030,10 @@ struct stark_dprove {
 
 namespace stark {
 
-// coef[c][k] *= g2^(r k) for the batch of step columns (coset shift of the LDE).
-__global__ void coset_scale_kernel(fe* __restrict__ coef, uint32_t log_steps, uint64_t total, const fe* __restrict__ lo,
-                                   const fe* __restrict__ hi, uint32_t kb, uint64_t r, uint64_t prec_mask) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= total) return;
-  const uint64_t k = g & (((uint64_t)1 << log_steps) - 1);
-  fe_store(coef + g, fe_mul(fe_load(coef + g), pow_tab(lo, hi, kb, (r * k) & prec_mask)));
-}
-
 // Coset LDE of `batch` step columns (coef, destroyed) into out (batch x P).
 static stark_status lde_coset(DProveState& d, fe* coef, uint32_t batch, fe* out, const Twiddles& tw_g1_inv,
                               const Twiddles& tw_g2, const Twiddles& tw_h) {
-  STARK_TRY(ntt_device(d.ctx, coef, d.log_steps, batch, tw_g1_inv, true, d.s));
-  if (d.r) {
-    const uint64_t total = (uint64_t)batch << d.log_steps;
-    hipLaunchKernelGGL(coset_scale_kernel, dim3(blocks_for(total)), dim3(256), 0, d.s, coef, d.log_steps, total,
-                       tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, (uint64_t)d.r, d.prec - 1);
-    STARK_HIP(d.ctx, hipGetLastError());
-  }
-  const uint32_t log_p = d.log_prec - d.log_g;
-  return ntt_device_from(d.ctx, coef, log_p - d.log_steps, out, log_p, batch, tw_h, false, d.s);
+  return coset_lde(d.ctx, coef, batch, out, d.log_steps, d.log_prec, d.log_g, d.r, tw_g1_inv, tw_g2, tw_h, d.s);
 }
 
 static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
@@ -1024,7 +1041,10 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
                                  size_t n_public, const size_t* public_first_indices, size_t n_pfi,
                                  const size_t* permuted_indices, const uint64_t* coefficients, const uint64_t* flag0,
                                  const uint64_t* flag1, const uint64_t* flag2, const uint8_t* flag_bytes,
-                                 size_t n_constraints, size_t n_wires, hipStream_t s, stark_dprove* h) {
+                                 size_t n_constraints, size_t n_wires, hipStream_t s, stark_dprove* h,
+                                 const fe* pre = nullptr) {
+  // pre != nullptr: this rank's prepared circuit columns (circuit_lde with world, rank): the coset
+  // LDEs of K F0 F1 F2 IDX PIDX and the Zb inverses; only S, P and A are extended here.
   const FieldHost& F = FieldHost::get();
   DProveState& d = h->st;
   if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
@@ -1120,12 +1140,12 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_HIP(ctx, hipMemcpyAsync(consts, hc2.data(), hc2.size() * sizeof(fe), hipMemcpyHostToDevice, s));
   // Step columns (prove.rs:59-69), host or device sources.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
-  for (int c = 0; c < 6; ++c) {
+  for (int c = pre ? 4 : 0; c < 6; ++c) {
     if (!(flag_bytes && c >= 1 && c <= 3))
       STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyDefault, s));
     if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
   }
-  if (flag_bytes) {
+  if (flag_bytes && !pre) {
     uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel (sized for the 3 os flag bytes)
     STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyDefault, s));
     hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
@@ -1141,7 +1161,10 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
   STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
   STARK_TRY(merkle_build(ctx, d.acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
-  STARK_TRY(lde_coset(d, raw, 8, cols, *tw1i, *tw2, *twh));
+  if (pre)
+    STARK_TRY(lde_coset(d, raw + 4 * steps, 2, cols + 4 * P, *tw1i, *tw2, *twh));
+  else
+    STARK_TRY(lde_coset(d, raw, 8, cols, *tw1i, *tw2, *twh));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
                      (uint32_t)(prec - 1), mc.r2, d.d_tr);
   STARK_HIP(ctx, hipGetLastError());
@@ -1157,15 +1180,21 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
                      (const fe*)inv_dnm, steps, raw);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(lde_coset(d, raw, 1, cols + 8 * P, *tw1i, *tw2, *twh));
-  // Zb2 / Zb3 at this rank's points and their inverses.
-  hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
-                     (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
-                     zb, zb + P);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
+  if (!pre) {  // Zb2 / Zb3 at this rank's points and their inverses
+    hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
+                       (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
+                       zb, zb + P);
+    STARK_HIP(ctx, hipGetLastError());
+    STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
+  }
   ConstraintArgs ca;
   for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * P;
-  ca.inv_zb = inv_zb;
+  ca.inv_zb = pre ? pre + 6 * P : inv_zb;
+  if (pre) {
+    for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * P;
+    ca.col[6] = pre + 4 * P;
+    ca.col[7] = pre + 5 * P;
+  }
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
   ca.lo = tw2->d_lo;
@@ -1185,7 +1214,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   ca.tr = d.d_tr;
   ca.mr2 = mc.r2;
   set_inv_z(ca, g2, steps);
-  ca.mont_cols = 0;
+  ca.mont_cols = pre ? 1 : 0;
   {
     const HostFp w8 = F.pow_u64(g2, steps);
     HostFp wt = F.one();
@@ -1275,6 +1304,32 @@ stark_status stark_dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, c
   *out = h.release();
   return STARK_OK;
 }
+
+}  // extern "C"
+
+stark_status stark::dprove_begin_prepared(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint64_t* witness_trace,
+                                          const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
+                                          size_t n_public, const size_t* public_first_indices, size_t n_pfi,
+                                          const size_t* permuted_indices, const uint64_t* coefficients,
+                                          const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
+                                          const fe* pre, void* stream, stark_dprove** out) {
+  if (!ctx || !out || !pre) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  auto h = std::make_unique<stark_dprove>();
+  hipStream_t s = pick_stream(ctx, stream);
+  const stark_status st = dprove_begin(ctx, world, rank, witness_trace, computational_trace, os, public_wires,
+                                       n_public, public_first_indices, n_pfi, permuted_indices, coefficients, nullptr,
+                                       nullptr, nullptr, flag_bytes, n_constraints, n_wires, s, h.get(), pre);
+  if (st != STARK_OK) {
+    hipStreamSynchronize(s);
+    return st;
+  }
+  *out = h.release();
+  return STARK_OK;
+}
+
+extern "C" {
 
 stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
                                       size_t r1cs_len, const uint8_t* wtns, size_t wtns_len, void* stream,

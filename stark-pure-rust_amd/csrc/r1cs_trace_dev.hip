@@ -338,6 +338,7 @@ struct PreparedCircuit {
   DevBuf arena, lde;
   size_t os = 0, n_wires = 0, n_public = 0;
   uint32_t n_c = 0;
+  uint32_t world = 1, rank = 0;  // the points rank + world j of the precision domain (distributed prover)
   uint64_t a_len = 0;
   std::vector<size_t> pfi;
   const uint32_t* base = nullptr;
@@ -445,7 +446,7 @@ static stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1
   c.flags = flags;
   c.perm = (const uint64_t*)(A + o_perm);
   c.slot_wire = (const uint32_t*)(A + o_sw);
-  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.lde, s);
+  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s);
 }
 
 // The witness of one proof: decode, then S and P from the circuit's slot wires.
@@ -550,7 +551,7 @@ void stark_r1cs_circuit_free(stark_r1cs_circuit* c) { delete c; }
 
 stark_status stark_prove_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit, const uint8_t* wtns,
                                       size_t wtns_len, stark_r1cs_proof** out) {
-  if (!ctx || !circuit || !wtns || !out || circuit->ctx != ctx) return STARK_ERR_BAD_ARG;
+  if (!ctx || !circuit || !wtns || !out || circuit->ctx != ctx || circuit->c.world != 1) return STARK_ERR_BAD_ARG;
   *out = nullptr;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   const PreparedCircuit& c = circuit->c;
@@ -560,6 +561,39 @@ stark_status stark_prove_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* 
   return mk_r1cs_proof_prepared(ctx, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, c.os, dt.public_wires.data(),
                                 dt.public_wires.size() / 4, c.pfi.data(), c.pfi.size() / 2, (const size_t*)c.perm,
                                 (const uint64_t*)c.coef, c.flags, c.n_c, c.n_wires, (const fe*)c.lde.ptr, out);
+}
+
+stark_status stark_dprove_circuit_new(stark_ctx* ctx, uint32_t world, uint32_t rank, const uint8_t* r1cs,
+                                      size_t r1cs_len, stark_r1cs_circuit** out) {
+  if (!ctx || !r1cs || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  if (world == 0 || world > 8 || (world & (world - 1)) || rank >= world) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  auto h = std::make_unique<stark_r1cs_circuit>();
+  h->ctx = ctx;
+  h->c.world = world;
+  h->c.rank = rank;
+  const stark_status st = circuit_build(ctx, r1cs, r1cs_len, h->c);
+  hipStreamSynchronize(ctx->stream);
+  if (st != STARK_OK) return st;
+  *out = h.release();
+  return STARK_OK;
+}
+
+stark_status stark_dprove_begin_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit, const uint8_t* wtns,
+                                        size_t wtns_len, void* stream, stark_dprove** out) {
+  if (!ctx || !circuit || !wtns || !out || circuit->ctx != ctx) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const PreparedCircuit& c = circuit->c;
+  DevTrace dt;
+  stark_status st = circuit_witness(ctx, c, wtns, wtns_len, &dt);
+  if (st != STARK_OK) return st;
+  STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the witness columns are built on the context stream
+  return dprove_begin_prepared(ctx, c.world, c.rank, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, c.os,
+                               dt.public_wires.data(), dt.public_wires.size() / 4, c.pfi.data(), c.pfi.size() / 2,
+                               (const size_t*)c.perm, (const uint64_t*)c.coef, c.flags, c.n_c, c.n_wires,
+                               (const fe*)c.lde.ptr, stream, out);
 }
 
 }  // extern "C"

@@ -115,6 +115,10 @@ _SIGNATURES = {
     "stark_r1cs_circuit_new": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_circuit_free": ([_vp], None),
     "stark_prove_r1cs_circuit": ([_vp, _vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_circuit_new": ([_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                  ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_dprove_begin_circuit": ([_vp, _vp, ctypes.c_char_p, ctypes.c_size_t, _vp, ctypes.POINTER(_vp)],
+                                   ctypes.c_int),
     "stark_fri_fold_dev": ([_vp, _vp, _vp, ctypes.c_size_t, _u64p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _vp],
                            ctypes.c_int),
     "stark_r1cs_proof_json_from_parts": ([_u8p, _u8p, _u8p, _vp, _vp, _vp, ctypes.c_size_t, _u8p, ctypes.c_size_t,

@@ -212,9 +212,10 @@ FRI_TAIL_LOG = 16
 _EMPTY_LAST = '{"Last":{"last":[]}}]}'
 
 
-def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: int = FRI_TAIL_LOG):
+def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: int = FRI_TAIL_LOG, circuit=None):
     """prove_with_witness (run.rs:310-452) over the G ranks of `group`.
-    Every rank calls it; rank 0 returns the StarkProof JSON, the others None."""
+    Every rank calls it; rank 0 returns the StarkProof JSON, the others None.
+    circuit: this rank's DistCircuit (the .r1cs-only work done once; r1cs is then unused)."""
     G = dist.get_world_size(group)
     r = dist.get_rank(group)
     ph = _Phases(r)
@@ -224,7 +225,7 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
     # reports its status first and all of them raise together.
     h, status, info = None, 0, None
     try:
-        h = ops.begin(r1cs, wtns, G, r)
+        h = ops.begin(r1cs, wtns, G, r, circuit)
         status, info = ops.info(h)
     except Exception as e:  # noqa: BLE001 - re-raised below on every rank
         status = getattr(e, "code", -1) or -1
@@ -294,6 +295,28 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
             ops.end(h)
 
 
+class DistCircuit:
+    """A circuit prepared on this rank for prove_distributed (stark_dprove_circuit_new): the
+    slot tables and this rank's coset LDEs of K, F0-F2, IDX, PIDX and Zb inverses stay in HBM,
+    so each proof extends only S, P and A (cf. stark_amd.r1cs.R1csCircuit on one GPU)."""
+
+    def __init__(self, ctx, r1cs: bytes, group=None):
+        from . import _vp
+        self.ctx = ctx
+        self.G = dist.get_world_size(group)
+        self.r = dist.get_rank(group)
+        self.h = _vp()
+        ctx.check(ctx.lib.stark_dprove_circuit_new(ctx.h, self.G, self.r, r1cs, len(r1cs), ctypes.byref(self.h)),
+                  "dprove_circuit_new")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.ctx.lib.stark_r1cs_circuit_free(self.h)
+        except Exception:
+            pass
+
+
 class _OpenReq(ctypes.Structure):
     _fields_ = [("tree", ctypes.c_void_p), ("d_rows", ctypes.c_void_p), ("row_bytes", ctypes.c_size_t),
                 ("n_rows", ctypes.c_size_t), ("idx", ctypes.POINTER(ctypes.c_size_t)), ("k", ctypes.c_size_t),
@@ -321,11 +344,17 @@ class GpuProverOps:
         from . import StarkError
         raise StarkError(code, where)
 
-    def begin(self, r1cs: bytes, wtns: bytes, G: int, r: int):
+    def begin(self, r1cs: bytes, wtns: bytes, G: int, r: int, circuit=None):
         from . import _vp
         h = _vp()
-        self.ctx.check(self.lib.stark_dprove_begin_bytes(self.ctx.h, G, r, r1cs, len(r1cs), wtns, len(wtns),
-                                                         self._stream(), ctypes.byref(h)), "dprove_begin")
+        if circuit is not None:
+            if (circuit.G, circuit.r) != (G, r):
+                raise ValueError("DistCircuit prepared for another rank / world size")
+            self.ctx.check(self.lib.stark_dprove_begin_circuit(self.ctx.h, circuit.h, wtns, len(wtns), self._stream(),
+                                                               ctypes.byref(h)), "dprove_begin")
+        else:
+            self.ctx.check(self.lib.stark_dprove_begin_bytes(self.ctx.h, G, r, r1cs, len(r1cs), wtns, len(wtns),
+                                                             self._stream(), ctypes.byref(h)), "dprove_begin")
         return h
 
     def info(self, h):

@@ -72,7 +72,7 @@ class OracleProverOps:
     def raise_status(self, code, where):
         raise RuntimeError(f"{where}: {code}")
 
-    def begin(self, r1cs, wtns, G, r):
+    def begin(self, r1cs, wtns, G, r, circuit=None):
         tr = self.R.build_trace(self.R.read_r1cs(r1cs), self.R.read_witness(wtns))
         rows, a_root = self.R.r1cs_rows(self.o, tr, cpus=2)
         prec = len(rows) // 256

@@ -87,3 +87,58 @@ def test_prove_distributed_gpu_synthetic(world):
     """A 2^14-step synthetic circuit: the distributed proof equals the single-GPU proof."""
     got, single = _run(world, None, 14)
     assert got == single
+
+
+def _worker_circuit(rank, world, port, out_q):
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=80))
+    import stark_amd as S
+    from stark_amd.dprove import DistCircuit, GpuProverOps, prove_distributed
+    from stark_amd.r1cs import prove_with_witness
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth_r1cs
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = S.Context(0)
+    r1, _ = synth_r1cs.for_steps(13)
+    circ = DistCircuit(ctx, r1)
+    got = []
+    for inputs in [(5, 6), (7, 8)]:
+        _, wt = synth_r1cs.for_steps(13, inputs=inputs)
+        js = prove_distributed(GpuProverOps(ctx), None, wt, circuit=circ)
+        if rank == 0:
+            got.append(hashlib.sha256(js.encode()).hexdigest() ==
+                       hashlib.sha256(prove_with_witness(ctx, r1, wt).to_json().encode()).hexdigest())
+    r1p, wtp = open(os.path.join(FIX, "pedersen_test.r1cs"), "rb").read(), open(os.path.join(FIX, "pedersen_test.wtns"), "rb").read()
+    js = prove_distributed(GpuProverOps(ctx), None, wtp, circuit=DistCircuit(ctx, r1p))
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
+    if rank == 0:
+        got.append(hashlib.sha256(js.encode()).hexdigest() == golden["pedersen_test"]["json_sha256"])
+    out_q.put((rank, got))
+    dist.barrier()
+    del circ
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 4])
+def test_prove_distributed_prepared_circuit(world):
+    """DistCircuit: two witnesses of one synthetic circuit equal the single-GPU proofs; pedersen_test
+    equals the golden digest."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_circuit, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=110) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0
+    assert res[0] == [True, True, True]

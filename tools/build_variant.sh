@@ -1,13 +1,14 @@
 #!/bin/bash
 # Builds an experimental variant of libstark_hip.so: copies csrc/ to a temp
-# dir, applies a python transform to ntt.hip, compiles.  Timing-only builds;
-# never shipped.   usage: build_variant.sh <out.so> <python-expr on s> [extra hipcc flags]
+# dir, applies a python transform to ntt.hip (or $VARIANT_FILE), compiles.
+# Timing-only builds; never shipped.
+# usage: [VARIANT_FILE=merkle.hip] build_variant.sh <out.so> <python-expr on s> [extra hipcc flags]
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$1; EXPR=$2; shift 2
 TMP=$(mktemp -d)
 cp "$ROOT"/stark-pure-rust_amd/csrc/* "$TMP"/
-python3 - "$TMP/ntt.hip" "$EXPR" <<'PY'
+python3 - "$TMP/${VARIANT_FILE:-ntt.hip}" "$EXPR" <<'PY'
 import sys
 p, expr = sys.argv[1], sys.argv[2]
 s = open(p).read()
