@@ -399,18 +399,24 @@ def main():
     valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
     valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
-    try:
-        # VALU issue occupancy of the same kernel (committed rocprofv3 SQ counters): wave64 VALU
-        # instructions per launch x ~4.5 cycles each (the half-rate mad/carry ops that are ~90 % of the
-        # mix, tools/microbench/isa_lat.hip) over the SIMD-cycles of the measured launch.
-        sq = json.load(open(SQ_PROFILE))["kernels"]["stark::ntt_pass_kernel<8, false>"]
-        if log_n == 24 and world == 1:
-            simd_cycles = 1024 * 2.4e9 * (ev_ms / passes) / 1000.0
-            valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
-            valu["issue_busy_frac_est"] = round(sq["SQ_INSTS_VALU"] * 4.5 / simd_cycles, 3)
-            valu["sq_profile"] = os.path.relpath(SQ_PROFILE, ROOT)
-    except (OSError, KeyError, ValueError):
-        pass
+    if world == 1:
+        # VALU issue occupancy of the dominant kernel.  Each product issues 128 v_mad_u64_u32 + 128
+        # v_addc_co_u32, measured at ~4.6 cycles per wave64 instruction (tools/microbench/isa_rates.hip);
+        # their share of the SIMD-cycles of the measured launches (1024 SIMDs x 2.4 GHz):
+        simd_cycles = 1024 * 2.4e9 * ev_ms / 1000.0
+        valu["mad_carry_issue_frac"] = round(modmuls * 256 / 64 * 4.6 / simd_cycles, 3)
+        try:
+            # All VALU instructions (committed rocprofv3 SQ_INSTS_VALU of the same kernel) at 2.3 cycles
+            # (VOP2) to 4.6 cycles (VOP3 / carry ops): the range of the whole issue occupancy.
+            sq = json.load(open(SQ_PROFILE))["kernels"]["stark::ntt_pass_kernel<8, false>"]
+            if log_n == 24:
+                insts = sq["SQ_INSTS_VALU"] * passes
+                valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
+                valu["all_valu_issue_frac_range"] = [round(insts * 2.3 / simd_cycles, 3),
+                                                     round(insts * 4.6 / simd_cycles, 3)]
+                valu["sq_profile"] = os.path.relpath(SQ_PROFILE, ROOT)
+        except (OSError, KeyError, ValueError):
+            pass
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
