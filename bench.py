@@ -103,6 +103,19 @@ def end_to_end(ctx):
         prove_with_witness(ctx, r1, wt).to_json()
         ts.append(time.perf_counter() - t0)
     out["prove_pedersen_ms"] = round(min(ts) * 1000.0, 3)
+    for name in ("compute", "poseidon3_test"):          # configs 1 and 4 (single GPU), bit-exact
+        r1n = open(os.path.join(fix, f"{name}.r1cs"), "rb").read()
+        wtn = open(os.path.join(fix, f"{name}.wtns"), "rb").read()
+        jsn = prove_with_witness(ctx, r1n, wtn).to_json()
+        tn = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            prove_with_witness(ctx, r1n, wtn).to_json()
+            tn.append(time.perf_counter() - t0)
+        short = name.split("_")[0]
+        out[f"prove_{short}_ms"] = round(min(tn) * 1000.0, 3)
+        out[f"prove_{short}_bitexact_vs_golden"] = \
+            hashlib.sha256(jsn.encode()).hexdigest() == golden[name]["json_sha256"]
     out["prove_synth_2^20_steps_ms"] = round(synth_ms(3) * 1000.0, 3)
     # The same proofs from a prepared circuit (R1csCircuit: the .r1cs-only work, including the LDEs of
     # K, F0-F2, IDX, PIDX, done once outside the timed region): a prover serving many witnesses of
@@ -306,6 +319,13 @@ def main():
         extras["merkle_2^24x32B_leaves_per_s"] = n / (mk_ms / 1000.0)
         extras["merkle_2^24x32B_ms"] = round(mk_ms, 4)
         extras["merkle_roofline_frac"] = round(96.0 * n / (mk_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
+        # Secondary leaf shapes: 256-B leaves (the main tree's P|A|S|D1..B3 rows; the same
+        # 512 MiB buffer read as 2^21 rows) and 2^20 x 40-B accumulator leaves.
+        for cnt, ll, key in ((n // 8, 256, "merkle_2^21x256B"), (1 << 20, 40, "merkle_2^20x40B")):
+            tree.update_dev(dptr, cnt, ll, stream=sptr)
+            t_ms = timed_events(lambda: tree.update_dev(dptr, cnt, ll, stream=sptr), stream, 5)
+            extras[f"{key}_leaves_per_s"] = cnt / (t_ms / 1000.0)
+            extras[f"{key}_ms"] = round(t_ms, 4)
         del tree
         # FRI prove wall clock at precision 2^23 (largest a reference proof can use, fri/src/utils.rs:88)
         lf = 23

@@ -1,6 +1,7 @@
 """GPU: the four-step multi-GPU NTT with libstark_hip local steps.  On the
 one-GPU test box both ranks share GPU 0 and exchange through gloo; the 8-GPU
 bench uses the same code with RCCL ("nccl")."""
+import datetime
 import os
 import socket
 
@@ -26,7 +27,9 @@ def _free_port():
 def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)   # a stuck rank prints its stack and exits
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=80))
     import stark_amd as S
     from stark_amd.distributed import GpuOps, cyclic_ntt
     torch.cuda.set_device(0)
@@ -52,9 +55,11 @@ def test_cyclic_ntt_gpu(world, log_n, inverse):
     procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
     for p in procs:
         p.start()
-    parts = dict(q.get(timeout=600) for _ in range(world))
+    parts = dict(q.get(timeout=110) for _ in range(world))
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
         assert p.exitcode == 0
     n = 1 << log_n
     M, c = n // world, n // world // world
@@ -117,7 +122,9 @@ def test_ntt_strided_tw(ctx, oracle, log_g, inverse):
 def _worker_merkle(rank, world, port, log_m, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)   # a stuck rank prints its stack and exits
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=80))
     import stark_amd as S
     from stark_amd.distributed import DistributedMerkle, GpuOps
     torch.cuda.set_device(0)
@@ -144,9 +151,11 @@ def test_distributed_merkle_gpu(world, log_m):
     procs = [ctx.Process(target=_worker_merkle, args=(r, world, port, log_m, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=600) for _ in range(world)]
+    res = [q.get(timeout=110) for _ in range(world)]
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
         assert p.exitcode == 0
     n = world << log_m
     blob = O.random_elements(n, 99).tobytes()
@@ -162,7 +171,9 @@ def test_distributed_merkle_gpu(world, log_m):
 def _worker(rank, world, port, log_n, inverse, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)   # a stuck rank prints its stack and exits
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=80))
     import stark_amd as S
     from stark_amd.distributed import GpuOps, four_step_ntt
     torch.cuda.set_device(0)
@@ -189,9 +200,11 @@ def test_four_step_ntt_gpu(world, log_n, inverse):
     procs = [ctx.Process(target=_worker, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
     for p in procs:
         p.start()
-    parts = dict(q.get(timeout=600) for _ in range(world))
+    parts = dict(q.get(timeout=110) for _ in range(world))
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
         assert p.exitcode == 0
     got = np.concatenate([parts[r] for r in range(world)])
     o = O.Oracle()
