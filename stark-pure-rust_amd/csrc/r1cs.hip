@@ -591,6 +591,70 @@ static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint3
   return coset_lde(ctx, coef, batch, out, log_steps, log_prec, 0, 0, tw_g1_inv, tw_g2, tw_g2, s);
 }
 
+// The proof's roots (prove.rs:71-94): g2 = 7^((p-1)/precision), g1 = g2^skips = xs[skips], and
+// h = g2^world (the generator of one rank's residue class of the domain), with the twiddle
+// tables of g2, g1^-1 (the LDE's iNTT) and h.
+struct ProofRoots {
+  HostFp g2;
+  uint64_t g2c[4];
+  const Twiddles *tw2 = nullptr, *tw1i = nullptr, *twh = nullptr;
+};
+
+static stark_status proof_roots(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t world,
+                                ProofRoots& R) {
+  const FieldHost& F = FieldHost::get();
+  uint64_t pm1[4];  // (p - 1) / precision
+  memcpy(pm1, FieldHost::kP, 32);
+  pm1[0] -= 1;
+  for (uint32_t k = 0; k < log_prec; ++k)
+    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
+  R.g2 = F.pow(F.from_u64(7), pm1, 4);
+  uint32_t log_g = 0;
+  while ((1u << log_g) < world) ++log_g;
+  uint64_t g1ic[4], hc[4];
+  F.to_canonical(R.g2, R.g2c);
+  F.to_canonical(F.inv(F.pow_u64(R.g2, (uint64_t)1 << (log_prec - log_steps))), g1ic);
+  F.to_canonical(F.pow_u64(R.g2, world), hc);
+  STARK_TRY(get_twiddles(ctx, R.g2c, log_prec, &R.tw2));
+  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &R.tw1i));
+  STARK_TRY(get_twiddles(ctx, hc, log_prec - log_g, &R.twh));
+  return STARK_OK;
+}
+
+// The proof's host-side constants (utils.rs:421-474): the boundary points x_k = g2^(skips w_k) of
+// the public wires' first uses (Montgomery, for Zb2), the coefficients of the interpolant I2
+// through (x_k, public value) and of I3 through (x_last, 1) (canonical): 2 n_pfi + 1 elements.
+static std::vector<fe> boundary_consts(const HostFp& g2, uint64_t prec, uint64_t skips, const uint64_t* public_wires,
+                                       const size_t* public_first_indices, size_t n_pfi, HostFp* x_last_out) {
+  const FieldHost& F = FieldHost::get();
+  const HostFp x_last = F.pow_u64(g2, prec - skips);
+  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
+  for (size_t i = 0; i < n_pfi; ++i) {
+    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
+    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
+  }
+  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
+  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
+  auto canon_fe = [&](const HostFp& x) {
+    uint64_t c[4];
+    F.to_canonical(x, c);
+    fe v;
+    for (int k = 0; k < 4; ++k) {
+      v.w[2 * k] = (uint32_t)c[k];
+      v.w[2 * k + 1] = (uint32_t)(c[k] >> 32);
+    }
+    return v;
+  };
+  std::vector<fe> h(2 * n_pfi + 2);
+  for (size_t i = 0; i < n_pfi; ++i) {
+    h[i] = to_dev(xv[i]);
+    h[n_pfi + i] = canon_fe(interp2[i]);
+  }
+  h[2 * n_pfi] = canon_fe(interp3[0]);
+  *x_last_out = x_last;
+  return h;
+}
+
 static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                size_t os, const uint64_t* public_wires, size_t n_public,
                                const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
@@ -617,23 +681,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     if (public_first_indices[2 * i] >= n_public || public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
 
   // Roots (prove.rs:71-94): g2 = 7^((p-1)/precision), g1 = g2^8.
-  uint64_t pm1[4];
-  {
-    const uint64_t* p = FieldHost::kP;
-    memcpy(pm1, p, 32);
-    pm1[0] -= 1;
-    for (uint32_t k = 0; k < log_prec; ++k)
-      for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
-  }
-  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
-  const HostFp g1 = F.pow_u64(g2, skips);
-  uint64_t g2c[4], g1ic[4];
-  F.to_canonical(g2, g2c);
-  F.to_canonical(F.inv(g1), g1ic);
-  const Twiddles* tw2 = nullptr;
-  const Twiddles* tw1i = nullptr;
-  STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
-  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
+  ProofRoots roots;
+  STARK_TRY(proof_roots(ctx, log_steps, log_prec, 1, roots));
+  const HostFp g2 = roots.g2;
+  const uint64_t* g2c = roots.g2c;
+  const Twiddles* tw2 = roots.tw2;
+  const Twiddles* tw1i = roots.tw1i;
   const Mont mc = mont();
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
@@ -661,33 +714,10 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(cv.commit(ctx, ctx->r1cs_arena));
 
   // Interpolants and boundary points (utils.rs:421-474), host side (#pub points).
-  const HostFp x_last = F.pow_u64(g2, prec - skips);
-  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
-  for (size_t i = 0; i < n_pfi; ++i) {
-    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
-    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
-  }
-  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
-  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
-  std::vector<fe> h(2 * n_pfi + 2);  // alive until the proof's final synchronisation
-  {
-    for (size_t i = 0; i < n_pfi; ++i) {
-      h[i] = to_dev(xv[i]);  // Montgomery x_k for Zb2
-      uint64_t c[4];
-      F.to_canonical(interp2[i], c);
-      for (int k = 0; k < 4; ++k) {
-        h[n_pfi + i].w[2 * k] = (uint32_t)c[k];
-        h[n_pfi + i].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
-      }
-    }
-    uint64_t c[4];
-    F.to_canonical(interp3[0], c);
-    for (int k = 0; k < 4; ++k) {
-      h[2 * n_pfi].w[2 * k] = (uint32_t)c[k];
-      h[2 * n_pfi].w[2 * k + 1] = (uint32_t)(c[k] >> 32);
-    }
-    STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
-  }
+  HostFp x_last;
+  // alive until the proof's final synchronisation
+  const std::vector<fe> h = boundary_consts(g2, prec, skips, public_wires, public_first_indices, n_pfi, &x_last);
+  STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).  The
   // inputs may be host or device pointers (the device trace builder's columns): hipMemcpyDefault.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
@@ -901,20 +931,10 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
   if (log_prec >= 24) return STARK_ERR_BAD_LENGTH;
   const uint64_t steps = (uint64_t)1 << log_steps, prec = (uint64_t)1 << log_prec;
   const uint64_t P = prec >> log_g;  // this rank's points r + world j
-  uint64_t pm1[4];
-  memcpy(pm1, FieldHost::kP, 32);
-  pm1[0] -= 1;
-  for (uint32_t k = 0; k < log_prec; ++k)
-    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
-  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
-  uint64_t g2c[4], g1ic[4], hc[4];
-  F.to_canonical(g2, g2c);
-  F.to_canonical(F.inv(F.pow_u64(g2, prec / steps)), g1ic);
-  F.to_canonical(F.pow_u64(g2, world), hc);
-  const Twiddles *tw2 = nullptr, *tw1i = nullptr, *twh = nullptr;
-  STARK_TRY(get_twiddles(ctx, g2c, log_prec, &tw2));
-  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
-  STARK_TRY(get_twiddles(ctx, hc, log_prec - log_g, &twh));
+  ProofRoots roots;
+  STARK_TRY(proof_roots(ctx, log_steps, log_prec, world, roots));
+  const HostFp g2 = roots.g2;
+  const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   for (size_t i = 0; i < n_pfi; ++i)
     if (public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
   DevBuf tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 P + n_pfi)
@@ -1072,21 +1092,11 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
     if (public_first_indices[2 * i] >= n_public || public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
 
   // Roots (prove.rs:71-94); h = g2^G generates this rank's coset of size P.
-  uint64_t pm1[4];
-  memcpy(pm1, FieldHost::kP, 32);
-  pm1[0] -= 1;
-  for (uint32_t k = 0; k < log_prec; ++k)
-    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
-  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
-  const HostFp g1 = F.pow_u64(g2, skips);
-  uint64_t g1ic[4], hc[4];
-  F.to_canonical(g2, d.g2c);
-  F.to_canonical(F.inv(g1), g1ic);
-  F.to_canonical(F.pow_u64(g2, world), hc);
-  const Twiddles *tw2 = nullptr, *tw1i = nullptr, *twh = nullptr;
-  STARK_TRY(get_twiddles(ctx, d.g2c, log_prec, &tw2));
-  STARK_TRY(get_twiddles(ctx, g1ic, log_steps, &tw1i));
-  STARK_TRY(get_twiddles(ctx, hc, log_prec - d.log_g, &twh));
+  ProofRoots roots;
+  STARK_TRY(proof_roots(ctx, log_steps, log_prec, world, roots));
+  const HostFp g2 = roots.g2;
+  memcpy(d.g2c, roots.g2c, 32);
+  const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   const Mont mc = mont();
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts;
@@ -1113,30 +1123,8 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_TRY(cv.commit(ctx, d.arena));
 
   // Interpolants and boundary points (utils.rs:421-474).
-  const HostFp x_last = F.pow_u64(g2, prec - skips);
-  std::vector<HostFp> xv(n_pfi), yv(n_pfi);
-  for (size_t i = 0; i < n_pfi; ++i) {
-    xv[i] = F.pow_u64(g2, skips * public_first_indices[2 * i + 1]);
-    yv[i] = host_fe(public_wires + 4 * public_first_indices[2 * i]);
-  }
-  const std::vector<HostFp> interp2 = lagrange_interp(xv, yv);
-  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
-  std::vector<fe> hc2(2 * n_pfi + 2);
-  auto canon_fe = [&](const HostFp& x) {
-    uint64_t c[4];
-    F.to_canonical(x, c);
-    fe v;
-    for (int k = 0; k < 4; ++k) {
-      v.w[2 * k] = (uint32_t)c[k];
-      v.w[2 * k + 1] = (uint32_t)(c[k] >> 32);
-    }
-    return v;
-  };
-  for (size_t i = 0; i < n_pfi; ++i) {
-    hc2[i] = to_dev(xv[i]);
-    hc2[n_pfi + i] = canon_fe(interp2[i]);
-  }
-  hc2[2 * n_pfi] = canon_fe(interp3[0]);
+  HostFp x_last;
+  const std::vector<fe> hc2 = boundary_consts(g2, prec, skips, public_wires, public_first_indices, n_pfi, &x_last);
   STARK_HIP(ctx, hipMemcpyAsync(consts, hc2.data(), hc2.size() * sizeof(fe), hipMemcpyHostToDevice, s));
   // Step columns (prove.rs:59-69), host or device sources.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
