@@ -138,10 +138,6 @@ class DistTree:
         return leaves, nodes
 
 
-def _from_bytes_le(b: bytes) -> int:
-    return int.from_bytes(b, "little") % P
-
-
 def _k_values(m_root: bytes) -> list:
     """prove.rs:274-283 (mk_seed + from_str of the BE digest)."""
     return [1] + [int.from_bytes(blake(m_root + bytes([i])), "big") % P for i in range(1, 11)]

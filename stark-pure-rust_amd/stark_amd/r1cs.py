@@ -15,7 +15,7 @@ import ctypes
 
 import numpy as np
 
-from . import Context, StarkError, _elems, _p64, _szp, _u64p, _vp, load_library
+from . import Context, StarkError, _elems, _p64, _szp, _vp, load_library
 
 
 class StarkProof:
