@@ -360,6 +360,34 @@ stark_status stark_memcpy_h2d(stark_ctx* ctx, void* d_dst, const void* h_src, si
 stark_status stark_memcpy_d2h(stark_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
 stark_status stark_ctx_synchronize(stark_ctx* ctx);
 
+/* ---- Verifier (packages/fri/src/fri.rs:226-404, packages/r1cs-stark/src/verify.rs:13-258,
+ * run.rs:454-526, 556-592) ------------------------------------------------------------
+ * STARK_OK: the proof verifies.  STARK_ERR_CHECK: the reference would fail an assert
+ * (an invalid proof).  STARK_ERR_BAD_ARG: malformed input, including a proof JSON that
+ * serde_json would not parse as StarkProof<BlakeDigest>.  The circuit-only extensions
+ * (K, F0-F2, IDX, PIDX over the precision domain) come from a prepared circuit on the
+ * GPU; the Merkle paths, FRI layer checks and the 80 spot checks run on the host. */
+
+/* verify_low_degree_proof (fri.rs:226-242): layers[0..n_layers) are the Middle layers,
+ * last_values[i] (last_lens[i] bytes) the Last layer's values; root_of_unity canonical. */
+stark_status stark_verify_low_degree_proof(const uint8_t merkle_root[32], const uint64_t root_of_unity[4],
+                                           const stark_fri_layer_parts* layers, size_t n_layers,
+                                           const uint8_t* const* last_values, const size_t* last_lens,
+                                           size_t n_last, size_t max_deg_plus_1, uint32_t exclude_multiples_of);
+/* verify_with_witness (run.rs:454-526) on a prepared circuit; public_wires = n_public
+ * 32-byte little-endian integers (n_public >= 1 + n_public_inputs + n_public_outputs). */
+stark_status stark_verify_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit,
+                                       const uint8_t* public_wires, size_t n_public, const char* proof_json,
+                                       size_t json_len);
+/* The same from the .r1cs bytes (read_r1cs + verify_with_witness). */
+stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
+                                     const uint8_t* public_wires, size_t n_public, const char* proof_json,
+                                     size_t json_len);
+/* verify_with_file_path (run.rs:556-592) on bytes: the public wires are the first
+ * 1 + n_public_inputs + n_public_outputs witness values. */
+stark_status stark_verify_with_witness(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                                       size_t wtns_len, const char* proof_json, size_t json_len);
+
 #ifdef __cplusplus
 }
 #endif

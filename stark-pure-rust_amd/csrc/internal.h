@@ -218,6 +218,24 @@ stark_status dprove_begin_prepared(stark_ctx* ctx, uint32_t world, uint32_t rank
                                    const size_t* permuted_indices, const uint64_t* coefficients,
                                    const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires, const fe* pre,
                                    void* stream, stark_dprove** out);
+// A circuit prepared for many proofs (r1cs_trace_dev.hip): everything of a proof that depends on
+// the .r1cs alone.  lde = circuit_lde's columns for (world, rank).
+struct PreparedCircuit {
+  DevBuf arena, lde;
+  size_t os = 0, n_wires = 0, n_public = 0;
+  uint32_t n_c = 0;
+  uint32_t world = 1, rank = 0;  // the points rank + world j of the precision domain (distributed prover)
+  uint64_t a_len = 0;
+  std::vector<size_t> pfi;
+  const uint32_t* base = nullptr;
+  const fe* coef = nullptr;
+  const uint8_t* flags = nullptr;
+  const uint64_t* perm = nullptr;
+  const uint32_t* slot_wire = nullptr;
+};
+stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c);
+// lagrange_interp (fri/src/poly_utils.rs:409-439): coefficients, low degree first (r1cs.hip).
+std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys);
 stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
                                       const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,
@@ -251,3 +269,13 @@ inline fe to_dev(const HostFp& x) {
 }
 
 }  // namespace stark
+
+// A prepared circuit handle (stark_r1cs_circuit_new, r1cs_trace_dev.hip).
+struct stark_r1cs_circuit {
+  stark_ctx* ctx = nullptr;
+  stark::PreparedCircuit c;
+  ~stark_r1cs_circuit() {
+    if (c.arena.ptr) hipFree(c.arena.ptr);
+    if (c.lde.ptr) hipFree(c.lde.ptr);
+  }
+};

@@ -487,7 +487,7 @@ static HostFp host_fe(const uint64_t* c) { return FieldHost::get().from_canonica
 
 // lagrange_interp (fri/src/poly_utils.rs:409-439): the unique interpolant,
 // n coefficients, Montgomery on the host.
-static std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys) {
+std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys) {
   const FieldHost& F = FieldHost::get();
   const size_t n = xs.size();
   std::vector<HostFp> root(1, F.one());

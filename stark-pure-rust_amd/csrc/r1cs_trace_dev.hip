@@ -334,21 +334,8 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // permutation, the public wires' first uses, and the LDEs of K, F0, F1, F2, IDX
 // and PIDX.  A proof for a new witness then builds S and P (wit_fill_kernel) and
 // extends only S, P and A: 3 of the 9 LDE columns.
-struct PreparedCircuit {
-  DevBuf arena, lde;
-  size_t os = 0, n_wires = 0, n_public = 0;
-  uint32_t n_c = 0;
-  uint32_t world = 1, rank = 0;  // the points rank + world j of the precision domain (distributed prover)
-  uint64_t a_len = 0;
-  std::vector<size_t> pfi;
-  const uint32_t* base = nullptr;
-  const fe* coef = nullptr;
-  const uint8_t* flags = nullptr;
-  const uint64_t* perm = nullptr;
-  const uint32_t* slot_wire = nullptr;
-};
 
-static stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c) {
+stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c) {
   R1csHeader hd;
   stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
   if (st != STARK_OK) return st;
@@ -500,18 +487,6 @@ static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, co
   return STARK_OK;
 }
 
-}  // namespace stark
-
-struct stark_r1cs_circuit {
-  stark_ctx* ctx = nullptr;
-  stark::PreparedCircuit c;
-  ~stark_r1cs_circuit() {
-    if (c.arena.ptr) hipFree(c.arena.ptr);
-    if (c.lde.ptr) hipFree(c.lde.ptr);
-  }
-};
-
-namespace stark {
 }  // namespace stark
 
 using namespace stark;

@@ -1,0 +1,565 @@
+// Verifier: verify_low_degree_proof (packages/fri/src/fri.rs:226-404) and
+// verify_with_witness + verify_r1cs_proof (packages/r1cs-stark/src/run.rs:454-526,
+// verify.rs:13-258).
+//
+// The verifier's data-parallel part is the same as the prover's: the
+// extensions of K, F0-F2, IDX and PIDX over the precision domain (read at the
+// 80 spot-check positions).  It is taken from a prepared circuit
+// (circuit_build: slot layout, flags, permutation and those LDEs on the GPU);
+// the rest -- Merkle paths, the FRI layer checks and the 80 spot checks -- is
+// a few thousand hashes and products on the host.
+//
+// Status: STARK_OK for a valid proof, STARK_ERR_CHECK where the reference
+// would fail an assert (an invalid proof), STARK_ERR_BAD_ARG for malformed
+// input (including the reference's Err results).
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "blake2s.h"
+
+namespace stark {
+namespace {
+
+// ---- the proof, as serde_json writes it (utils.rs:122-130, merkle_tree.rs:14-18, fri.rs:16-26) ----
+
+struct Branch {  // commitment::merkle_tree::Proof
+  std::vector<uint8_t> leaf;
+  std::vector<uint8_t> nodes;  // 32 B each, leaf -> root
+};
+
+struct FriIn {  // FriProof::Middle { root2, column_branches, poly_branches } | Last { last }
+  bool last = false;
+  uint8_t root2[32] = {0};
+  std::vector<Branch> col, poly;
+  std::vector<std::vector<uint8_t>> last_vals;
+};
+
+struct ProofIn {
+  uint8_t m_root[32], l_root[32], a_root[32];
+  std::vector<Branch> main, lcomb;
+  std::vector<FriIn> fri;
+};
+
+// A reader for exactly this schema: objects with string keys, arrays, u8 numbers.
+class Json {
+ public:
+  Json(const char* s, size_t n) : p_(s), e_(s + n) {}
+  bool ok = true;
+
+  bool accept(char c) {
+    ws();
+    if (p_ < e_ && *p_ == c) {
+      ++p_;
+      return true;
+    }
+    return false;
+  }
+  void expect(char c) {
+    if (!accept(c)) ok = false;
+  }
+  std::string key() {
+    std::string k;
+    expect('"');
+    while (ok && p_ < e_ && *p_ != '"') k.push_back(*p_++);
+    if (p_ >= e_) ok = false;
+    ++p_;
+    expect(':');
+    return k;
+  }
+  void bytes(std::vector<uint8_t>& out) {
+    out.clear();
+    expect('[');
+    if (!ok || accept(']')) return;
+    do {
+      ws();
+      unsigned v = 0;
+      int nd = 0;
+      while (p_ < e_ && *p_ >= '0' && *p_ <= '9' && nd < 4) {
+        v = 10 * v + (unsigned)(*p_++ - '0');
+        ++nd;
+      }
+      if (nd == 0 || v > 255) {
+        ok = false;
+        return;
+      }
+      out.push_back((uint8_t)v);
+    } while (ok && accept(','));
+    expect(']');
+  }
+  void digest(uint8_t out[32]) {
+    std::vector<uint8_t> v;
+    bytes(v);
+    if (v.size() != 32) ok = false;
+    if (ok) memcpy(out, v.data(), 32);
+  }
+  void branch(Branch& b) {
+    expect('{');
+    bool has_leaf = false, has_nodes = false;
+    do {
+      const std::string k = key();
+      if (k == "leaf") {
+        bytes(b.leaf);
+        has_leaf = true;
+      } else if (k == "nodes") {
+        expect('[');
+        if (!accept(']')) {
+          do {
+            uint8_t d[32];
+            digest(d);
+            b.nodes.insert(b.nodes.end(), d, d + 32);
+          } while (ok && accept(','));
+          expect(']');
+        }
+        has_nodes = true;
+      } else {
+        ok = false;
+      }
+    } while (ok && accept(','));
+    expect('}');
+    if (!has_leaf || !has_nodes) ok = false;
+  }
+  void branches(std::vector<Branch>& v) {
+    expect('[');
+    if (!ok || accept(']')) return;
+    do {
+      v.emplace_back();
+      branch(v.back());
+    } while (ok && accept(','));
+    expect(']');
+  }
+  void fri_layer(FriIn& f) {
+    expect('{');
+    const std::string tag = key();
+    expect('{');
+    if (tag == "Middle") {
+      bool r = false, c = false, q = false;
+      do {
+        const std::string k = key();
+        if (k == "root2") {
+          digest(f.root2);
+          r = true;
+        } else if (k == "column_branches") {
+          branches(f.col);
+          c = true;
+        } else if (k == "poly_branches") {
+          branches(f.poly);
+          q = true;
+        } else {
+          ok = false;
+        }
+      } while (ok && accept(','));
+      if (!(r && c && q)) ok = false;
+    } else if (tag == "Last") {
+      f.last = true;
+      if (key() != "last") ok = false;
+      expect('[');
+      if (ok && !accept(']')) {
+        do {
+          f.last_vals.emplace_back();
+          bytes(f.last_vals.back());
+        } while (ok && accept(','));
+        expect(']');
+      }
+    } else {
+      ok = false;
+    }
+    expect('}');
+    expect('}');
+  }
+  void stark_proof(ProofIn& pr) {
+    expect('{');
+    int seen = 0;
+    do {
+      const std::string k = key();
+      if (k == "m_root") digest(pr.m_root), seen |= 1;
+      else if (k == "l_root") digest(pr.l_root), seen |= 2;
+      else if (k == "a_root") digest(pr.a_root), seen |= 4;
+      else if (k == "main_branches") branches(pr.main), seen |= 8;
+      else if (k == "linear_comb_branches") branches(pr.lcomb), seen |= 16;
+      else if (k == "fri_proof") {
+        expect('[');
+        if (!accept(']')) {
+          do {
+            pr.fri.emplace_back();
+            fri_layer(pr.fri.back());
+          } while (ok && accept(','));
+          expect(']');
+        }
+        seen |= 32;
+      } else {
+        ok = false;
+      }
+    } while (ok && accept(','));
+    expect('}');
+    ws();
+    if (seen != 63 || p_ != e_) ok = false;
+  }
+
+ private:
+  void ws() {
+    while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+  }
+  const char* p_;
+  const char* e_;
+};
+
+// ---- field helpers ----
+
+// T::from_bytes_le (ff_utils/src/fp.rs:70-77): the little-endian integer of the bytes mod p.
+HostFp fe_from_bytes(const std::vector<uint8_t>& b) {
+  const FieldHost& F = FieldHost::get();
+  if (b.size() <= 32) return F.from_bytes_le(b.data(), b.size());
+  HostFp acc = F.zero();
+  const HostFp base = F.from_u64(256);
+  for (size_t i = b.size(); i-- > 0;) acc = F.add(F.mul(acc, base), F.from_u64(b[i]));
+  return acc;
+}
+
+HostFp eval_poly(const std::vector<HostFp>& poly, const HostFp& x) {  // eval_poly_at, poly_utils.rs:93-102
+  const FieldHost& F = FieldHost::get();
+  HostFp acc = F.zero();
+  for (size_t k = poly.size(); k-- > 0;) acc = F.add(F.mul(acc, x), poly[k]);
+  return acc;
+}
+
+// Proof::validate (merkle_tree.rs:25-43) for each (index, proof) pair; verify_multi_branch
+// (:46-58) zips, so every index needs its proof.
+bool branches_valid(const uint8_t root[32], const std::vector<size_t>& idx, const std::vector<Branch>& br) {
+  if (br.size() < idx.size()) return false;
+  for (size_t i = 0; i < idx.size(); ++i) {
+    uint8_t cur[32], msg[64];
+    b2s_host(br[i].leaf.data(), br[i].leaf.size(), cur);
+    size_t pos = idx[i];
+    for (size_t d = 0; d < br[i].nodes.size() / 32; ++d) {
+      const uint8_t* sib = br[i].nodes.data() + 32 * d;
+      memcpy(msg, pos % 2 == 0 ? cur : sib, 32);
+      memcpy(msg + 32, pos % 2 == 0 ? sib : cur, 32);
+      b2s_host(msg, 64, cur);
+      pos /= 2;
+    }
+    if (memcmp(cur, root, 32) != 0) return false;
+  }
+  return true;
+}
+
+bool sampler(const uint8_t seed[32], size_t modulus, uint32_t count, uint32_t excl, std::vector<size_t>& out) {
+  if (modulus > 0xFFFFFFFFull) return false;
+  std::vector<uint32_t> v(count);
+  if (stark_get_pseudorandom_indices(seed, 32, (uint32_t)modulus, count, excl, v.data()) != STARK_OK) return false;
+  out.assign(v.begin(), v.end());
+  return true;
+}
+
+// verify_low_degree_proof_rec (fri.rs:244-404).
+stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std::vector<FriIn>& proof,
+                        size_t max_deg_plus_1, uint32_t excl) {
+  const FieldHost& F = FieldHost::get();
+  if (proof.empty()) return STARK_ERR_BAD_ARG;
+  uint64_t rou_deg = 1;
+  for (HostFp t = root; !FieldHost::eq(t, F.one()); t = F.mul(t, t)) {
+    rou_deg *= 2;
+    if (rou_deg > ((uint64_t)1 << 28)) return STARK_ERR_BAD_ARG;  // not a root of unity of 2-power order
+  }
+  if (rou_deg < 4 && proof.size() > 1) return STARK_ERR_BAD_ARG;
+  uint8_t m_root[32];
+  memcpy(m_root, merkle_root_in, 32);
+  HostFp quartic[4] = {F.one(), F.one(), F.one(), F.one()};
+  if (rou_deg >= 4)
+    for (int j = 1; j < 4; ++j) quartic[j] = F.pow_u64(root, rou_deg / 4 * (uint64_t)j);
+  const HostFp inv4 = F.inv(F.from_u64(4));
+  for (size_t l = 0; l + 1 < proof.size(); ++l) {
+    const FriIn& L = proof[l];
+    if (L.last) return STARK_ERR_BAD_ARG;  // "FRI proofs must consist of FriProof::Middle except the last element."
+    const HostFp special_x = F.from_bytes_le(m_root, 32);
+    const size_t q = rou_deg / 4;
+    std::vector<size_t> ys;
+    if (!sampler(L.root2, q, 40, excl, ys)) return STARK_ERR_CHECK;  // get_pseudorandom_indices panics
+    std::vector<size_t> poly_pos;
+    for (size_t y : ys)
+      for (size_t j = 0; j < 4; ++j) poly_pos.push_back(j * q + y);
+    if (!branches_valid(L.root2, ys, L.col) || !branches_valid(m_root, poly_pos, L.poly)) return STARK_ERR_CHECK;
+    for (size_t i = 0; i < ys.size(); ++i) {
+      // The cubic through (x1 zeta^j, row_j) at special_x (multi_interp_4 + eval_quartic,
+      // poly_utils.rs:442-511): Lagrange weights prod_{k != j}(sx - x_k) / (4 x1^3 zeta^(3j)).
+      const HostFp x1 = F.pow_u64(root, ys[i]);
+      HostFp xs[4], num[4];
+      for (int j = 0; j < 4; ++j) xs[j] = F.mul(quartic[j], x1);
+      for (int j = 0; j < 4; ++j) {
+        num[j] = F.one();
+        for (int k = 0; k < 4; ++k)
+          if (k != j) num[j] = F.mul(num[j], F.sub(special_x, xs[k]));
+      }
+      const HostFp x1_3 = F.mul(F.mul(x1, x1), x1);
+      const HostFp inv_den = F.mul(inv4, F.inv(x1_3));  // 1 / (4 x1^3); zeta^(-3j) = zeta^j
+      HostFp val = F.zero();
+      for (int j = 0; j < 4; ++j)
+        val = F.add(val, F.mul(F.mul(fe_from_bytes(L.poly[i * 4 + j].leaf), num[j]), F.mul(inv_den, quartic[j])));
+      if (!FieldHost::eq(val, fe_from_bytes(L.col[i].leaf))) return STARK_ERR_CHECK;  // assert_eq (fri.rs:337)
+    }
+    memcpy(m_root, L.root2, 32);
+    root = F.pow_u64(root, 4);
+    max_deg_plus_1 /= 4;
+    rou_deg /= 4;
+    if (rou_deg < 4 && l + 2 < proof.size()) return STARK_ERR_BAD_ARG;
+  }
+  const FriIn& last = proof.back();
+  if (!last.last) return STARK_ERR_BAD_ARG;  // "The last element of FRI proofs must be FriProof::Last."
+  if (max_deg_plus_1 < 16 / 2) return STARK_ERR_CHECK;           // MIN_DEG_DIRECT_CHECKING / 2 (fri.rs:348-351)
+  const size_t n = last.last_vals.size();
+  if (n <= max_deg_plus_1) return STARK_ERR_CHECK;               // fri.rs:359
+  if (n & (n - 1)) return STARK_ERR_CHECK;                       // MerkleProofInPlace::update (merkle_proof_in_place.rs:113)
+  {
+    // m_tree over the raw last values (fri.rs:367-372).
+    std::vector<std::vector<uint8_t>> lv;
+    std::vector<uint8_t> cur(32 * n);
+    for (size_t i = 0; i < n; ++i) b2s_host(last.last_vals[i].data(), last.last_vals[i].size(), &cur[32 * i]);
+    for (size_t w = n; w > 1; w /= 2) {
+      std::vector<uint8_t> up(32 * (w / 2));
+      for (size_t i = 0; i < w / 2; ++i) b2s_host(&cur[64 * i], 64, &up[32 * i]);
+      cur.swap(up);
+    }
+    if (memcmp(cur.data(), m_root, 32) != 0) return STARK_ERR_CHECK;
+  }
+  // Degree of the last values (fri.rs:377-401): xs = expand_root_of_unity(root).
+  std::vector<HostFp> xs(1, F.one());
+  for (HostFp t = root; !FieldHost::eq(t, F.one()); t = F.mul(t, root)) xs.push_back(t);
+  std::vector<size_t> pts;
+  for (size_t pos = 0; pos < n; ++pos)
+    if (excl == 0 || pos % excl != 0) pts.push_back(pos);
+  if (pts.size() < max_deg_plus_1) return STARK_ERR_CHECK;  // split_off panics
+  for (size_t pos : pts)
+    if (pos >= xs.size()) return STARK_ERR_CHECK;  // xs[pos] out of bounds
+  std::vector<HostFp> xv, yv;
+  for (size_t i = 0; i < max_deg_plus_1; ++i) {
+    xv.push_back(xs[pts[i]]);
+    yv.push_back(fe_from_bytes(last.last_vals[pts[i]]));
+  }
+  const std::vector<HostFp> poly = lagrange_interp(xv, yv);
+  for (size_t i = max_deg_plus_1; i < pts.size(); ++i)
+    if (!FieldHost::eq(eval_poly(poly, xs[pts[i]]), fe_from_bytes(last.last_vals[pts[i]]))) return STARK_ERR_CHECK;
+  return STARK_OK;
+}
+
+uint32_t log2_ceil_ref(size_t v) {  // log2_ceil (r1cs-stark/src/utils.rs:14-23)
+  uint32_t l = 1;
+  for (size_t t = v; t > 1; t /= 2) ++l;
+  return l;
+}
+
+}  // namespace
+
+// verify_r1cs_proof (verify.rs:13-258) for a prepared circuit; `pub_bytes` holds the public
+// wires as 32-byte little-endian integers (from_bytes_le, run.rs:477-480).
+static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const uint8_t* pub_bytes, size_t n_public,
+                                const ProofIn& pr) {
+  const FieldHost& F = FieldHost::get();
+  if (c.world != 1) return STARK_ERR_BAD_ARG;
+  if (n_public < c.n_public) return STARK_ERR_BAD_ARG;  // public_wires[w] for w < n_public (run.rs:503-509)
+  std::vector<HostFp> pub(c.n_public);
+  for (size_t i = 0; i < c.n_public; ++i) pub[i] = F.from_bytes_le(pub_bytes + 32 * i, 32);
+  if (!FieldHost::eq(pub[0], F.one())) return STARK_ERR_CHECK;  // run.rs:480
+  const size_t os = c.os;
+  const uint32_t log_steps = log2_ceil_ref(os - 1);
+  const uint64_t steps = std::max<uint64_t>((uint64_t)1 << log_steps, 8), prec = 8 * steps, skips = 8;
+  uint64_t pm1[4];  // g2 = 7^((p-1)/precision) (verify.rs:55-63)
+  memcpy(pm1, FieldHost::kP, 32);
+  pm1[0] -= 1;
+  for (uint64_t t = prec; t > 1; t /= 2)
+    for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
+  const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
+  // FRI on the linear combination (verify.rs:80-84).
+  stark_status st = verify_fri(pr.l_root, g2, pr.fri, prec / 4, (uint32_t)skips);
+  if (st != STARK_OK) return st;
+  // Spot checks (verify.rs:86-118).
+  std::vector<size_t> positions, aug;
+  if (!sampler(pr.l_root, prec, 80, (uint32_t)skips, positions)) return STARK_ERR_CHECK;
+  for (size_t j : positions) {
+    aug.push_back(j);
+    aug.push_back((j + prec - skips) % prec);
+    aug.push_back((j + os / 3 * skips) % prec);
+    aug.push_back((j + os / 3 * 2 * skips) % prec);
+  }
+  if (!branches_valid(pr.m_root, aug, pr.main) || !branches_valid(pr.l_root, positions, pr.lcomb))
+    return STARK_ERR_CHECK;
+  for (size_t i = 0; i < aug.size(); ++i)
+    if (pr.main[i].leaf.size() < 256) return STARK_ERR_CHECK;  // m_branch[k] chunks (verify.rs:185-200)
+  // K, F0-F2, IDX, PIDX at the positions: the circuit's extensions (K, F0-F2 stored as Montgomery
+  // images, IDX and PIDX canonical), gathered in one launch.
+  const size_t n_pos = positions.size();
+  std::vector<uint8_t> got(6 * n_pos * 32);
+  {
+    stark_open_req req[6];
+    for (int k = 0; k < 6; ++k)
+      req[k] = stark_open_req{nullptr, (const uint8_t*)c.lde.ptr + (size_t)k * prec * 32, 32, prec,
+                              positions.data(), n_pos, got.data() + (size_t)k * n_pos * 32, nullptr};
+    st = stark_open_batch(ctx, req, 6, nullptr);
+    if (st != STARK_OK) return st;
+  }
+  auto col_val = [&](int k, size_t i) {
+    HostFp v;
+    memcpy(v.v, got.data() + ((size_t)k * n_pos + i) * 32, 32);
+    while (FieldHost::ge_p(v.v)) FieldHost::sub_p_in_place(v.v);
+    return k < 4 ? v : F.from_canonical(v.v);  // a Montgomery image's bits are the HostFp itself
+  };
+  // Boundary interpolants (verify.rs:151-155, utils.rs:421-474) and Zb2's points.
+  std::vector<HostFp> bx, by;
+  for (size_t i = 0; i + 1 < c.pfi.size(); i += 2) {
+    bx.push_back(F.pow_u64(g2, skips * c.pfi[i + 1]));
+    by.push_back(pub[c.pfi[i]]);
+  }
+  const std::vector<HostFp> interp2 = lagrange_interp(bx, by);
+  const HostFp x_last = F.pow_u64(g2, (steps - 1) * skips);
+  const std::vector<HostFp> interp3 = lagrange_interp({x_last}, {F.one()});
+  // r (utils.rs:272-290) and k (verify.rs:164-173).
+  HostFp r[3];
+  {
+    std::vector<size_t> rnd;
+    if (!sampler(pr.a_root, prec, 24, 0, rnd)) return STARK_ERR_CHECK;
+    for (int k = 0; k < 3; ++k) {
+      uint8_t be[32];
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t v = (uint32_t)rnd[8 * k + i];
+        be[4 * i] = (uint8_t)(v >> 24);
+        be[4 * i + 1] = (uint8_t)(v >> 16);
+        be[4 * i + 2] = (uint8_t)(v >> 8);
+        be[4 * i + 3] = (uint8_t)v;
+      }
+      r[k] = F.from_bytes_le(be, 32);
+    }
+  }
+  HostFp kk[11];
+  kk[0] = F.one();
+  for (int i = 1; i < 11; ++i) {
+    uint8_t msg[33], h[32], le[32];
+    memcpy(msg, pr.m_root, 32);
+    msg[32] = (uint8_t)i;
+    b2s_host(msg, 33, h);
+    for (int b = 0; b < 32; ++b) le[b] = h[31 - b];  // from_str of the big-endian integer
+    kk[i] = F.from_bytes_le(le, 32);
+  }
+  for (size_t i = 0; i < positions.size(); ++i) {
+    const HostFp x = F.pow_u64(g2, positions[i]);
+    auto leaf = [&](int b, int chunk) {
+      std::vector<uint8_t> v(pr.main[4 * i + b].leaf.begin() + 32 * chunk,
+                             pr.main[4 * i + b].leaf.begin() + 32 * chunk + 32);
+      return fe_from_bytes(v);
+    };
+    const HostFp p_x = leaf(0, 0), p_prev = leaf(1, 0), p_w = leaf(2, 0), p_2w = leaf(3, 0);
+    const HostFp a_x = leaf(0, 1), a_prev = leaf(1, 1), s_x = leaf(0, 2), d1 = leaf(0, 3), d2 = leaf(0, 4),
+                 d3 = leaf(0, 5), b2 = leaf(0, 6), b3 = leaf(0, 7);
+    const HostFp z = F.sub(F.pow_u64(x, steps), F.one());  // best_fft of X^steps - 1 at x
+    const HostFp k_x = col_val(0, i), f0 = col_val(1, i), f1 = col_val(2, i), f2 = col_val(3, i);
+    const HostFp ext_idx = col_val(4, i), ext_pidx = col_val(5, i);
+    // Q1 = Z D1, Q2 = Z D2 (verify.rs:208-219)
+    if (!FieldHost::eq(F.mul(f0, F.sub(F.sub(p_x, F.mul(f1, p_prev)), F.mul(k_x, s_x))), F.mul(z, d1)))
+      return STARK_ERR_CHECK;
+    if (!FieldHost::eq(F.mul(f2, F.sub(p_2w, F.mul(p_x, p_w))), F.mul(z, d2))) return STARK_ERR_CHECK;
+    // Q3 = Z D3 (verify.rs:221-225)
+    const HostFp rs = F.mul(r[2], s_x);
+    const HostFp nmr = F.add(F.add(r[0], F.mul(r[1], ext_idx)), rs);
+    const HostFp dnm = F.add(F.add(r[0], F.mul(r[1], ext_pidx)), rs);
+    if (!FieldHost::eq(F.sub(F.mul(a_x, dnm), F.mul(a_prev, nmr)), F.mul(z, d3))) return STARK_ERR_CHECK;
+    // Boundary constraints (verify.rs:227-238)
+    HostFp zb2 = F.one();
+    for (const HostFp& xk : bx) zb2 = F.mul(zb2, F.sub(x, xk));
+    if (!FieldHost::eq(F.sub(s_x, eval_poly(interp2, x)), F.mul(zb2, b2))) return STARK_ERR_CHECK;
+    if (!FieldHost::eq(F.sub(a_x, eval_poly(interp3, x)), F.mul(F.sub(x, x_last), b3))) return STARK_ERR_CHECK;
+    // The linear combination (verify.rs:240-254)
+    const HostFp xs = F.pow_u64(x, steps);
+    HostFp l = F.mul(kk[0], d1);
+    l = F.add(l, F.mul(kk[1], d2));
+    l = F.add(l, F.mul(kk[2], d3));
+    l = F.add(l, F.mul(kk[3], p_x));
+    l = F.add(l, F.mul(F.mul(kk[4], p_x), xs));
+    l = F.add(l, F.mul(kk[5], b2));
+    l = F.add(l, F.mul(F.mul(kk[6], b2), xs));
+    l = F.add(l, F.mul(kk[7], b3));
+    l = F.add(l, F.mul(F.mul(kk[8], b3), xs));
+    l = F.add(l, F.mul(kk[9], a_x));
+    l = F.add(l, F.mul(kk[10], s_x));
+    if (!FieldHost::eq(fe_from_bytes(pr.lcomb[i].leaf), l)) return STARK_ERR_CHECK;
+  }
+  return STARK_OK;
+}
+
+}  // namespace stark
+
+using namespace stark;
+
+extern "C" {
+
+stark_status stark_verify_low_degree_proof(const uint8_t merkle_root[32], const uint64_t root_of_unity[4],
+                                           const stark_fri_layer_parts* layers, size_t n_layers,
+                                           const uint8_t* const* last_values, const size_t* last_lens, size_t n_last,
+                                           size_t max_deg_plus_1, uint32_t exclude_multiples_of) {
+  if (!merkle_root || !root_of_unity || (n_layers && !layers) || (n_last && (!last_values || !last_lens)))
+    return STARK_ERR_BAD_ARG;
+  std::vector<FriIn> proof(n_layers + 1);
+  for (size_t l = 0; l < n_layers; ++l) {
+    const stark_fri_layer_parts& P = layers[l];
+    if (!P.root2) return STARK_ERR_BAD_ARG;
+    memcpy(proof[l].root2, P.root2, 32);
+    for (int which = 0; which < 2; ++which) {
+      const stark_branches& B = which ? P.poly : P.column;
+      std::vector<Branch>& out = which ? proof[l].poly : proof[l].col;
+      if (B.k && (!B.leaves || (B.depth && !B.nodes))) return STARK_ERR_BAD_ARG;
+      for (size_t i = 0; i < B.k; ++i) {
+        Branch b;
+        b.leaf.assign(B.leaves + i * B.leaf_len, B.leaves + (i + 1) * B.leaf_len);
+        b.nodes.assign(B.nodes + i * B.depth * 32, B.nodes + (i + 1) * B.depth * 32);
+        out.push_back(std::move(b));
+      }
+    }
+  }
+  proof[n_layers].last = true;
+  for (size_t i = 0; i < n_last; ++i) proof[n_layers].last_vals.emplace_back(last_values[i], last_values[i] + last_lens[i]);
+  const FieldHost& F = FieldHost::get();
+  return verify_fri(merkle_root, F.from_canonical(root_of_unity), proof, max_deg_plus_1, exclude_multiples_of);
+}
+
+stark_status stark_verify_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit,
+                                       const uint8_t* public_wires, size_t n_public, const char* proof_json,
+                                       size_t json_len) {
+  if (!ctx || !circuit || circuit->ctx != ctx || !public_wires || !proof_json || n_public == 0)
+    return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  ProofIn pr;
+  Json j(proof_json, json_len);
+  j.stark_proof(pr);
+  if (!j.ok) return STARK_ERR_BAD_ARG;  // serde_json::from_reader fails (run.rs:579)
+  return verify_r1cs(ctx, circuit->c, public_wires, n_public, pr);
+}
+
+stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
+                                     const uint8_t* public_wires, size_t n_public, const char* proof_json,
+                                     size_t json_len) {
+  if (!ctx || !r1cs || !public_wires || !proof_json || n_public == 0) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  stark_r1cs_circuit circ;
+  circ.ctx = ctx;
+  stark_status st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
+  hipStreamSynchronize(ctx->stream);
+  if (st != STARK_OK) return st;
+  return stark_verify_r1cs_circuit(ctx, &circ, public_wires, n_public, proof_json, json_len);
+}
+
+stark_status stark_verify_with_witness(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
+                                       size_t wtns_len, const char* proof_json, size_t json_len) {
+  if (!ctx || !r1cs || !wtns || !proof_json) return STARK_ERR_BAD_ARG;
+  R1csHeader hd;
+  WtnsHeader wh;
+  stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
+  if (st == STARK_OK) st = parse_wtns_header(wtns, wtns_len, &wh);
+  if (st != STARK_OK) return st;
+  // public_wires = witness[..1 + n_public_inputs + n_public_outputs] (run.rs:582-585)
+  const size_t n_public = 1 + (size_t)hd.n_pub_in + hd.n_pub_out;
+  if (n_public > wh.n_wit) return STARK_ERR_BAD_ARG;
+  std::vector<uint8_t> pub(32 * n_public, 0);
+  for (size_t i = 0; i < n_public; ++i) memcpy(&pub[32 * i], wtns + wh.values_off + i * wh.field_size, wh.field_size);
+  return stark_verify_r1cs_bytes(ctx, r1cs, r1cs_len, pub.data(), n_public, proof_json, json_len);
+}
+
+}  // extern "C"

@@ -132,6 +132,14 @@ _SIGNATURES = {
     "stark_dprove_rows": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_dprove_lincomb": ([_vp, _u8p, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_dprove_free": ([_vp], None),
+    "stark_verify_low_degree_proof": ([_u8p, _u64p, _vp, ctypes.c_size_t, _vp, _szp, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_uint32], ctypes.c_int),
+    "stark_verify_r1cs_circuit": ([_vp, _vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t],
+                                  ctypes.c_int),
+    "stark_verify_r1cs_bytes": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                 ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "stark_verify_with_witness": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                   ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
 }
 
 _lib = None

@@ -39,6 +39,7 @@ import torch
 import torch.distributed as dist
 
 from . import P, blake, get_pseudorandom_indices
+from .verify import _Branches, _FriLayer
 
 EXTENSION_FACTOR = 8        # r1cs-stark/src/utils.rs:135
 SPOT_CHECK_SECURITY_FACTOR = 80  # utils.rs:136
@@ -141,15 +142,6 @@ class DistTree:
 def _k_values(m_root: bytes) -> list:
     """prove.rs:274-283 (mk_seed + from_str of the BE digest)."""
     return [1] + [int.from_bytes(blake(m_root + bytes([i])), "big") % P for i in range(1, 11)]
-
-
-class _Branches(ctypes.Structure):
-    _fields_ = [("leaves", ctypes.c_char_p), ("nodes", ctypes.c_char_p), ("k", ctypes.c_size_t),
-                ("leaf_len", ctypes.c_size_t), ("depth", ctypes.c_size_t)]
-
-
-class _FriLayer(ctypes.Structure):
-    _fields_ = [("root2", ctypes.c_char_p), ("column", _Branches), ("poly", _Branches)]
 
 
 def _branches(opened, keep: list) -> _Branches:

@@ -1,0 +1,70 @@
+"""The product verifier's host part: stark_verify_low_degree_proof (fri.rs:226-404)
+in libstark_hip.so needs no GPU, so it runs here.  It must accept the oracle's FRI
+proofs (the oracle's prover is pinned by the golden vectors, test_oracle_kat.py),
+agree with the restated verifier (oracle/stark_verify.py), and reject tampering and
+proofs of values that are not of low degree."""
+import copy
+import json
+
+import pytest
+
+import oracle as O
+from stark_verify import verify_low_degree_proof as ref_verify
+
+S = pytest.importorskip("stark_amd")
+from stark_amd.verify import verify_low_degree_proof  # noqa: E402
+
+
+def _proof(oracle, log_n, excl, seed=5, deg_div=4, low=True):
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    if low:
+        vals = oracle.best_fft(O.random_elements(n // deg_div, seed), w, log_n, cpus=4)
+    else:
+        vals = O.random_elements(n, seed)
+    js = oracle.prove_low_degree_json(vals, w, n // deg_div, excl, chunks=4)
+    root, _ = oracle.merkle(b"".join(O.to_bytes_le(x) for x in O.from_limbs(vals)), n, 32, [], chunks=4)
+    return root, w, json.loads(js), n // deg_div
+
+
+@pytest.mark.parametrize("log_n,excl", [(8, 8), (10, 0), (12, 8), (13, 4)])
+def test_accepts_oracle_proofs(oracle, log_n, excl):
+    root, w, proof, md = _proof(oracle, log_n, excl)
+    assert ref_verify(root, w, copy.deepcopy(proof), md, excl)
+    assert verify_low_degree_proof(root, w, proof, md, excl)
+
+
+def _expect_reject(root, w, proof, md, excl):
+    with pytest.raises(AssertionError):
+        verify_low_degree_proof(root, w, proof, md, excl)
+    with pytest.raises(AssertionError):
+        ref_verify(root, w, copy.deepcopy(proof), md, excl)
+
+
+def test_rejects_tampering(oracle):
+    root, w, proof, md = _proof(oracle, 12, 8)
+    p = copy.deepcopy(proof)
+    p[0]["Middle"]["column_branches"][3]["leaf"][0] ^= 1       # Merkle path no longer reaches root2
+    _expect_reject(root, w, p, md, 8)
+    p = copy.deepcopy(proof)
+    p[0]["Middle"]["poly_branches"][5]["nodes"][0][7] ^= 0x40
+    _expect_reject(root, w, p, md, 8)
+    p = copy.deepcopy(proof)
+    p[-1]["Last"]["last"][9][0] ^= 2                              # last layer root mismatch
+    _expect_reject(root, w, p, md, 8)
+    _expect_reject(bytes(32), w, proof, md, 8)                     # wrong commitment
+    _expect_reject(root, w, proof, md // 8, 8)                     # claimed degree bound too low
+
+
+def test_rejects_high_degree(oracle):
+    """Random values (full degree) with a proof made anyway: the column or last-layer checks fail."""
+    root, w, proof, md = _proof(oracle, 12, 8, low=False)
+    _expect_reject(root, w, proof, md, 8)
+
+
+def test_malformed_raises(oracle):
+    root, w, proof, md = _proof(oracle, 10, 8)
+    with pytest.raises(S.StarkError):
+        verify_low_degree_proof(root, w, proof[:-1], md, 8)        # no Last layer
+    with pytest.raises(S.StarkError):
+        verify_low_degree_proof(root, 5, proof, md, 8)             # not a root of unity of 2-power order
