@@ -405,16 +405,19 @@ def main():
                 "ms_per_transform": round(ev_ms, 4), "avg_launch_ms": round(ev_ms / passes, 4),
                 "rocprof_avg_launch_ms": round(prof_avg, 4) if prof_avg else None,
                 "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
-    # modular products per transform: radix-4 steps (3 per group of 4, 1 in the
-    # first step) + column twiddles (1 per element in table passes, 2 in two-level passes)
+    # modular products per transform (csrc/ntt.hip): each radix-4 step multiplies 4 of every 4
+    # elements (w, w, w' and w_{4m}^(jj+m)); the first step of an even pass only the last (n/4);
+    # column twiddles 1 per element from a table (w_{Ns R} powers within the 2^16-entry table, or
+    # the last pass's full table for 2^17..2^26), 2 in the two-level lo * hi form.
     lr = [log_n // passes + (1 if i < log_n % passes else 0) for i in range(passes)]
     modmuls = 0
     ns = 0
-    for r in lr:
+    for i, r in enumerate(lr):
         steps = r // 2
         modmuls += n * (steps - (0 if r % 2 else 1)) + n // 4 * (0 if r % 2 else 1)
         if ns:
-            modmuls += n * (1 if ns + r <= 16 else 2)
+            table = ns + r <= 16 or (i == len(lr) - 1 and 17 <= log_n <= 26)
+            modmuls += n * (1 if table else 2)
         ns += r
     valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
