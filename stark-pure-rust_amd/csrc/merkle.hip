@@ -150,30 +150,64 @@ __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint
   __shared__ __attribute__((aligned(16))) Digest lds[kMerkleBlock];
   const uint64_t base = (uint64_t)blockIdx.x * block;
   const uint32_t here = (uint32_t)((count - base) < block ? (count - base) : block);
-  for (uint32_t i = threadIdx.x; i < here; i += blockDim.x) {
-    const uint64_t node = base + i;
-    Digest d;
-    if (leaves) {
-      d = LEAF32 ? hash_leaf32(leaves + node * 32) : hash_leaf(leaves + node * leaf_len, leaf_len);
-    } else {
-      d = hash_pair(load_digest(below + 2 * node), load_digest(below + 2 * node + 1));
+  if (leaves && !LEAF32) {
+    for (uint32_t i = threadIdx.x; i < here; i += blockDim.x) {
+      const uint64_t node = base + i;
+      const Digest d = hash_leaf(leaves + node * leaf_len, leaf_len);
+      store_digest(out.lv[0] + node, d);
+      lds[i] = d;
     }
-    store_digest(out.lv[0] + node, d);
-    lds[i] = d;
+  } else {
+    // 32-byte leaves or child pairs: the next node's message words are
+    // loaded while the current one is hashed, so HBM latency hides behind
+    // the compression instead of stalling every iteration.
+    constexpr int kWords = LEAF32 ? 2 : 4;  // uint4 per node input
+    const uint4* src = LEAF32 ? reinterpret_cast<const uint4*>(leaves + base * 32)
+                              : reinterpret_cast<const uint4*>(below + 2 * base);
+    uint4 nxt[kWords];
+    uint32_t i = threadIdx.x;
+    if (i < here) {
+#pragma unroll
+      for (int w = 0; w < kWords; ++w) nxt[w] = src[(size_t)i * kWords + w];
+    }
+    for (; i < here; i += blockDim.x) {
+      uint4 cur[kWords];
+#pragma unroll
+      for (int w = 0; w < kWords; ++w) cur[w] = nxt[w];
+      if (i + blockDim.x < here) {
+#pragma unroll
+        for (int w = 0; w < kWords; ++w) nxt[w] = src[(size_t)(i + blockDim.x) * kWords + w];
+      }
+      uint32_t m[16];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint4 x = w < kWords ? cur[w < kWords ? w : 0] : make_uint4(0, 0, 0, 0);
+        m[4 * w] = x.x; m[4 * w + 1] = x.y; m[4 * w + 2] = x.z; m[4 * w + 3] = x.w;
+      }
+      Digest d;
+      b2s_init(d.h);
+      b2s_compress(d.h, m, LEAF32 ? 32 : 64, 0, true);
+      store_digest(out.lv[0] + base + i, d);
+      lds[i] = d;
+    }
   }
   __syncthreads();
   uint32_t width = here;
   for (uint32_t k = 1; k <= extra; ++k) {
-    width >>= 1;
-    Digest res[kMerkleBlock / 2 / kMerkleThreads];
-    uint32_t c = 0;
-    for (uint32_t i = threadIdx.x; i < width; i += blockDim.x) res[c++] = hash_pair(lds[2 * i], lds[2 * i + 1]);
+    width >>= 1;  // <= kMerkleBlock / 2 = 2 nodes per thread, held in registers (no scratch array)
+    static_assert(kMerkleBlock / 2 <= 2 * kMerkleThreads, "two pair hashes per thread per level");
+    const uint32_t i0 = threadIdx.x, i1 = threadIdx.x + blockDim.x;
+    Digest r0, r1;
+    if (i0 < width) r0 = hash_pair(lds[2 * i0], lds[2 * i0 + 1]);
+    if (i1 < width) r1 = hash_pair(lds[2 * i1], lds[2 * i1 + 1]);
     __syncthreads();
-    c = 0;
-    for (uint32_t i = threadIdx.x; i < width; i += blockDim.x) {
-      lds[i] = res[c];
-      store_digest(out.lv[k] + (base >> k) + i, res[c]);
-      ++c;
+    if (i0 < width) {
+      lds[i0] = r0;
+      store_digest(out.lv[k] + (base >> k) + i0, r0);
+    }
+    if (i1 < width) {
+      lds[i1] = r1;
+      store_digest(out.lv[k] + (base >> k) + i1, r1);
     }
     __syncthreads();
   }
