@@ -385,6 +385,14 @@ def main():
     # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element
     # per transform (read 32 + write 32) x n / transform time (HIP events).
     ntt_bytes = 64.0 * n
+    if world > 1:
+        # The timed step also holds the all-to-all and the cross-rank DFT: time this rank's local
+        # 2^log_n transform (the same ntt_pass_kernel launches) on its own for the kernel roofline.
+        tmp = buf.clone()
+        ctx.ntt_dev(tmp.data_ptr(), log_n, 1, w, inverse=False, stream=sptr)
+        ev_ms = timed_events(lambda: ctx.ntt_dev(tmp.data_ptr(), log_n, 1, w, inverse=False, stream=sptr),
+                             stream, 5)
+        del tmp
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     passes = (log_n + 7) // 8
     traffic = None
