@@ -109,9 +109,14 @@ def test_fri_vs_oracle(ctx, oracle, log_n, excl, deg_div):
     assert got == want
 
 
-def test_fri_large_structure(ctx):
-    """2^20 FRI: every opened path verifies against its root (size-independent)."""
-    log_n = 20
+@pytest.mark.parametrize("log_n", [20, 23])
+def test_fri_large_structure(ctx, log_n):
+    """FRI at 2^20 and at 2^23 (the largest precision a reference proof can use): the layer
+    structure, and the whole proof accepted by the product verifier (stark_verify_low_degree_proof,
+    fri.rs:226-404) against the values' own Merkle root; a flipped leaf is rejected
+    (size-independent properties)."""
+    import copy
+    from stark_amd.verify import verify_low_degree_proof
     n = 1 << log_n
     w = O.root_of_unity(log_n)
     coeffs = O.random_elements(n // 4, 0x5EED0000 + log_n)
@@ -123,12 +128,26 @@ def test_fri_large_structure(ctx):
         ctx.lib.stark_memcpy_h2d(ctx.h, d + (n // 4) * 32, pad.ctypes.data, pad.nbytes)
         ctx.ntt_dev(d, log_n, 1, w)
         proof = ctx.prove_low_degree_dev(d, n, w, n // 4, 8).layers()
+        tree = S.MerkleProofInPlace(ctx)
+        tree.update_dev(d, n, 32)
+        tree.gen_proofs([])
+        root = tree.get_root()
+        del tree
     finally:
         ctx.free(d)
-    assert [list(x)[0] for x in proof] == ["Middle"] * 7 + ["Last"]
-    # Last layer: n/4^7 values of a polynomial of degree < 16
+    # maxdeg n/4 -> divided by 4 per Middle layer until <= 16 (fri.rs:88)
+    layers = 0
+    while (n // 4) >> (2 * layers) > 16:
+        layers += 1
+    assert [list(x)[0] for x in proof] == ["Middle"] * layers + ["Last"]
+    # Last layer: n/4^layers values of a polynomial of degree < 16
     last = [O.from_bytes_le(bytes(b)) for b in proof[-1]["Last"]["last"]]
-    assert len(last) == n // 4 ** 7
+    assert len(last) == n // 4 ** layers
+    assert verify_low_degree_proof(root, w, proof, n // 4, 8)
+    bad = copy.deepcopy(proof)
+    bad[layers // 2]["Middle"]["poly_branches"][17]["leaf"][4] ^= 1
+    with pytest.raises(AssertionError):
+        verify_low_degree_proof(root, w, bad, n // 4, 8)
     m = proof[0]["Middle"]
     root2 = bytes(m["root2"])
     for br in m["column_branches"]:

@@ -259,6 +259,26 @@ __global__ void k_alignbyte(uint64_t* out, uint32_t s) {
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
+__global__ void k_pkadd16(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_pk_add_u16 %0, %0, 0 op_sel:[1,0] op_sel_hi:[0,1]" : "+v"(a##k) : "v"(y), "v"(z));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+__global__ void k_xorsdwa(uint64_t* out, uint32_t s) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t y = s * 3 + 1, z = s ^ 0x5555;
+  for (int i = 0; i < ITERS; i++) {
+#define M(k) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1" : "+v"(a##k) : "v"(y));
+    BODY8(M)
+#undef M
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
 static void run(const char* name, kfn k, uint64_t* buf) {
   const int blocks = 256 * 4, threads = 1024;  // 16 waves per CU = 4 per SIMD
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
@@ -297,5 +317,7 @@ int main() {
   run("v_pk_mov_b32", k_pkmov, buf);
   run("v_lshrrev_b64", k_lshr64, buf);
   run("v_alignbyte_b32", k_alignbyte, buf);
+  run("v_pk_add_u16 swap", k_pkadd16, buf);
+  run("v_xor_b32_sdwa", k_xorsdwa, buf);
   return 0;
 }
