@@ -64,7 +64,7 @@ struct Twiddles {
   fe* d_lo = nullptr;
   fe* d_hi = nullptr;
   fe* d_small = nullptr;
-  fe* d_t16 = nullptr;   // t16[i] = w^(i n / 2^l16), l16 = min(16, log_n)
+  fe* d_t16 = nullptr;   // t16[i] = w^(i n / 2^l16), l16 = min(16, log_n) (18 from 2^25 on)
   fe* d_hi_s = nullptr;  // hi[i] * n^-1   (last pass of an inverse transform)
   fe* d_t16_s = nullptr; // t16[i] * n^-1
   uint32_t l16 = 0;

@@ -277,7 +277,11 @@ struct PassPlan {
   uint32_t log_r[8] = {0};
 };
 
-constexpr uint32_t kMaxLogR = 8;
+constexpr uint32_t kMaxLogR = 9;  // largest radix with a kernel instance and small-root table
+// Radix cap of a size: 2^8 up to 2^24 (three passes of 256 at the headline size); 2^9 from 2^25 on,
+// so 2^25 and 2^26 take three passes, not four (2^26: 13.25 n products instead of 14.5 n, with the
+// column-twiddle table of 2^18 entries below).
+inline uint32_t max_log_r(uint32_t log_n) { return log_n >= 25 ? 9 : 8; }
 // Workgroups of a persistent pass: 256 CUs x 2 resident 256-thread groups.
 constexpr uint64_t kPersistentGrid = 256 * 2;
 #ifndef STARK_NTT_PERSISTENT
@@ -290,7 +294,8 @@ constexpr bool kPersistent = STARK_NTT_PERSISTENT != 0;
 // which the cached full last-pass twiddle table depends on.)
 PassPlan plan_passes(uint32_t log_n) {
   PassPlan p;
-  p.n_pass = (int)((log_n + kMaxLogR - 1) / kMaxLogR);
+  const uint32_t cap = max_log_r(log_n);
+  p.n_pass = (int)((log_n + cap - 1) / cap);
   const uint32_t base = log_n / p.n_pass, extra = log_n % p.n_pass;
   for (int i = 0; i < p.n_pass; ++i) p.log_r[i] = base + ((uint32_t)(p.n_pass - 1 - i) < extra ? 1 : 0);
   return p;
@@ -317,6 +322,7 @@ pass_fn pass_kernel(uint32_t log_r, bool persist) {
     case 6: return persist ? ntt_pass_kernel<6, true> : ntt_pass_kernel<6, false>;
     case 7: return persist ? ntt_pass_kernel<7, true> : ntt_pass_kernel<7, false>;
     case 8: return persist ? ntt_pass_kernel<8, true> : ntt_pass_kernel<8, false>;
+    case 9: return persist ? ntt_pass_kernel<9, true> : ntt_pass_kernel<9, false>;
     default: return nullptr;
   }
 }
@@ -372,8 +378,9 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     }
   }
   if (h_small.empty()) h_small.push_back(to_dev(F.one()));
-  // t16[i] = w^(i n / 2^l16): the w_{Ns R} powers of every pass with Ns R <= 2^16.
-  tw->l16 = log_n < 16 ? log_n : 16;
+  // t16[i] = w^(i n / 2^l16): the w_{Ns R} powers of every pass with Ns R <= 2^l16
+  // (2^16 entries; 2^18 from 2^25 on, where the middle pass of radix 2^9 has Ns R = 2^17 / 2^18).
+  tw->l16 = log_n >= 25 ? 18 : (log_n < 16 ? log_n : 16);
   const size_t n16 = (size_t)1 << tw->l16;
   std::vector<fe> h_t16(n16);
   {

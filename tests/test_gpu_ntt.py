@@ -86,9 +86,10 @@ def test_ntt_errors(ctx):
     assert e.value.code == 2
 
 
-@pytest.mark.parametrize("log_n", [20, 22, 24])
-def test_ntt_roundtrip_large(ctx, log_n):
-    """fwd then inv == identity at full size (size-independent property)."""
+@pytest.mark.parametrize("log_n", [20, 22, 24, 25, 26])
+def test_ntt_roundtrip_large(ctx, oracle, log_n):
+    """fwd then inv == identity at full size (size-independent property); from 2^25 on (radix-512
+    passes) two forward outputs are also checked against the oracle's Horner evaluation."""
     n = 1 << log_n
     c = O.random_elements(n, 0x5EED0000 + log_n)
     w = O.root_of_unity(log_n)
@@ -103,6 +104,11 @@ def test_ntt_roundtrip_large(ctx, log_n):
         back = np.empty_like(c)
         ctx.d2h(back, d)
         assert np.array_equal(back, c)
+        if log_n >= 25:
+            rng = np.random.default_rng(log_n)
+            idx = [int(i) for i in rng.integers(0, n, 2)]
+            xs = O.to_limbs([pow(w, i, O.P) for i in idx])
+            assert np.array_equal(oracle.eval_poly_multi(c, xs), mid[idx])
         if log_n > 20:
             return
         # spot-check 2 outputs of the forward transform against the DFT definition
