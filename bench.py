@@ -137,7 +137,20 @@ def end_to_end(ctx):
     del c
     rs, ws = synth_r1cs.for_steps(20)
     out["prove_synth_2^20_steps_prepared_circuit_ms"], c = prepared_ms(rs, ws, 3)
+    # The verifier (verify_with_file_path on bytes, run.rs:556-592): cold (circuit extensions built per
+    # call) on pedersen_test and on the synthetic 2^20-step proof; both must accept.
+    from stark_amd.verify import verify_with_wtns
+    js_s = c.prove(ws).to_json()
     del c
+    for key, (rb, wb, jb) in (("pedersen", (r1, wt, js)), ("synth_2^20_steps", (rs, ws, js_s))):
+        ok = verify_with_wtns(ctx, rb, wb, jb)
+        tv = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            verify_with_wtns(ctx, rb, wb, jb)
+            tv.append(time.perf_counter() - t0)
+        out[f"verify_{key}_ms"] = round(min(tv) * 1000.0, 3)
+        out[f"verify_{key}_accepts"] = bool(ok)
     return out
 
 
