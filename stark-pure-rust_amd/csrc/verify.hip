@@ -281,10 +281,23 @@ stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std
     for (size_t y : ys)
       for (size_t j = 0; j < 4; ++j) poly_pos.push_back(j * q + y);
     if (!branches_valid(L.root2, ys, L.col) || !branches_valid(m_root, poly_pos, L.poly)) return STARK_ERR_CHECK;
+    // x1 = root^y per row and 1 / x1^3 for all rows with one inversion (Montgomery's trick).
+    const size_t k_rows = ys.size();
+    std::vector<HostFp> x1s(k_rows), inv_x13(k_rows), pre(k_rows + 1);
+    pre[0] = F.one();
+    for (size_t i = 0; i < k_rows; ++i) {
+      x1s[i] = F.pow_u64(root, ys[i]);
+      pre[i + 1] = F.mul(pre[i], F.mul(F.mul(x1s[i], x1s[i]), x1s[i]));
+    }
+    HostFp acc_inv = F.inv(pre[k_rows]);  // every x1 is a root of unity, never zero
+    for (size_t i = k_rows; i-- > 0;) {
+      inv_x13[i] = F.mul(acc_inv, pre[i]);
+      acc_inv = F.mul(acc_inv, F.mul(F.mul(x1s[i], x1s[i]), x1s[i]));
+    }
     for (size_t i = 0; i < ys.size(); ++i) {
       // The cubic through (x1 zeta^j, row_j) at special_x (multi_interp_4 + eval_quartic,
       // poly_utils.rs:442-511): Lagrange weights prod_{k != j}(sx - x_k) / (4 x1^3 zeta^(3j)).
-      const HostFp x1 = F.pow_u64(root, ys[i]);
+      const HostFp x1 = x1s[i];
       HostFp xs[4], num[4];
       for (int j = 0; j < 4; ++j) xs[j] = F.mul(quartic[j], x1);
       for (int j = 0; j < 4; ++j) {
@@ -292,8 +305,7 @@ stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std
         for (int k = 0; k < 4; ++k)
           if (k != j) num[j] = F.mul(num[j], F.sub(special_x, xs[k]));
       }
-      const HostFp x1_3 = F.mul(F.mul(x1, x1), x1);
-      const HostFp inv_den = F.mul(inv4, F.inv(x1_3));  // 1 / (4 x1^3); zeta^(-3j) = zeta^j
+      const HostFp inv_den = F.mul(inv4, inv_x13[i]);  // 1 / (4 x1^3); zeta^(-3j) = zeta^j
       HostFp val = F.zero();
       for (int j = 0; j < 4; ++j)
         val = F.add(val, F.mul(F.mul(fe_from_bytes(L.poly[i * 4 + j].leaf), num[j]), F.mul(inv_den, quartic[j])));
