@@ -114,10 +114,14 @@ class FieldHost {
   }
   HostFp pow(const HostFp& a, const uint64_t* e, int nlimbs) const {
     HostFp r = one_;
+    bool started = false;  // squarings of one before the top set bit are skipped
     for (int i = nlimbs - 1; i >= 0; --i)
       for (int bit = 63; bit >= 0; --bit) {
-        r = mul(r, r);
-        if ((e[i] >> bit) & 1) r = mul(r, a);
+        if (started) r = mul(r, r);
+        if ((e[i] >> bit) & 1) {
+          r = started ? mul(r, a) : a;
+          started = true;
+        }
       }
     return r;
   }

@@ -91,6 +91,8 @@ struct stark_ctx {
   stark::DevBuf fri_cols;    // folded FRI columns (prove_low_degree)
   stark::DevBuf r1cs_arena;  // mk_r1cs_proof working set
   stark::DevBuf trace_arena;  // device trace builder working set (r1cs_trace_dev.hip)
+  stark::DevBuf lde_tmp;      // circuit_lde's step columns and Zb values
+  stark::DevBuf verify_arena, verify_lde;  // the verifier's circuit, kept for the next call
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};

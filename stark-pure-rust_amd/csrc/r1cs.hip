@@ -937,7 +937,7 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
   const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   for (size_t i = 0; i < n_pfi; ++i)
     if (public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
-  DevBuf tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 P + n_pfi)
+  DevBuf& tmp = ctx->lde_tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 P + n_pfi)
   STARK_TRY(ensure_buf(ctx, tmp, (6 * steps + 2 * P + n_pfi + 1) * sizeof(fe)));
   stark_status st = ensure_buf(ctx, out, 8 * P * sizeof(fe));
   if (st == STARK_OK) {
@@ -973,8 +973,7 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
   }
-  hipStreamSynchronize(s);
-  hipFree(tmp.ptr);
+  hipStreamSynchronize(s);  // tmp (a context buffer) is free for the next call
   return st;
 }
 

@@ -550,12 +550,18 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
                                      size_t json_len) {
   if (!ctx || !r1cs || !public_wires || !proof_json || n_public == 0) return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
+  // The circuit's buffers are the context's, grown as needed and kept for the next call
+  // (hipMalloc / hipFree of the extensions would otherwise dominate a small circuit's check).
   stark_r1cs_circuit circ;
   circ.ctx = ctx;
+  std::swap(circ.c.arena, ctx->verify_arena);
+  std::swap(circ.c.lde, ctx->verify_lde);
   stark_status st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
   hipStreamSynchronize(ctx->stream);
-  if (st != STARK_OK) return st;
-  return stark_verify_r1cs_circuit(ctx, &circ, public_wires, n_public, proof_json, json_len);
+  if (st == STARK_OK) st = stark_verify_r1cs_circuit(ctx, &circ, public_wires, n_public, proof_json, json_len);
+  std::swap(circ.c.arena, ctx->verify_arena);
+  std::swap(circ.c.lde, ctx->verify_lde);
+  return st;
 }
 
 stark_status stark_verify_with_witness(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
