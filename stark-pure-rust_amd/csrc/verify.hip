@@ -14,6 +14,7 @@
 // input (including the reference's Err results).
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -69,15 +70,17 @@ class Json {
     expect(':');
     return k;
   }
+  // A u8 array.  Tight loop: serde_json writes no whitespace, so the separator is checked
+  // before falling back to the general whitespace skip.
   void bytes(std::vector<uint8_t>& out) {
     out.clear();
     expect('[');
     if (!ok || accept(']')) return;
-    do {
-      ws();
+    ws();
+    for (;;) {
       unsigned v = 0;
       int nd = 0;
-      while (p_ < e_ && *p_ >= '0' && *p_ <= '9' && nd < 4) {
+      while (p_ < e_ && (unsigned)(*p_ - '0') < 10u && nd < 4) {
         v = 10 * v + (unsigned)(*p_++ - '0');
         ++nd;
       }
@@ -86,14 +89,29 @@ class Json {
         return;
       }
       out.push_back((uint8_t)v);
-    } while (ok && accept(','));
-    expect(']');
+      if (p_ < e_ && *p_ == ',') {
+        ++p_;
+        if (p_ < e_ && (unsigned)(*p_ - '0') >= 10u) ws();
+        continue;
+      }
+      if (p_ < e_ && *p_ == ']') {
+        ++p_;
+        return;
+      }
+      ws();
+      if (p_ < e_ && *p_ == ',') {
+        ++p_;
+        ws();
+        continue;
+      }
+      expect(']');
+      return;
+    }
   }
   void digest(uint8_t out[32]) {
-    std::vector<uint8_t> v;
-    bytes(v);
-    if (v.size() != 32) ok = false;
-    if (ok) memcpy(out, v.data(), 32);
+    bytes(tmp_);  // reused buffer: no allocation per digest
+    if (tmp_.size() != 32) ok = false;
+    if (ok) memcpy(out, tmp_.data(), 32);
   }
   void branch(Branch& b) {
     expect('{');
@@ -204,6 +222,7 @@ class Json {
   }
   const char* p_;
   const char* e_;
+  std::vector<uint8_t> tmp_;
 };
 
 // ---- field helpers ----
@@ -227,21 +246,41 @@ HostFp eval_poly(const std::vector<HostFp>& poly, const HostFp& x) {  // eval_po
 
 // Proof::validate (merkle_tree.rs:25-43) for each (index, proof) pair; verify_multi_branch
 // (:46-58) zips, so every index needs its proof.
+bool branch_valid(const uint8_t root[32], size_t index, const Branch& b) {
+  uint8_t cur[32], msg[64];
+  b2s_host(b.leaf.data(), b.leaf.size(), cur);
+  size_t pos = index;
+  for (size_t d = 0; d < b.nodes.size() / 32; ++d) {
+    const uint8_t* sib = b.nodes.data() + 32 * d;
+    memcpy(msg, pos % 2 == 0 ? cur : sib, 32);
+    memcpy(msg + 32, pos % 2 == 0 ? sib : cur, 32);
+    b2s_host(msg, 64, cur);
+    pos /= 2;
+  }
+  return memcmp(cur, root, 32) == 0;
+}
+
+// Proof::validate (merkle_tree.rs:25-43) for each (index, proof) pair; verify_multi_branch
+// (:46-58) zips, so every index needs its proof.  The paths are checked on the host workers.
 bool branches_valid(const uint8_t root[32], const std::vector<size_t>& idx, const std::vector<Branch>& br) {
   if (br.size() < idx.size()) return false;
-  for (size_t i = 0; i < idx.size(); ++i) {
-    uint8_t cur[32], msg[64];
-    b2s_host(br[i].leaf.data(), br[i].leaf.size(), cur);
-    size_t pos = idx[i];
-    for (size_t d = 0; d < br[i].nodes.size() / 32; ++d) {
-      const uint8_t* sib = br[i].nodes.data() + 32 * d;
-      memcpy(msg, pos % 2 == 0 ? cur : sib, 32);
-      memcpy(msg + 32, pos % 2 == 0 ? sib : cur, 32);
-      b2s_host(msg, 64, cur);
-      pos /= 2;
-    }
-    if (memcmp(cur, root, 32) != 0) return false;
+  const size_t k = idx.size();
+  const unsigned parts = (unsigned)std::min<size_t>(host_threads(), (k + 31) / 32);
+  if (parts <= 1) {
+    for (size_t i = 0; i < k; ++i)
+      if (!branch_valid(root, idx[i], br[i])) return false;
+    return true;
   }
+  std::vector<uint8_t> good(parts, 1);
+  host_parallel(parts, [&](unsigned t) {
+    for (size_t i = k * t / parts; i < k * (t + 1) / parts; ++i)
+      if (!branch_valid(root, idx[i], br[i])) {
+        good[t] = 0;
+        return;
+      }
+  });
+  for (uint8_t g : good)
+    if (!g) return false;
   return true;
 }
 
