@@ -451,6 +451,15 @@ def main():
     valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
     valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
+    try:
+        # The peak above assumes 2.4 GHz; the pass kernel's clock under load, from the committed
+        # GRBM_GUI_ACTIVE pass (profiles/r01_clock_counters.json), prices the bound at the real clock.
+        clk = json.load(open(os.path.join(ROOT, "profiles", "r01_clock_counters.json")))["kernels"]
+        ghz = next(v["effective_clock_ghz"] for k, v in clk.items() if "ntt_pass_kernel<8" in k)
+        valu["measured_clock_ghz"] = ghz
+        valu["frac_at_measured_clock"] = round(valu["frac"] * 2.4 / ghz, 4)
+    except (OSError, KeyError, ValueError, StopIteration):
+        pass
     if world == 1:
         # VALU issue occupancy of the dominant kernel.  Each product issues 128 v_mad_u64_u32 + 128
         # v_addc_co_u32, measured at ~4.6 cycles per wave64 instruction (tools/microbench/isa_rates.hip);
