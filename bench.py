@@ -16,8 +16,11 @@ barrier-bracketed and the max over ranks is used.
 """
 import argparse
 import datetime
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,10 +29,10 @@ sys.path.insert(0, os.path.join(ROOT, "stark-pure-rust_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
-import stark_amd as S  # noqa: E402
+S = None  # stark_amd, imported in main() once this process is known to be a rank
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 # VALU bound of the modular product: every Montgomery product issues 128
@@ -39,6 +42,7 @@ MODMUL_PEAK = 1024 * 2.4e9 * 64 / (256 * 4)
 LOG_N = 24
 PROFILE = os.path.join(ROOT, "profiles", "r01_summary.json")
 SQ_PROFILE = os.path.join(ROOT, "profiles", "r01_ntt_sq_counters.json")
+LARGE = os.path.join(ROOT, "tests", "golden", "large_digests.json")
 
 
 def parse():
@@ -49,7 +53,76 @@ def parse():
     ap.add_argument("--log-n", type=int, default=LOG_N)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and rendezvous only (CPU test of the --gpus N launcher)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int | None:
+    """`bench.py --gpus N` with N > 1 and no launcher around it: start torch.distributed.run as a
+    CHILD process (one rank per GPU, rendezvous on 127.0.0.1) before anything touches the GPU, wait,
+    and hand back its exit code (its stdout, the rank-0 JSON line, is inherited).  Under a launcher
+    the requested N must be the world it started.  Returns None when this process is a rank."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        return subprocess.run(cmd).returncode
+    if int(world) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    return None
+
+
+def sha256(a) -> str:
+    if isinstance(a, str):
+        a = a.encode()
+    elif isinstance(a, np.ndarray):
+        a = np.ascontiguousarray(a, dtype=np.uint64).tobytes()
+    return hashlib.sha256(a).hexdigest()
+
+
+def large_digests() -> dict:
+    try:
+        return json.load(open(LARGE))
+    except (OSError, ValueError):
+        return {}
+
+
+def host_cpus():
+    """(physical cores of the host, CPUs this process may use).  The reference's Worker::new takes
+    num_cpus::get_physical() threads and parallel_fft splits into 2^floor(log2) of them
+    (multicore.rs:43-45, fft.rs:332-351); the GPU box grants one job a share of the host (its
+    OMP_NUM_THREADS), so the baseline uses the smaller of the two."""
+    phys = set()
+    cur = {}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (x.strip() for x in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                phys.add((cur.get("physical id", "0"), cur.get("core id", cur.get("processor"))))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id", "0"), cur.get("core id", cur.get("processor"))))
+    except OSError:
+        pass
+    physical = len(phys) or (os.cpu_count() or 1)
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or allowed
+    return physical, min(allowed, share)
 
 
 def synthetic(n, seed):
@@ -79,9 +152,13 @@ def end_to_end(ctx):
     fix = os.path.join(ROOT, "tests", "golden", "r1cs")
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
     out = {}
+    big = large_digests().get("prove_synth_2^20_steps", {})
+
     def synth_ms(reps):
         rs, ws = synth_r1cs.for_steps(20)
-        prove_with_witness(ctx, rs, ws).to_json()
+        js20 = prove_with_witness(ctx, rs, ws).to_json()
+        if big:
+            out["prove_synth_2^20_steps_bitexact_vs_oracle_digest"] = sha256(js20) == big.get("json_sha256")
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -186,6 +263,14 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
         return round(float(t.cpu()[0]) * 1000.0, 3)
 
     out["prove_pedersen_distributed_ms"] = timed(r1, wt, 3)
+    # config 4: poseidon3_test over the N GPUs, bit-exact against the golden digest
+    r1p = open(os.path.join(fix, "poseidon3_test.r1cs"), "rb").read()
+    wtp = open(os.path.join(fix, "poseidon3_test.wtns"), "rb").read()
+    jsp = prove_distributed(ops, r1p, wtp)
+    if rank == 0:
+        out["prove_poseidon3_distributed_bitexact_vs_golden"] = \
+            hashlib.sha256(jsp.encode()).hexdigest() == golden["poseidon3_test"]["json_sha256"]
+    out["prove_poseidon3_distributed_ms"] = timed(r1p, wtp, 3)
     rs, ws = synth_r1cs.for_steps(20)
     prove_distributed(ops, rs, ws)   # warm: twiddles, arenas
     out["prove_synth_2^20_steps_distributed_ms"] = timed(rs, ws, 3)
@@ -198,16 +283,83 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
     return out
 
 
+MERKLE_SQ = os.path.join(ROOT, "profiles", "r02_merkle_sq_counters.json")
+
+
+def merkle_valu_roofline(n: int, ms: float) -> dict:
+    """Blake2s issue roofline of a 2^log n x 32-B tree build: n leaf compressions (one 32-B block
+    each) + n - 1 node compressions (64-B blocks) = 2n - 1.  The VALU instructions per compression
+    and the clock under load come from the committed rocprofv3 SQ pass (MERKLE_SQ); the issue
+    bound prices them at VOP2 2.3 / VOP3 4.6 cycles per wave64 instruction (tools/microbench)."""
+    comp = 2 * n - 1
+    out = {"compressions": comp, "achieved_compressions_per_s": comp / (ms / 1000.0)}
+    try:
+        prof = json.load(open(MERKLE_SQ))
+        per = prof["valu_insts_per_compression"]
+        cyc = prof["issue_cycles_per_compression"]
+        ghz = prof.get("effective_clock_ghz", 2.4)
+        peak = 1024 * ghz * 1e9 * 64 / cyc          # compressions/s at that clock, all SIMDs issuing
+        out.update({"valu_insts_per_compression": per, "issue_cycles_per_compression_wave64": cyc,
+                    "clock_ghz": ghz, "peak_compressions_per_s": peak,
+                    "frac": round(out["achieved_compressions_per_s"] / peak, 4),
+                    "sq_profile": os.path.relpath(MERKLE_SQ, ROOT)})
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
+
+
+def ntt_products(log_n: int, plan: list) -> int:
+    """Modular products of one forward 2^log_n transform, counted from csrc/ntt.hip's pass kernel:
+    each radix-4 step multiplies 4 of every 4 elements (w_{2m}^jj twice, w_{4m}^jj, w_{4m}^(jj+m)),
+    the s = 0 step of an even radix only by w_{4m}^(jj+m) (n/4), an odd radix runs a product-free
+    radix-2 stage 0 first; every pass after the first multiplies each element by its column twiddle,
+    one product from a table (t16 when Ns R <= 2^l16, or the last pass's full table for 2^17..2^26)
+    or two in the lo * hi form."""
+    n = 1 << log_n
+    l16 = 18 if log_n >= 25 else min(log_n, 16)
+    total, ns = 0, 0
+    for i, r in enumerate(plan):
+        if r % 2:
+            total += n * ((r - 1) // 2)
+        else:
+            total += n * (r // 2 - 1) + n // 4
+        if ns:
+            last = i == len(plan) - 1
+            table = ns + r <= l16 or (last and log_n > l16 and 17 <= log_n <= 26)
+            total += n * (1 if table else 2)
+        ns += r
+    return total
+
+
 def main():
+    global S
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    backend = os.environ.get("STARK_BENCH_BACKEND", "nccl")
+    if args.launch_check:
+        # The launcher's CPU rehearsal: rendezvous, one collective, report the world that ran.
+        if world > 1:
+            dist.init_process_group("gloo", init_method="env://", timeout=datetime.timedelta(seconds=120))
+            t = torch.tensor([1.0])
+            dist.all_reduce(t)
+            world_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            world_seen = 1
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_in_all_reduce": world_seen}))
+        return
+    import stark_amd
+    S = stark_amd
     # One rank per GPU.  (local % device_count and STARK_BENCH_BACKEND=gloo exist only to rehearse
     # the N > 1 path with several ranks on a one-GPU box; the driver's runs use RCCL, one GPU per rank.)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        backend = os.environ.get("STARK_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", init_method="env://", device_id=torch.device(f"cuda:{local}"),
                                     timeout=datetime.timedelta(seconds=300))
@@ -230,6 +382,27 @@ def main():
     buf = torch.from_numpy(host.view(np.int64)).to(f"cuda:{local}")
     torch.cuda.synchronize()
     dptr = buf.data_ptr()
+    big = large_digests()
+    parity = {}
+    gpu_fwd = None
+    if world == 1:
+        # Parity of the exact timed path (stark_ntt_dev, device-resident) on the step's input:
+        # forward and inverse against the oracle's digests (tests/golden/large_digests.json);
+        # the CPU baseline below re-checks the forward output element for element.
+        chk = buf.clone()
+        ctx.ntt_dev(chk.data_ptr(), log_n, 1, w, inverse=False, stream=sptr)
+        stream.synchronize()
+        gpu_fwd = chk.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()
+        chk.copy_(buf)
+        ctx.ntt_dev(chk.data_ptr(), log_n, 1, w, inverse=True, stream=sptr)
+        stream.synchronize()
+        gpu_inv = chk.cpu().numpy().view(np.uint64).reshape(-1, 4)
+        rec = big.get(f"ntt_2^{log_n}")
+        if rec and sha256(host) == rec["input_sha256"]:
+            parity[f"ntt_2^{log_n}_fwd_bitexact_vs_oracle_digest"] = sha256(gpu_fwd) == rec["forward_sha256"]
+            parity[f"ntt_2^{log_n}_inv_bitexact_vs_oracle_digest"] = sha256(gpu_inv) == rec["inverse_sha256"]
+        del chk, gpu_inv
+        torch.cuda.empty_cache()
     pipelined = world > 1 and dist.get_backend() == "nccl"
     if world > 1:
         from stark_amd.distributed import GpuOps, cyclic_ntt, cyclic_ntt_pipelined
@@ -281,14 +454,26 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * n * args.steps / elapsed
 
-    extras = {}
+    extras = dict(parity)
     if not args.no_extras and world == 1:
-        # config 2: 2^20 forward + inverse pair, bit-exact round trip checked
+        # config 2: 2^20 forward + inverse pair; each direction checked against the oracle's digest
         n20 = 1 << 20
         w20 = O.root_of_unity(20)
         h20 = synthetic(n20, 0x5EED0000 + 20)
         b20 = torch.from_numpy(h20.view(np.int64)).to(f"cuda:{local}")
+        rec20 = big.get("ntt_2^20", {})
+        ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=False, stream=sptr)
+        stream.synchronize()
+        f20 = sha256(b20.cpu().numpy().view(np.uint64))
+        b20.copy_(torch.from_numpy(h20.view(np.int64)))
+        ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=True, stream=sptr)
+        stream.synchronize()
+        i20 = sha256(b20.cpu().numpy().view(np.uint64))
+        b20.copy_(torch.from_numpy(h20.view(np.int64)))
         torch.cuda.synchronize()
+        if rec20:
+            extras["ntt_2^20_fwd_bitexact_vs_oracle_digest"] = f20 == rec20["forward_sha256"]
+            extras["ntt_2^20_inv_bitexact_vs_oracle_digest"] = i20 == rec20["inverse_sha256"]
 
         def pair():
             ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=False, stream=sptr)
@@ -301,7 +486,7 @@ def main():
         extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
         # The host-buffer entry point (best_fft on a host Vec: H2D + NTT + D2H), PCIe-inclusive;
         # reported beside `value`, never as it.
-        hc = buf.cpu().numpy().view(np.uint64).reshape(-1, 4)
+        hc = host.copy()
         ctx.best_fft(hc, w, log_n)
         t_h = time.perf_counter()
         ctx.best_fft(hc, w, log_n)
@@ -334,6 +519,7 @@ def main():
         extras["merkle_2^24x32B_leaves_per_s"] = n / (mk_ms / 1000.0)
         extras["merkle_2^24x32B_ms"] = round(mk_ms, 4)
         extras["merkle_roofline_frac"] = round(96.0 * n / (mk_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
+        extras["merkle_valu_roofline"] = merkle_valu_roofline(n, mk_ms)
         # Secondary leaf shapes: 256-B leaves (the main tree's P|A|S|D1..B3 rows; the same
         # 512 MiB buffer read as 2^21 rows) and 2^20 x 40-B accumulator leaves.
         for cnt, ll, key in ((n // 8, 256, "merkle_2^21x256B"), (1 << 20, 40, "merkle_2^20x40B")):
@@ -342,7 +528,8 @@ def main():
             extras[f"{key}_leaves_per_s"] = cnt / (t_ms / 1000.0)
             extras[f"{key}_ms"] = round(t_ms, 4)
         del tree
-        # FRI prove wall clock at precision 2^23 (largest a reference proof can use, fri/src/utils.rs:88)
+        # FRI prove wall clock at precision 2^23 (largest a reference proof can use, fri/src/utils.rs:88),
+        # the proof checked against the oracle's digest (same input as make_large_golden.py).
         lf = 23
         nf = 1 << lf
         wf = O.root_of_unity(lf)
@@ -353,7 +540,9 @@ def main():
         torch.cuda.synchronize()
         ctx.ntt_dev(bf.data_ptr(), lf, 1, wf, stream=sptr)
         stream.synchronize()
-        ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
+        proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
+        if big.get("fri_2^23"):
+            extras["fri_2^23_bitexact_vs_oracle_digest"] = sha256(proof.to_json()) == big["fri_2^23"]["json_sha256"]
         t1 = time.perf_counter()
         proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
         extras["fri_prove_2^23_ms"] = round((time.perf_counter() - t1) * 1000.0, 3)
@@ -402,9 +591,9 @@ def main():
         except Exception as e:  # symmetric failures still print the headline line
             extras["distributed_prove_error"] = repr(e)[:300]
 
-    # Roofline of the dominant kernel, ntt_pass_kernel: one 2^24 transform is
-    # `passes` launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element
-    # per transform (read 32 + write 32) x n / transform time (HIP events).
+    # Roofline of the dominant kernel, ntt_pass_kernel: one 2^log_n transform is len(plan)
+    # launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element per transform (read 32 +
+    # write 32) x n / transform time (HIP events on the launch stream).
     ntt_bytes = 64.0 * n
     if world > 1:
         # The timed step also holds the all-to-all and the cross-rank DFT: time this rank's local
@@ -415,39 +604,32 @@ def main():
                              stream, 5)
         del tmp
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
-    passes = (log_n + 7) // 8
+    plan = S.ntt_plan(log_n)
+    passes = len(plan)
+    kname = f"stark::ntt_pass_kernel<{plan[-1]}, false>"
     traffic = None
-    prof_avg = None
+    prof_avg = prof_med = None
     try:
         prof = json.load(open(PROFILE))
-        rec = prof["pmc_bytes_per_launch"].get("stark::ntt_pass_kernel<8, false>")
+        rec = prof["pmc_bytes_per_launch"].get(kname)
         if rec and log_n == 24:
             # HBM bytes of one transform: the PMC per-launch average (FETCH_SIZE x 2 + WRITE_SIZE,
             # MI355X_MICROARCH.md) x the transform's launches.
             traffic = passes * rec["hbm_bytes"]
-            prof_avg = prof["kernels"]["stark::ntt_pass_kernel<8, false>"]["avg_ns"] / 1e6
+            k = prof["kernels"][kname]
+            prof_avg = k["avg_ns"] / 1e6
+            prof_med = k.get("steady_median_ns", 0) / 1e6 or None
     except (OSError, KeyError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "kernel": f"ntt_pass_kernel<8> x {passes} launches per 2^{log_n} transform",
+                "traffic_over_algorithmic": round(traffic / ntt_bytes, 3) if traffic else None,
+                "kernel": f"ntt_pass_kernel x {passes} launches (radices 2^{plan}) per 2^{log_n} transform",
                 "ms_per_transform": round(ev_ms, 4), "avg_launch_ms": round(ev_ms / passes, 4),
                 "rocprof_avg_launch_ms": round(prof_avg, 4) if prof_avg else None,
+                "rocprof_steady_median_launch_ms": round(prof_med, 4) if prof_med else None,
                 "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
-    # modular products per transform (csrc/ntt.hip): each radix-4 step multiplies 4 of every 4
-    # elements (w, w, w' and w_{4m}^(jj+m)); the first step of an even pass only the last (n/4);
-    # column twiddles 1 per element from a table (w_{Ns R} powers within the 2^16-entry table, or
-    # the last pass's full table for 2^17..2^26), 2 in the two-level lo * hi form.
-    lr = [log_n // passes + (1 if i < log_n % passes else 0) for i in range(passes)]
-    modmuls = 0
-    ns = 0
-    for i, r in enumerate(lr):
-        steps = r // 2
-        modmuls += n * (steps - (0 if r % 2 else 1)) + n // 4 * (0 if r % 2 else 1)
-        if ns:
-            table = ns + r <= 16 or (i == len(lr) - 1 and 17 <= log_n <= 26)
-            modmuls += n * (1 if table else 2)
-        ns += r
+    modmuls = ntt_products(log_n, plan)
     valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
     valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
@@ -458,6 +640,7 @@ def main():
         ghz = next(v["effective_clock_ghz"] for k, v in clk.items() if "ntt_pass_kernel<8" in k)
         valu["measured_clock_ghz"] = ghz
         valu["frac_at_measured_clock"] = round(valu["frac"] * 2.4 / ghz, 4)
+        roofline["valu_frac_at_measured_clock"] = valu["frac_at_measured_clock"]
     except (OSError, KeyError, ValueError, StopIteration):
         pass
     if world == 1:
@@ -469,7 +652,7 @@ def main():
         try:
             # All VALU instructions (committed rocprofv3 SQ_INSTS_VALU of the same kernel) at 2.3 cycles
             # (VOP2) to 4.6 cycles (VOP3 / carry ops): the range of the whole issue occupancy.
-            sq = json.load(open(SQ_PROFILE))["kernels"]["stark::ntt_pass_kernel<8, false>"]
+            sq = json.load(open(SQ_PROFILE))["kernels"][kname]
             if log_n == 24:
                 insts = sq["SQ_INSTS_VALU"] * passes
                 valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
@@ -481,28 +664,32 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle as O2
-        o = O2.Oracle()
-        cores = min(16, os.cpu_count() or 1)
+        # The reference algorithm on the host: the oracle's C restatement of best_fft / parallel_fft
+        # (fft.rs:195-251, 327-357) with T = 2^floor(log2(cores)) threads as Worker::new splits it,
+        # on the SAME input as the GPU step; its output is compared with the GPU's element for element.
+        o = O.Oracle()
+        physical, usable = host_cpus()
+        cores = min(physical, usable)
         threads = 1 << (cores.bit_length() - 1)
-        lc = log_n  # the same workload as the GPU step (one 2^24 transform, ~3 s on 16 threads)
-        hc = synthetic(1 << lc, 1234)
-        wc = O2.root_of_unity(lc)
         t2 = time.perf_counter()
-        o.best_fft(hc, wc, lc, cpus=threads)
+        cpu_out = o.best_fft(host, w, log_n, cpus=threads)
         tc = time.perf_counter() - t2
-        cpu = {"value": (1 << lc) / tc, "unit": "field-elems/s", "cores": threads, "kind": "port",
-               "sample": f"one 2^{lc}-point best_fft (oracle C restatement of fft.rs parallel_fft, "
-                         f"{threads} threads), {tc:.2f} s"}
-
-    if cpu is not None and not args.no_extras:
-        # End-to-end CPU baseline: the oracle's restatement of mk_r1cs_proof on pedersen_test.
-        import r1cs as R
-        tr = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "pedersen_test"))
-        t3 = time.perf_counter()
-        R.mk_r1cs_proof_json(o, tr, cpus=threads)
-        extras["prove_pedersen_cpu_port_ms"] = round((time.perf_counter() - t3) * 1000.0, 1)
-        extras["prove_pedersen_cpu_port_threads"] = threads
+        cpu = {"value": n / tc, "unit": "field-elems/s", "cores": threads, "threads": threads,
+               "host_physical_cores": physical, "cpus_granted": usable, "kind": "port",
+               "sample": f"one 2^{log_n}-point best_fft on the bench step's input (oracle C restatement of "
+                         f"fft.rs parallel_fft, {threads} threads = 2^floor(log2 min(physical cores {physical}, "
+                         f"CPUs granted {usable}))), {tc:.2f} s",
+               "gpu_output_bitexact": bool(gpu_fwd is not None and np.array_equal(cpu_out, gpu_fwd))}
+        extras[f"ntt_2^{log_n}_bitexact_vs_cpu_baseline"] = cpu["gpu_output_bitexact"]
+        del cpu_out
+        if not args.no_extras:
+            # End-to-end CPU baseline: the oracle's restatement of mk_r1cs_proof on pedersen_test.
+            import r1cs as R
+            tr = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "pedersen_test"))
+            t3 = time.perf_counter()
+            R.mk_r1cs_proof_json(o, tr, cpus=threads)
+            extras["prove_pedersen_cpu_port_ms"] = round((time.perf_counter() - t3) * 1000.0, 1)
+            extras["prove_pedersen_cpu_port_threads"] = threads
 
     if rank == 0:
         line = {"metric": "2^24-pt NTT field-elems/sec", "value": value, "unit": "field-elems/s",
@@ -516,7 +703,7 @@ def main():
                            "parallelism": f"distributed NTT x{world} (one all-to-all)" if world > 1 else "single GPU"},
                 "roofline": roofline, "valu_roofline": valu, "cpu_baseline": cpu}
         line.update(extras)
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -82,6 +82,10 @@ stark_status stark_fft_in_place(stark_ctx* ctx, uint64_t* values, const uint64_t
  * semantics.  Asynchronous on `stream` (NULL = context stream). */
 stark_status stark_ntt_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t batch,
                            const uint64_t root[4], int inverse, void* stream);
+/* Diagnostics, no reference counterpart: the Stockham pass plan of a 2^log_n transform.
+ * Writes up to `cap` log2 radices (first pass first) to log_r and returns the number of
+ * passes (0 for log_n < 2, where no pass kernel runs).  bench.py prices its roofline with it. */
+uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap);
 /* Low-degree extension, the pattern of r1cs-stark/src/prove.rs:100-101 (and
  * :160-167, 183-184): inv_best_fft(values, g1, log2 steps) followed by
  * best_fft(coefficients zero-padded to steps << log_blowup, g2), where g2 is a

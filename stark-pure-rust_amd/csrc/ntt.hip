@@ -468,6 +468,17 @@ static bool full_table_enabled() {
   return on;
 }
 
+}  // namespace stark
+
+extern "C" uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap) {
+  if (log_n < 2 || log_n > 28) return 0;
+  const stark::PassPlan p = stark::plan_passes(log_n);
+  for (int i = 0; i < p.n_pass && (uint32_t)i < cap; ++i) log_r[i] = p.log_r[i];
+  return (uint32_t)p.n_pass;
+}
+
+namespace stark {
+
 uint32_t ntt_first_log_r(uint32_t log_n) { return log_n < 2 ? log_n : plan_passes(log_n).log_r[0]; }
 
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,

@@ -408,7 +408,10 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
                                 const ProofIn& pr) {
   const FieldHost& F = FieldHost::get();
   if (c.world != 1) return STARK_ERR_BAD_ARG;
-  if (n_public < c.n_public) return STARK_ERR_BAD_ARG;  // public_wires[w] for w < n_public (run.rs:503-509)
+  // The reference builds its boundary points from every supplied wire (run.rs:503-509); a prepared
+  // circuit holds the first uses of the header's 1 + n_pub_in + n_pub_out wires only, so any other
+  // count is refused rather than silently truncated.
+  if (n_public != c.n_public) return STARK_ERR_BAD_ARG;
   std::vector<HostFp> pub(c.n_public);
   for (size_t i = 0; i < c.n_public; ++i) pub[i] = F.from_bytes_le(pub_bytes + 32 * i, 32);
   if (!FieldHost::eq(pub[0], F.one())) return STARK_ERR_CHECK;  // run.rs:480

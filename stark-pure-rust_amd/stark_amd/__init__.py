@@ -54,6 +54,7 @@ _SIGNATURES = {
     "stark_inv_best_fft": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p], ctypes.c_int),
     "stark_fft_in_place": ([_vp, _u64p, _u64p, ctypes.c_uint32, ctypes.c_int], ctypes.c_int),
     "stark_ntt_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_int, _vp], ctypes.c_int),
+    "stark_ntt_plan": ([ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32], ctypes.c_uint32),
     "stark_expand_root_of_unity": ([_vp, _u64p, _u64p, ctypes.c_size_t, _szp], ctypes.c_int),
     "stark_multi_inv": ([_vp, _u64p, ctypes.c_size_t, _u64p], ctypes.c_int),
     "stark_eval_poly_at_multi": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_size_t, _u64p], ctypes.c_int),
@@ -246,6 +247,13 @@ class Context:
         r = _limbs(root_of_unity)
         self.check(self.lib.stark_fft_in_place(self.h, _p64(v), _p64(r), log_order_of_root, 0), "serial_fft")
 
+    def inv_serial_fft(self, values: np.ndarray, root_of_unity, log_order_of_root: int) -> None:
+        """fft.rs:284-293 (in place on exactly 2^log values, root^-1 then n^-1)."""
+        v = values
+        assert v.dtype == np.uint64 and v.flags["C_CONTIGUOUS"]
+        r = _limbs(root_of_unity)
+        self.check(self.lib.stark_fft_in_place(self.h, _p64(v), _p64(r), log_order_of_root, 1), "inv_serial_fft")
+
     def ntt_dev(self, d_ptr: int, log_n: int, batch: int, root, inverse: bool = False, stream: int = 0) -> None:
         r = _limbs(root)
         self.check(self.lib.stark_ntt_dev(self.h, d_ptr, log_n, batch, _p64(r), 1 if inverse else 0, stream or None),
@@ -412,6 +420,14 @@ class FriProofList:
 
 
 # ---- host-side helpers with the reference names ------------------------------
+def ntt_plan(log_n: int) -> list:
+    """log2 radices of the Stockham passes of a 2^log_n transform (stark_ntt_plan; host-only)."""
+    lib = load_library()
+    out = (ctypes.c_uint32 * 8)()
+    k = lib.stark_ntt_plan(log_n, out, 8)
+    return list(out)[:k]
+
+
 def blake(message: bytes) -> bytes:
     """fri/src/utils.rs:5-10 (computed by libstark_hip's host Blake2s)."""
     lib = load_library()

@@ -1,0 +1,117 @@
+"""GPU parity at the sizes bench.py times.
+
+* The dense 2^24 forward and inverse NTT through `stark_ntt_dev` -- the exact device-resident
+  path the bench times (3 radix-256 Stockham passes, the last with the full twiddle table) --
+  compared element for element with the oracle's best_fft / inv_best_fft (fft.rs:327-379) run
+  live on the same input, and with the committed digests of tests/golden/large_digests.json.
+* Config 2: the dense 2^20 forward and inverse, full vector, same two checks.
+* prove_low_degree (fri.rs:46-224) at precision 2^23 on bench.py's FRI input, and mk_r1cs_proof
+  (prove.rs:14-378) on the synthetic 2^20-step circuit: the JSON hashes to the digest of the
+  oracle's JSON (tests/golden/make_large_golden.py generated both in the container).
+* serial_fft / inv_serial_fft in place (`stark_fft_in_place`, fft.rs:150-193, 284-293).
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+BIG = json.load(open(os.path.join(HERE, "golden", "large_digests.json")))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+# Host threads for the live oracle: the GPU box's CPU share is 16 (power of two, as Worker::new
+# splits parallel_fft, multicore.rs:43-45).
+CPUS = 16
+
+
+def _sha(a) -> str:
+    if isinstance(a, str):
+        a = a.encode()
+    elif isinstance(a, np.ndarray):
+        a = np.ascontiguousarray(a, dtype=np.uint64).tobytes()
+    return hashlib.sha256(a).hexdigest()
+
+
+def _ntt_dev(ctx, c, log_n, w, inverse):
+    d = ctx.alloc(c.nbytes)
+    try:
+        ctx.h2d(d, c)
+        ctx.ntt_dev(d, log_n, 1, w, inverse=inverse)
+        out = np.empty_like(c)
+        ctx.d2h(out, d)
+    finally:
+        ctx.free(d)
+    return out
+
+
+@pytest.mark.parametrize("log_n", [20, 24])
+def test_ntt_dense_full_vector_vs_oracle(ctx, oracle, log_n):
+    rec = BIG[f"ntt_2^{log_n}"]
+    c = O.random_elements(1 << log_n, 0x5EED0000 + log_n)
+    assert _sha(c) == rec["input_sha256"]
+    w = O.root_of_unity(log_n)
+    fwd = _ntt_dev(ctx, c, log_n, w, inverse=False)
+    assert _sha(fwd) == rec["forward_sha256"]
+    assert np.array_equal(fwd, oracle.best_fft(c, w, log_n, cpus=CPUS))
+    inv = _ntt_dev(ctx, c, log_n, w, inverse=True)
+    assert _sha(inv) == rec["inverse_sha256"]
+    assert np.array_equal(inv, oracle.inv_best_fft(c, w, log_n, cpus=CPUS))
+
+
+def test_ntt_2_24_host_entry_point(ctx):
+    """best_fft on a host vector (H2D + the same passes + D2H) gives the same 2^24 output."""
+    rec = BIG["ntt_2^24"]
+    c = O.random_elements(1 << 24, 0x5EED0000 + 24)
+    assert _sha(ctx.best_fft(c, O.root_of_unity(24), 24)) == rec["forward_sha256"]
+
+
+def test_fri_2_23_vs_oracle_digest(ctx):
+    rec = BIG["fri_2^23"]
+    lf = 23
+    nf = 1 << lf
+    wf = O.root_of_unity(lf)
+    coef = O.random_elements(nf // 4, 0x5EED0000 + lf)
+    vals = ctx.best_fft(coef, wf, lf)
+    assert _sha(vals) == rec["values_sha256"]
+    js = ctx.prove_low_degree(vals, wf, nf // 4, 8).to_json()
+    assert len(js) == rec["json_len"]
+    assert _sha(js) == rec["json_sha256"]
+    # the device-resident entry point bench.py times
+    d = ctx.alloc(vals.nbytes)
+    try:
+        ctx.h2d(d, vals)
+        js_dev = ctx.prove_low_degree_dev(d, nf, wf, nf // 4, 8).to_json()
+    finally:
+        ctx.free(d)
+    assert _sha(js_dev) == rec["json_sha256"]
+
+
+def test_synth_2_20_steps_proof_vs_oracle_digest(ctx):
+    import synth_r1cs
+    from stark_amd.r1cs import prove_with_witness
+    rec = BIG["prove_synth_2^20_steps"]
+    rs, ws = synth_r1cs.for_steps(20)
+    assert _sha(rs) == rec["r1cs_sha256"] and _sha(ws) == rec["wtns_sha256"]
+    js = prove_with_witness(ctx, rs, ws).to_json()
+    assert len(js) == rec["json_len"]
+    assert _sha(js) == rec["json_sha256"]
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 10, 18])
+def test_fft_in_place_vs_oracle(ctx, oracle, log_n):
+    n = 1 << log_n
+    c = O.random_elements(n, 0x5EED0100 + log_n)
+    w = O.root_of_unity(log_n)
+    v = c.copy()
+    ctx.serial_fft(v, w, log_n)
+    assert np.array_equal(v, oracle.best_fft(c, w, log_n, cpus=8))
+    ctx.inv_serial_fft(v, w, log_n)
+    assert np.array_equal(v, c)
+    u = c.copy()
+    ctx.inv_serial_fft(u, w, log_n)
+    assert np.array_equal(u, oracle.inv_best_fft(c, w, log_n, cpus=8))

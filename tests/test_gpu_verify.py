@@ -102,6 +102,13 @@ def test_rejects_wrong_public_wires(ctx, proofs):
         verify_with_witness(ctx, r1, bad, js)
     with pytest.raises(AssertionError):          # public_wires[0] must be one (run.rs:480)
         verify_with_witness(ctx, r1, [2] + pub[1:], js)
+    # The reference takes boundary points from every supplied wire (run.rs:503-509): a count other
+    # than the header's 1 + n_pub_in + n_pub_out is refused (STARK_ERR_BAD_ARG), never truncated.
+    from stark_amd import StarkError
+    for wrong in (pub + [5], pub[:-1]):
+        with pytest.raises(StarkError) as e:
+            verify_with_witness(ctx, r1, wrong, js)
+        assert e.value.code == 3
 
 
 def test_rejects_proof_of_other_circuit(ctx, proofs):

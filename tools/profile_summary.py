@@ -29,6 +29,15 @@ def main():
         summary["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                                 "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                                                 "pct": float(r["Percentage"])}
+    # Steady state: the median launch duration over the second half of each kernel's launches in
+    # the kernel trace (the first launches include clock ramp-up and table builds).
+    durs = collections.defaultdict(list)
+    for r in sorted(load(f"{stats_dir}/*kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"])):
+        durs[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for k, d in durs.items():
+        if k in summary["kernels"] and d:
+            tail = sorted(d[len(d) // 2:])
+            summary["kernels"][k]["steady_median_ns"] = float(tail[len(tail) // 2])
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in (fetch_dir, write_dir):
         for r in load(f"{d}/*counter_collection.csv"):
