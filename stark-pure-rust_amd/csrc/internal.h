@@ -58,15 +58,15 @@ struct DevBuf {
 // Twiddle set for one (root, log_n): everything in Montgomery form.
 //   lo[i] = w^i                   i < 2^kb
 //   hi[i] = w^(i * 2^kb)          i < 2^(log_n - kb)
-//   small_off[l] = offset into `small` of w_R^k = w^(k * n / R), k < R/2, R = 2^l
+//   small_off[l] = offset (in fe) into `small` of the Shoup pairs of w_R^k = w^(k * n / R), k < R/2, R = 2^l
 struct Twiddles {
   uint32_t log_n = 0, kb = 0;
   fe* d_lo = nullptr;
   fe* d_hi = nullptr;
-  fe* d_small = nullptr;
-  fe* d_t16 = nullptr;   // t16[i] = w^(i n / 2^l16), l16 = min(16, log_n) (18 from 2^25 on)
+  fe* d_small = nullptr; // Shoup pairs (shoup_pair), 2 fe per root
+  fe* d_t16 = nullptr;   // Shoup pairs of t16[i] = w^(i n / 2^l16), l16 = min(16, log_n) (18 from 2^25 on)
   fe* d_hi_s = nullptr;  // hi[i] * n^-1   (last pass of an inverse transform)
-  fe* d_t16_s = nullptr; // t16[i] * n^-1
+  fe* d_t16_s = nullptr; // Shoup pairs of t16[i] * n^-1
   uint32_t l16 = 0;
   uint32_t small_off[16] = {0};
   // Full column-twiddle table of the last pass (built on first use when that
@@ -268,6 +268,33 @@ inline fe to_dev(const HostFp& x) {
     r.w[2 * i + 1] = (uint32_t)(x.v[i] >> 32);
   }
   return r;
+}
+
+// Shoup pair of a constant w (tools/gen_fe_mul_asm.py shoup_stream): out[0] = w canonical,
+// out[1] = wq = floor(w 2^256 / p).  With m = w R mod p (the Montgomery image, R = 2^256),
+// w 2^256 = wq p + m exactly, so wq = (2^256 - m) p^-1 mod 2^256 (m = 0 <=> w = 0 <=> wq = 0).
+inline void shoup_pair(const HostFp& x, fe out[2]) {
+  static constexpr uint64_t kPinv256[4] = {0x3d1e0a6c10000001ull, 0x9a7979b4b396ee4cull, 0x1c6567d766f9dc6eull,
+                                           0x8c07d0e2f27cbe4dull};
+  uint64_t c[4];
+  FieldHost::get().to_canonical(x, c);
+  uint64_t neg[4], q[4] = {0, 0, 0, 0};
+  unsigned __int128 borrow = 0;
+  for (int i = 0; i < 4; ++i) {  // neg = 2^256 - m (mod 2^256)
+    const unsigned __int128 d = (unsigned __int128)0 - x.v[i] - borrow;
+    neg[i] = (uint64_t)d;
+    borrow = (d >> 64) ? 1 : 0;
+  }
+  for (int i = 0; i < 4; ++i) {  // q = neg * pinv mod 2^256
+    unsigned __int128 carry = 0;
+    for (int j = 0; i + j < 4; ++j) {
+      const unsigned __int128 t = (unsigned __int128)neg[i] * kPinv256[j] + q[i + j] + carry;
+      q[i + j] = (uint64_t)t;
+      carry = t >> 64;
+    }
+  }
+  memcpy(out[0].w, c, 32);
+  memcpy(out[1].w, q, 32);
 }
 
 }  // namespace stark

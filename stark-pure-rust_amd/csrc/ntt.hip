@@ -23,7 +23,7 @@ namespace stark {
 // Twiddle of column exponent e (< n): direct table when the pass's
 // w_{Ns R} powers fit the 2^16-entry table, else the two-level lo * hi form.
 struct ColTw {
-  const fe* t16;    // t16[i] = w^(i * n / 2^l16), i < 2^l16
+  const fe* t16;    // Shoup pairs of t16[i] = w^(i * n / 2^l16), i < 2^l16 (t16[2i], t16[2i + 1])
   const fe* lo;     // lo[i]  = w^i,                i < 2^kb
   const fe* hi;     // hi[i]  = w^(i 2^kb),         i < 2^(log_n - kb)
   const fe* full;   // last pass only: full[c R + r] = w^(c r) (or null)
@@ -43,6 +43,20 @@ struct Sparse {
   uint32_t skip, zero_log, log_in;
 };
 
+// Two independent lazy products: interleaved in one asm block (fe_mul_lazy2) unless
+// STARK_NTT_DUAL=0 (A/B switch, tools/build_variant.sh).
+#ifndef STARK_NTT_DUAL
+#define STARK_NTT_DUAL 1
+#endif
+__device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, const fe& c, const fe& d) {
+#if STARK_NTT_DUAL
+  fe_mul_lazy2(r, s, a, b, c, d);
+#else
+  r = fe_mul_lazy(a, b);
+  s = fe_mul_lazy(c, d);
+#endif
+}
+
 template <int LOG_R, bool PERSIST>
 __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
@@ -50,8 +64,8 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
                                                           uint32_t log_tiles, uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
-  fe* sm = lds;          // R/2 small roots w_R^k
-  fe* X = lds + R / 2;   // [R][B] data image
+  fe* sm = lds;          // R/2 small roots w_R^k as Shoup pairs: sm[2k] = w_R^k, sm[2k + 1] = its quotient
+  fe* X = lds + R;       // [R][B] data image
   const uint32_t B = 1u << log_b;
   const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
   const uint32_t tid = threadIdx.x;
@@ -60,7 +74,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
   const uint32_t tile_mask = (1u << log_tiles) - 1;
 
-  for (uint32_t k = tid; k < R / 2; k += blockDim.x) sm[k] = small[k];
+  for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
 
   // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row).
   uint32_t eb[4], er[4];
@@ -100,11 +114,17 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
+          // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
+          // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
+          mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
+          mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
         } else if (lnr <= ct.l16) {
+          // Shoup pairs from the L2-resident t16 table: v < 2^256 -> [0, 2p)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
-            tw[t] = ct.t16[k << (ct.l16 - lnr)];
+            const fe* e = ct.t16 + 2 * (k << (ct.l16 - lnr));
+            v[t] = fe_mul_shoup(v[t], e[0], e[1]);
           }
         } else {
           const uint32_t unit = log_n - lnr;
@@ -113,9 +133,9 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
             const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) << unit;
             tw[t] = fe_mul(ct.lo[ex & (((uint64_t)1 << ct.kb) - 1)], ct.hi[ex >> ct.kb]);
           }
+          mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
+          mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
         }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = fe_mul_lazy(v[t], tw[t]);  // v < 4p, tw < p -> [0, 2p)
       }
       if (sp.skip == 0) {
 #pragma unroll
@@ -180,9 +200,10 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         fe x3 = X[((base + 3 * m) << log_b) + b];
         fe t1, t3;
         if (s != 0) {
-          const fe ta = sm[jj << (LOG_R - 1 - s)];  // w_{2m}^jj
-          t1 = fe_mul_lazy(x1, ta);
-          t3 = fe_mul_lazy(x3, ta);
+          const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
+          const fe ta = sm[ia], taq = sm[ia + 1];
+          t1 = fe_mul_shoup(x1, ta, taq);
+          t3 = fe_mul_shoup(x3, ta, taq);
         } else {
           t1 = x1;
           t3 = x3;
@@ -191,16 +212,17 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         }
         fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
         fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
-        const fe tc = sm[(jj + m) << (LOG_R - 2 - s)];  // w_{4m}^(jj+m)
+        const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
+        const fe tc = sm[ic], tcq = sm[ic + 1];
         fe t2;
         if (s != 0) {
-          const fe tb = sm[jj << (LOG_R - 2 - s)];  // w_{4m}^jj
-          t2 = fe_mul_lazy(x2, tb);
+          const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
+          t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
         } else {
           t2 = x2;
           fe_csub2p(t2);
         }
-        t3 = fe_mul_lazy(x3, tc);
+        t3 = fe_mul_shoup(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
         X[(base << log_b) + b] = x0;
@@ -373,27 +395,35 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     const HostFp wr = F.pow_u64(w, (uint64_t)1 << (log_n - l));
     HostFp a = F.one();
     for (uint32_t k = 0; k < (1u << (l - 1)); ++k) {
-      h_small.push_back(to_dev(a));
+      fe pr[2];
+      shoup_pair(a, pr);
+      h_small.push_back(pr[0]);
+      h_small.push_back(pr[1]);
       a = F.mul(a, wr);
     }
   }
-  if (h_small.empty()) h_small.push_back(to_dev(F.one()));
+  if (h_small.empty()) {
+    fe pr[2];
+    shoup_pair(F.one(), pr);
+    h_small.push_back(pr[0]);
+    h_small.push_back(pr[1]);
+  }
   // t16[i] = w^(i n / 2^l16): the w_{Ns R} powers of every pass with Ns R <= 2^l16
   // (2^16 entries; 2^18 from 2^25 on, where the middle pass of radix 2^9 has Ns R = 2^17 / 2^18).
   tw->l16 = log_n >= 25 ? 18 : (log_n < 16 ? log_n : 16);
   const size_t n16 = (size_t)1 << tw->l16;
-  std::vector<fe> h_t16(n16);
+  std::vector<fe> h_t16(2 * n16);
   {
     const HostFp w16 = F.pow_u64(w, (uint64_t)1 << (log_n - tw->l16));
     HostFp a = F.one();
     for (size_t i = 0; i < n16; ++i) {
-      h_t16[i] = to_dev(a);
+      shoup_pair(a, &h_t16[2 * i]);
       a = F.mul(a, w16);
     }
   }
   // Copies scaled by n^-1: the inverse's last pass multiplies every element by
   // a column twiddle anyway, so folding n^-1 into it makes the scale free.
-  std::vector<fe> h_hi_s(n_hi), h_t16_s(n16);
+  std::vector<fe> h_hi_s(n_hi), h_t16_s(2 * n16);
   {
     HostFp a = F.one();
     const HostFp step_hi = F.pow_u64(w, (uint64_t)1 << tw->kb);
@@ -404,25 +434,25 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     const HostFp w16 = F.pow_u64(w, (uint64_t)1 << (log_n - tw->l16));
     a = F.one();
     for (size_t i = 0; i < n16; ++i) {
-      h_t16_s[i] = to_dev(F.mul(a, tw->inv_n));
+      shoup_pair(F.mul(a, tw->inv_n), &h_t16_s[2 * i]);
       a = F.mul(a, w16);
     }
   }
-  const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 2 * n16) * sizeof(fe);
+  const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 4 * n16) * sizeof(fe);
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return STARK_ERR_OOM;
   tw->d_lo = (fe*)d;
   tw->d_hi = tw->d_lo + n_lo;
   tw->d_small = tw->d_hi + n_hi;
   tw->d_t16 = tw->d_small + h_small.size();
-  tw->d_hi_s = tw->d_t16 + n16;
+  tw->d_hi_s = tw->d_t16 + 2 * n16;
   tw->d_t16_s = tw->d_hi_s + n_hi;
   STARK_HIP(ctx, hipMemcpy(tw->d_lo, h_lo.data(), n_lo * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi, h_hi.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_small, h_small.data(), h_small.size() * sizeof(fe), hipMemcpyHostToDevice));
-  STARK_HIP(ctx, hipMemcpy(tw->d_t16, h_t16.data(), n16 * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_t16, h_t16.data(), 2 * n16 * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi_s, h_hi_s.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
-  STARK_HIP(ctx, hipMemcpy(tw->d_t16_s, h_t16_s.data(), n16 * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_t16_s, h_t16_s.data(), 2 * n16 * sizeof(fe), hipMemcpyHostToDevice));
   *out = tw.get();
   ctx->tw.emplace(key, std::move(tw));
   return STARK_OK;
@@ -534,7 +564,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     const uint32_t lb = choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
-    const size_t lds = ((size_t)elems + (1u << (lr - 1))) * sizeof(fe);
+    const size_t lds = ((size_t)elems + (1u << lr)) * sizeof(fe);  // data image + R/2 Shoup pairs
     const uint32_t log_tiles = log_n - lr - lb;
     const uint64_t total = (uint64_t)batch << log_tiles;
     const bool persist = kPersistent && total > kPersistentGrid;

@@ -1,69 +1,70 @@
-"""Generates stark-pure-rust_amd/csrc/fe_mul_asm.h: the BN254 Montgomery
+"""Generates stark-pure-rust_amd/csrc/fe_mul_asm.inc: the BN254 Montgomery
 product as ONE inline-asm block (FIPS product scanning, 128 v_mad_u64_u32 into
-a 96-bit column accumulator).
+a 96-bit column accumulator), and the DUAL form that interleaves two
+independent products instruction by instruction.
 
 Why one block: hipcc pads one wait state after every inline-asm block whose
 outputs the next VALU touches, so the per-word-product asm of fp_dev.h costs a
-`s_nop 0` per product (2,225 per radix-256 NTT pass thread).  Inside one block
-nothing is padded: VALU -> VALU VGPR/SGPR dependencies interlock in hardware
-on CDNA (the only hazards in this stream would be readlane/permlane/DPP/MFMA,
-none of which appear).
+`s_nop 0` per product.  Inside one block nothing is padded: VALU -> VALU
+VGPR/SGPR dependencies interlock in hardware on CDNA (the only hazards in this
+stream would be readlane/permlane/DPP/MFMA, none of which appear).
+
+Why the dual form: a product is one serial dependency chain (every
+v_mad_u64_u32 accumulates into the column the previous one wrote, every
+v_addc_co_u32 counts the carry the previous mad wrote).  At the 4 waves per
+SIMD the NTT pass kernel runs at, a lone chain leaves issue slots empty
+(tools/microbench/mul_forms.hip: 121 G products/s at 4 waves/SIMD vs 142 at
+8); two interleaved chains give each wave independent work for every slot.
 
 Registers: the column accumulator (a 64-bit pair + a carry word) lives in the
-fixed VGPRs v0-v3 declared as clobbers (inline asm has no sub-register operand
-modifiers, and the column shift needs the pairs' halves): two pairs alternate
-by column (see PAIRS); m[j] lives in the output register r[j] until r[j] is
-written; p's limbs and -p^-1 are SGPR operands (one SGPR read per VOP3 is allowed).
+fixed VGPRs v0-v3 (v4-v7 for the second product) declared as clobbers (inline
+asm has no sub-register operand modifiers, and the column shift needs the
+pairs' halves): two pairs alternate by column; m[j] lives in the output
+register r[j] until r[j] is written; p's limbs and -p^-1 are SGPR operands
+(one SGPR read per VOP3 is allowed).
+
+Measured on gfx950 (tools/microbench/isa_rates.hip, mul_forms.hip): carry ops
+are half rate in either encoding (VOP3 with an SGPR pair, or VOP2 with VCC:
+4.1-4.2 cycles per wave64 instruction), so the VCC form buys nothing (+3 % at
+4 waves/SIMD, -1 % at 8); the generator keeps it for the record.
 
 usage: python tools/gen_fe_mul_asm.py > stark-pure-rust_amd/csrc/fe_mul_asm.inc
 (included by fp_dev.h inside namespace stark)
 """
-# Two aligned accumulator pairs, A = v[0:1] and B = v[2:3], alternate by column: column k
-# accumulates into P_k (A for even k) and counts its carry-outs into the high register of the
-# other pair; the column shift is then one full-rate v_mov_b32 (P_{k+1}.lo <- P_k.hi) instead of
-# a half-rate v_pk_mov_b32 of one fixed pair (64-bit VOP3 operands need even-aligned pairs).
-PAIRS = [(0, 1), (2, 3)]
 
 
-def gen(lazy: bool) -> list:
-    # operands: outputs r0..r7 (%0..%7), carry pair (%8, "=&s"); inputs a0..a7 (%9..%16),
-    # b0..b7 (%17..%24), p0..p7 (%25..%32, SGPR), pinv (%33, SGPR)
-    r = [f"%{i}" for i in range(8)]
-    cy = "%8"
-    a = [f"%{9 + i}" for i in range(8)]
-    b = [f"%{17 + i}" for i in range(8)]
-    p = [f"%{25 + i}" for i in range(8)]
-    pinv = "%33"
-    # m[j] lives in the output register r[j]: m_j is last read in column j+7 and
-    # r[j] is first written at the end of column j+8.
-    m = r
+def stream(r, a, b, p, pinv, cy, pairs, carry="sgpr") -> list:
+    """Instruction list of one Montgomery product r = a*b*2^-256 (lazy, [0, 2p))."""
+    m = r          # m[j] lives in r[j]: last read in column j+7, r[j] first written at the end of column j+8
     out = []
-    state = {"first": True, "col_first": True, "k": 0}
+    st = {"first": True, "col_first": True, "k": 0}
 
     def pair(k):
-        return PAIRS[k & 1]
+        return pairs[k & 1]
 
     def mac(x, y):
-        lo, hi = pair(state["k"])
-        c = pair(state["k"] + 1)[1]      # carry count: the other pair's high register
+        lo, hi = pair(st["k"])
+        c = pair(st["k"] + 1)[1]      # carry count: the other pair's high register
         acc = f"v[{lo}:{hi}]"
-        src2 = "0" if state["first"] else acc
+        src2 = "0" if st["first"] else acc
         out.append(f"v_mad_u64_u32 {acc}, {cy}, {x}, {y}, {src2}")
-        if state["col_first"]:
+        if st["col_first"]:
             out.append(f"v_addc_co_u32 v{c}, {cy}, 0, 0, {cy}")
+        elif carry == "vcc":
+            out.append(f"v_addc_co_u32_e32 v{c}, vcc, 0, v{c}, vcc")
         else:
             out.append(f"v_addc_co_u32 v{c}, {cy}, v{c}, 0, {cy}")
-        state["col_first"] = False
-        state["first"] = False
+        st["col_first"] = False
+        st["first"] = False
 
     def shift():
         # P_{k+1} = (P_k.hi, carry count of column k)
-        lo, hi = pair(state["k"])
-        out.append(f"v_mov_b32 v{pair(state['k'] + 1)[0]}, v{hi}")
-        state["k"] += 1
+        lo, hi = pair(st["k"])
+        out.append(f"v_mov_b32 v{pair(st['k'] + 1)[0]}, v{hi}")
+        st["k"] += 1
 
     for k in range(8):
-        state["col_first"] = True
+        st["col_first"] = True
         for j in range(k):
             mac(a[j], b[k - j])
             mac(m[j], p[k - j])
@@ -72,7 +73,7 @@ def gen(lazy: bool) -> list:
         mac(m[k], p[0])
         shift()
     for k in range(8, 15):
-        state["col_first"] = True
+        st["col_first"] = True
         for j in range(k - 7, 8):
             mac(a[j], b[k - j])
             mac(m[j], p[k - j])
@@ -83,21 +84,112 @@ def gen(lazy: bool) -> list:
     return out
 
 
-def emit(name: str, lazy: bool) -> str:
-    lines = gen(lazy)
-    body = "\\n\\t".join(lines)
-    clob = ", ".join(f'"v{x}"' for x in [0, 1, 2, 3])
+def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
+    """Instruction list of one Shoup product r = a*w mod p, r in [0, 2p), for a < 2^256 and a
+    constant w < p with wq = floor(w 2^256 / p):
+      1. q ~ floor(a wq / 2^256) from columns 6..15 of a*wq (43 word products; the dropped
+         columns 0..5 sum to < 7 * 2^224, so q is exact or one short);
+      2. r = a w + q (2^256 - p) mod 2^256 = a w - q p (72 word products, column 7 without carries):
+         exact q gives r in [0, 2p) (Shoup), a short one r in [p, 3p);
+      3. q can only be short when the column-7 word of step 1 is >= 2^32 - 8 (probability 2^-29):
+         `flag` (an SGPR pair) marks such lanes and the wave subtracts 2p where r >= 2p only then.
+    115 v_mad_u64_u32 + 99 v_addc_co_u32 against the Montgomery product's 128 + 128 + 8 v_mul_lo."""
+    out = []
+    st = {"first": True, "col_first": True, "k": 0, "count": True}
+
+    def pair(k):
+        return pairs[k & 1]
+
+    def mac(x, y):
+        lo, hi = pair(st["k"])
+        c = pair(st["k"] + 1)[1]
+        acc = f"v[{lo}:{hi}]"
+        src2 = "0" if st["first"] else acc
+        out.append(f"v_mad_u64_u32 {acc}, {cy}, {x}, {y}, {src2}")
+        if st["count"]:
+            if st["col_first"]:
+                out.append(f"v_addc_co_u32 v{c}, {cy}, 0, 0, {cy}")
+            else:
+                out.append(f"v_addc_co_u32 v{c}, {cy}, v{c}, 0, {cy}")
+        st["col_first"] = False
+        st["first"] = False
+
+    def shift():
+        lo, hi = pair(st["k"])
+        out.append(f"v_mov_b32 v{pair(st['k'] + 1)[0]}, v{hi}")
+        st["k"] += 1
+
+    # 1. q from columns 6..15 of a * wq
+    st["k"] = 6
+    for c in range(6, 15):
+        st["col_first"] = True
+        for i in range(max(0, c - 7), min(7, c) + 1):
+            mac(a[i], wq[c - i])
+        if c == 7:
+            out.append(f"v_cmp_lt_u32 {flag}, -9, v{pair(7)[0]}")    # column-7 word >= 2^32 - 8
+        if c >= 8:
+            out.append(f"v_mov_b32 {q[c - 8]}, v{pair(c)[0]}")
+        if c < 14:
+            shift()
+    out.append(f"v_mov_b32 {q[7]}, v{pair(14)[1]}")   # column 15: q < 2^256, no carry beyond
+    # 2. r = low 256 bits of a*w + q*(2^256 - p)
+    st["k"] = 0
+    st["first"] = True
+    for c in range(8):
+        st["col_first"] = True
+        st["count"] = c < 7            # column 7's carry-out leaves the 256 bits
+        for i in range(c + 1):
+            mac(a[i], w[c - i])
+            mac(q[i], np[c - i])
+        out.append(f"v_mov_b32 {r[c]}, v{pair(c)[0]}")
+        if c < 7:
+            shift()
+    return out
+
+
+def csub2p_block(r, tmp, label, flag, p2) -> list:
+    """if (any lane flagged) r -= 2p where r >= 2p (r < 3p); flagged lanes only ever need it."""
+    out = [f"s_and_b64 {flag}, {flag}, exec",
+           f"s_cmp_eq_u64 {flag}, 0",
+           f"s_cbranch_scc1 .Lshoup_ok%={label}"]
+    # tmp = r - 2p (2p's limbs moved into tmp first: a borrow-in already uses the constant bus)
+    for i in range(8):
+        out.append(f"v_mov_b32 {tmp[i]}, {p2[i]:#010x}")
+    out.append(f"v_sub_co_u32 {tmp[0]}, vcc, {r[0]}, {tmp[0]}")
+    for i in range(1, 8):
+        out.append(f"v_subb_co_u32 {tmp[i]}, vcc, {r[i]}, {tmp[i]}, vcc")
+    for i in range(8):
+        out.append(f"v_cndmask_b32 {r[i]}, {tmp[i]}, {r[i]}, vcc")
+    out.append(f".Lshoup_ok%={label}:")
+    return out
+
+
+PROLOGUE = '''  const uint32_t P0 = STARK_P0, P1 = STARK_P1, P2 = STARK_P2, P3 = STARK_P3, P4 = STARK_P4, P5 = STARK_P5,
+                 P6 = STARK_P6, P7 = STARK_P7, PINV = STARK_PINV32;'''
+
+
+def ops(prefix, var, start):
+    return [f"%{start + i}" for i in range(8)], ", ".join(f'"v"({var}.w[{i}])' for i in range(8))
+
+
+def emit_single(name: str, carry: str = "sgpr") -> str:
+    r = [f"%{i}" for i in range(8)]
+    cy = "%8" if carry == "sgpr" else "vcc"
+    a = [f"%{9 + i}" for i in range(8)]
+    b = [f"%{17 + i}" for i in range(8)]
+    p = [f"%{25 + i}" for i in range(8)]
+    body = "\\n\\t".join(stream(r, a, b, p, "%33", cy, [(0, 1), (2, 3)], carry))
+    clob = ", ".join(f'"v{x}"' for x in range(4)) + (', "vcc"' if carry == "vcc" else "")
     outs = ", ".join(f'"=&v"(r.w[{i}])' for i in range(8))
     ins_a = ", ".join(f'"v"(a.w[{i}])' for i in range(8))
     ins_b = ", ".join(f'"v"(b.w[{i}])' for i in range(8))
     ins_p = ", ".join(f'"s"(P{i})' for i in range(8))
     return f'''// Montgomery product a*b*2^-256 mod p, result in [0, 2p) (not reduced).
-// Inputs < 2^256 with a*b < 2^256 * p (e.g. a < 4p, b < p).  Generated by tools/gen_fe_mul_asm.py.
+// Inputs < 2^256 with a*b < 2^256 * p (e.g. a < 4p, b < p).
 __device__ __forceinline__ fe {name}(const fe& a, const fe& b) {{
   fe r;
   uint64_t cy;
-  const uint32_t P0 = STARK_P0, P1 = STARK_P1, P2 = STARK_P2, P3 = STARK_P3, P4 = STARK_P4, P5 = STARK_P5,
-                 P6 = STARK_P6, P7 = STARK_P7, PINV = STARK_PINV32;
+{PROLOGUE}
   asm("{body}"
       : {outs}, "=&s"(cy)
       : {ins_a},
@@ -110,6 +202,85 @@ __device__ __forceinline__ fe {name}(const fe& a, const fe& b) {{
 '''
 
 
+def emit_dual(name: str) -> str:
+    """r = a*b, s = c*d (two independent lazy Montgomery products), interleaved."""
+    r = [f"%{i}" for i in range(8)]
+    s = [f"%{8 + i}" for i in range(8)]
+    cya, cyb = "%16", "%17"
+    a = [f"%{18 + i}" for i in range(8)]
+    b = [f"%{26 + i}" for i in range(8)]
+    c = [f"%{34 + i}" for i in range(8)]
+    d = [f"%{42 + i}" for i in range(8)]
+    p = [f"%{50 + i}" for i in range(8)]
+    pinv = "%58"
+    sa = stream(r, a, b, p, pinv, cya, [(0, 1), (2, 3)])
+    sb = stream(s, c, d, p, pinv, cyb, [(4, 5), (6, 7)])
+    assert len(sa) == len(sb)
+    body = "\\n\\t".join(x for pair in zip(sa, sb) for x in pair)
+    clob = ", ".join(f'"v{x}"' for x in range(8))
+    outs = ", ".join([f'"=&v"(r.w[{i}])' for i in range(8)] + [f'"=&v"(s.w[{i}])' for i in range(8)])
+    ins = ", ".join([f'"v"(a.w[{i}])' for i in range(8)] + [f'"v"(b.w[{i}])' for i in range(8)] +
+                    [f'"v"(c.w[{i}])' for i in range(8)] + [f'"v"(d.w[{i}])' for i in range(8)])
+    ins_p = ", ".join(f'"s"(P{i})' for i in range(8))
+    return f'''// Two independent Montgomery products r = a*b*2^-256, s = c*d*2^-256 (each in [0, 2p), same
+// input bounds as fe_mul_lazy), their instruction streams interleaved one for one.
+__device__ __forceinline__ void {name}(fe& r, fe& s, const fe& a, const fe& b, const fe& c, const fe& d) {{
+  uint64_t cya, cyb;
+{PROLOGUE}
+  asm("{body}"
+      : {outs}, "=&s"(cya), "=&s"(cyb)
+      : {ins},
+        {ins_p}, "s"(PINV)
+      : {clob});
+  (void)cya;
+  (void)cyb;
+}}
+'''
+
+
+NP = [0x0fffffff, 0xbc1e0a6c, 0x86468f6e, 0xd7cc17b7, 0x7e7ea7a2, 0x47afba49, 0x1ece5fd6, 0xcf9bb18d]  # 2^256 - p
+P2 = [0xe0000002, 0x87c3eb27, 0xf372e122, 0x5067d090, 0x0302b0ba, 0x70a08b6d, 0xc2634053, 0x60c89ce5]  # 2p
+
+
+def emit_shoup(name: str) -> str:
+    r = [f"%{i}" for i in range(8)]
+    q = [f"%{8 + i}" for i in range(8)]
+    cy, flag = "%16", "%17"
+    a = [f"%{18 + i}" for i in range(8)]
+    w = [f"%{26 + i}" for i in range(8)]
+    wq = [f"%{34 + i}" for i in range(8)]
+    np_ = [f"%{42 + i}" for i in range(8)]
+    body_l = shoup_stream(r, q, a, w, wq, np_, cy, [(0, 1), (2, 3)], flag)
+    body_l += csub2p_block(r, q, "a", flag, P2)    # q is dead by then: reuse it as the temporary
+    body = "\\n\\t".join(body_l)
+    outs = ", ".join([f'"=&v"(r.w[{i}])' for i in range(8)] + [f'"=&v"(q{i})' for i in range(8)])
+    ins = ", ".join([f'"v"(a.w[{i}])' for i in range(8)] + [f'"v"(w.w[{i}])' for i in range(8)] +
+                    [f'"v"(wq.w[{i}])' for i in range(8)])
+    ins_np = ", ".join(f'"s"(N{i})' for i in range(8))
+    decl_n = ", ".join(f"N{i} = {NP[i]:#010x}u" for i in range(8))
+    return f'''// Shoup product by a constant: r = a*w mod p in [0, 2p) for any a < 2^256, w < p canonical and
+// wq = floor(w 2^256 / p) (tools/gen_fe_mul_asm.py shoup_stream: 115 v_mad_u64_u32).
+__device__ __forceinline__ fe {name}(const fe& a, const fe& w, const fe& wq) {{
+  fe r;
+  uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
+  uint64_t cy, flag;
+  const uint32_t {decl_n};
+  asm("{body}"
+      : {outs}, "=&s"(cy), "=&s"(flag)
+      : {ins},
+        {ins_np}
+      : "v0", "v1", "v2", "v3", "vcc", "scc");
+  (void)cy;
+  (void)flag;
+  return r;
+}}
+'''
+
+
 if __name__ == "__main__":
     print("// GENERATED by tools/gen_fe_mul_asm.py -- do not edit.  Included by fp_dev.h.")
-    print(emit("fe_mul_lazy", True))
+    print(emit_single("fe_mul_lazy"))
+    print(emit_dual("fe_mul_lazy2"))
+    print("// The VCC-carry (VOP2 addc) form of fe_mul_lazy: A/B reference only (tools/microbench/mul_forms.hip).")
+    print(emit_single("fe_mul_lazy_vcc", "vcc"))
+    print(emit_shoup("fe_mul_shoup"))
