@@ -48,6 +48,13 @@ struct Sparse {
 #ifndef STARK_NTT_DUAL
 #define STARK_NTT_DUAL 1
 #endif
+// Shoup products stay one chain per block: the interleaved pair (fe_mul_shoup2 in the r02
+// experiment) measured 1.867 vs 1.843 ms per 2^24 transform.
+__device__ __forceinline__ void shoup2(fe& r, fe& s, const fe& a, const fe& w, const fe& wq, const fe& c,
+                                       const fe& x, const fe& xq) {
+  r = fe_mul_shoup(a, w, wq);
+  s = fe_mul_shoup(c, x, xq);
+}
 __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, const fe& c, const fe& d) {
 #if STARK_NTT_DUAL
   fe_mul_lazy2(r, s, a, b, c, d);
@@ -57,7 +64,12 @@ __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, con
 #endif
 }
 
-template <int LOG_R, bool PERSIST>
+// COL: the pass's column-twiddle source, fixed per launch so each instance carries one product
+// form (kColNone: first pass; kColFull: last-pass full table, Montgomery; kColT16: Shoup pairs;
+// kColTwoLevel: lo * hi, Montgomery).
+enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
+
+template <int LOG_R, bool PERSIST, int COL>
 __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
                                                           const fe* __restrict__ small, fe scale, int do_scale,
@@ -107,10 +119,10 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
 
     // ---- column twiddle, scatter into the bit-reversed LDS image ----
     if (active) {
-      if (log_ns != 0) {
+      if (COL != kColNone) {
         const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
         fe tw[4];
-        if (ct.full != nullptr) {  // the transform's last pass (lnr == log_n) with a full table
+        if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
@@ -118,14 +130,16 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
           // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
           mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
           mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
-        } else if (lnr <= ct.l16) {
+        } else if (COL == kColT16) {
           // Shoup pairs from the L2-resident t16 table: v < 2^256 -> [0, 2p)
+          const fe* e[4];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
-            const fe* e = ct.t16 + 2 * (k << (ct.l16 - lnr));
-            v[t] = fe_mul_shoup(v[t], e[0], e[1]);
+            e[t] = ct.t16 + 2 * (k << (ct.l16 - lnr));
           }
+          shoup2(v[0], v[1], v[0], e[0][0], e[0][1], v[1], e[1][0], e[1][1]);
+          shoup2(v[2], v[3], v[2], e[2][0], e[2][1], v[3], e[3][0], e[3][1]);
         } else {
           const uint32_t unit = log_n - lnr;
 #pragma unroll
@@ -202,8 +216,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         if (s != 0) {
           const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
           const fe ta = sm[ia], taq = sm[ia + 1];
-          t1 = fe_mul_shoup(x1, ta, taq);
-          t3 = fe_mul_shoup(x3, ta, taq);
+          shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
         } else {
           t1 = x1;
           t3 = x3;
@@ -335,16 +348,34 @@ uint32_t choose_log_b(uint32_t log_n, uint32_t log_r) {
 typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, fe, int, uint32_t,
                         uint32_t, Sparse);
 
-pass_fn pass_kernel(uint32_t log_r, bool persist) {
+template <int LOG_R>
+pass_fn pass_kernel_r(bool persist, int col) {
+  if (kPersistent && persist) {
+    switch (col) {
+      case kColNone: return ntt_pass_kernel<LOG_R, kPersistent, kColNone>;
+      case kColFull: return ntt_pass_kernel<LOG_R, kPersistent, kColFull>;
+      case kColT16: return ntt_pass_kernel<LOG_R, kPersistent, kColT16>;
+      default: return ntt_pass_kernel<LOG_R, kPersistent, kColTwoLevel>;
+    }
+  }
+  switch (col) {
+    case kColNone: return ntt_pass_kernel<LOG_R, false, kColNone>;
+    case kColFull: return ntt_pass_kernel<LOG_R, false, kColFull>;
+    case kColT16: return ntt_pass_kernel<LOG_R, false, kColT16>;
+    default: return ntt_pass_kernel<LOG_R, false, kColTwoLevel>;
+  }
+}
+
+pass_fn pass_kernel(uint32_t log_r, bool persist, int col) {
   switch (log_r) {
-    case 2: return persist ? ntt_pass_kernel<2, true> : ntt_pass_kernel<2, false>;
-    case 3: return persist ? ntt_pass_kernel<3, true> : ntt_pass_kernel<3, false>;
-    case 4: return persist ? ntt_pass_kernel<4, true> : ntt_pass_kernel<4, false>;
-    case 5: return persist ? ntt_pass_kernel<5, true> : ntt_pass_kernel<5, false>;
-    case 6: return persist ? ntt_pass_kernel<6, true> : ntt_pass_kernel<6, false>;
-    case 7: return persist ? ntt_pass_kernel<7, true> : ntt_pass_kernel<7, false>;
-    case 8: return persist ? ntt_pass_kernel<8, true> : ntt_pass_kernel<8, false>;
-    case 9: return persist ? ntt_pass_kernel<9, true> : ntt_pass_kernel<9, false>;
+    case 2: return pass_kernel_r<2>(persist, col);
+    case 3: return pass_kernel_r<3>(persist, col);
+    case 4: return pass_kernel_r<4>(persist, col);
+    case 5: return pass_kernel_r<5>(persist, col);
+    case 6: return pass_kernel_r<6>(persist, col);
+    case 7: return pass_kernel_r<7>(persist, col);
+    case 8: return pass_kernel_r<8>(persist, col);
+    case 9: return pass_kernel_r<9>(persist, col);
     default: return nullptr;
   }
 }
@@ -578,7 +609,8 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
       if (st != STARK_OK) return st;
     }
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
-    hipLaunchKernelGGL(pass_kernel(lr, persist), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
+    const int col = log_ns == 0 ? kColNone : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
+    hipLaunchKernelGGL(pass_kernel(lr, persist, col), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], scale, (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total, sp);
     STARK_HIP(ctx, hipGetLastError());
