@@ -155,6 +155,9 @@ stark_status stark_merkle_update_dev(stark_merkle_tree* tree, const uint8_t* d_l
                                      size_t leaf_len, void* stream);
 /* width() (merkle_tree.rs:62) */
 size_t stark_merkle_width(const stark_merkle_tree* tree);
+/* Bytes per leaf of the last update (0 before one): sizes gen_proofs' leaves_out for a caller
+ * that, like MerkleTree::gen_proofs, does not keep the leaves (no reference counterpart). */
+size_t stark_merkle_leaf_len(const stark_merkle_tree* tree);
 /* get_root() (merkle_tree.rs:66): *root_len = 32, or 0 before the first
  * gen_proofs (the reference's H::default() = empty digest, :19). */
 stark_status stark_merkle_get_root(const stark_merkle_tree* tree, uint8_t root[32], size_t* root_len);

@@ -692,6 +692,7 @@ stark_status stark_open_batch(stark_ctx* ctx, const stark_open_req* reqs, size_t
 }
 
 size_t stark_merkle_width(const stark_merkle_tree* t) { return t ? t->n : 0; }
+size_t stark_merkle_leaf_len(const stark_merkle_tree* t) { return t ? t->leaf_len : 0; }
 
 stark_status stark_merkle_get_root(const stark_merkle_tree* t, uint8_t root[32], size_t* root_len) {
   if (!t || !root_len) return STARK_ERR_BAD_ARG;

@@ -66,6 +66,7 @@ _SIGNATURES = {
     "stark_merkle_update": ([_vp, _u8p, ctypes.c_size_t, ctypes.c_size_t], ctypes.c_int),
     "stark_merkle_update_dev": ([_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp], ctypes.c_int),
     "stark_merkle_width": ([_vp], ctypes.c_size_t),
+    "stark_merkle_leaf_len": ([_vp], ctypes.c_size_t),
     "stark_merkle_get_root": ([_vp, _u8p, _szp], ctypes.c_int),
     "stark_merkle_gen_proofs": ([_vp, _szp, ctypes.c_size_t, _u8p, _u8p], ctypes.c_int),
     "stark_merkle_verify": ([_u8p, _szp, ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t],

@@ -1,0 +1,49 @@
+"""The C ABI from a non-Python caller: tests/abi_client/shim_flow.cpp makes exactly the calls of the
+Rust shim in INTEGRATION.md (best_fft -> MerkleProofInPlace new/update/gen_proofs/get_root ->
+prove_low_degree -> serde JSON).  CPU: the program builds and links against libstark_hip.so.
+GPU: its outputs equal the oracle's best_fft (fft.rs:327-357), Merkle root and paths
+(merkle_proof_in_place.rs:106-206) and FRI proof JSON (fri.rs:46-224)."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CLIENT = os.path.join(HERE, "abi_client")
+BIN = os.path.join(CLIENT, "shim_flow")
+
+
+def test_client_builds_and_links():
+    subprocess.run(["make", "-s", "-C", CLIENT], check=True)
+    out = subprocess.run(["ldd", BIN], capture_output=True, text=True, check=True).stdout
+    assert "libstark_hip.so" in out and "not found" not in out.split("libstark_hip.so")[1].splitlines()[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,exclude", [(12, 8), (16, 8), (10, 0)])
+def test_client_matches_oracle(oracle, tmp_path, log_n, exclude):
+    assert os.path.exists(BIN), "build() compiles tests/abi_client/shim_flow"
+    n = 1 << log_n
+    coeffs = O.random_elements(n // 4, 0x5EED0300 + log_n)
+    w = O.root_of_unity(log_n)
+    idx = [0, 1, n - 1, 5, 5, n // 2 + 3]
+    blob = struct.pack("<4I", log_n, len(coeffs), len(idx), exclude) + O.to_limbs([w]).tobytes() + \
+        coeffs.tobytes() + np.array(idx, dtype=np.uint64).tobytes()
+    (tmp_path / "in.bin").write_bytes(blob)
+    r = subprocess.run([BIN, str(tmp_path / "in.bin"), str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    evals = np.frombuffer((tmp_path / "evals.bin").read_bytes(), dtype=np.uint64).reshape(-1, 4)
+    assert np.array_equal(evals, oracle.best_fft(coeffs, w, log_n, cpus=8))
+    root, paths = oracle.merkle(evals.tobytes(), n, 32, idx, chunks=4)
+    assert (tmp_path / "merkle_root.bin").read_bytes() == root
+    nodes = (tmp_path / "merkle_nodes.bin").read_bytes()
+    assert [[nodes[(i * log_n + d) * 32:(i * log_n + d + 1) * 32] for d in range(log_n)]
+            for i in range(len(idx))] == paths
+    leaves = (tmp_path / "merkle_leaves.bin").read_bytes()
+    assert leaves == b"".join(evals[i].tobytes() for i in idx)
+    want = oracle.prove_low_degree_json(evals, w, n // 4, exclude, chunks=4)
+    assert (tmp_path / "fri.json").read_text() == want

@@ -236,3 +236,60 @@ def test_transpose_and_twiddle(ctx):
     finally:
         ctx.free(d)
         ctx.free(e)
+
+
+def _worker_rccl_world1(port, out_q):
+    """Backend "nccl" (RCCL) at world 1 on the box's one GPU: the code the 8-GPU bench runs --
+    cyclic_ntt_pipelined's async all_to_all_single on RCCL's stream, the plain cyclic_ntt exchange
+    and DistributedMerkle's all_gather_object -- with trivial exchanges."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import faulthandler
+    faulthandler.dump_traceback_later(100, exit=True)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"),
+                            timeout=datetime.timedelta(seconds=90))
+    import stark_amd as S
+    from stark_amd.distributed import DistributedMerkle, GpuOps, cyclic_ntt, cyclic_ntt_pipelined
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = S.Context(0)
+    ops = GpuOps(ctx)
+    log_n = 14
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    ins = [O.random_elements(n, 0x5EED0400 + i) for i in range(2)]
+    pairs = [(torch.from_numpy(h.view(np.int64).copy()).cuda(), torch.empty((n, 4), dtype=torch.int64).cuda())
+             for h in ins]
+    cyclic_ntt_pipelined(pairs, 2, log_n, w, ops)
+    torch.cuda.synchronize()
+    res = {"pipelined": [b.cpu().numpy().view(np.uint64).copy() for _, b in pairs]}
+    x = torch.from_numpy(ins[0].view(np.int64).copy()).cuda()
+    res["cyclic"] = cyclic_ntt(x, log_n, w, ops).cpu().numpy().view(np.uint64).copy()
+    leaves = torch.from_numpy(ins[1].view(np.int64).copy()).cuda()
+    res["merkle_root"] = DistributedMerkle(ops).commit(leaves, n, 32)
+    torch.cuda.synchronize()
+    out_q.put(res)
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_pipelined_and_merkle():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl_world1, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=110)
+    p.join(timeout=60)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0
+    o = O.Oracle()
+    log_n = 14
+    w = O.root_of_unity(log_n)
+    ins = [O.random_elements(1 << log_n, 0x5EED0400 + i) for i in range(2)]
+    for h, got in zip(ins, res["pipelined"]):
+        assert np.array_equal(got, o.best_fft(h, w, log_n, cpus=8))
+    assert np.array_equal(res["cyclic"], o.best_fft(ins[0], w, log_n, cpus=8))
+    root, _ = o.merkle(ins[1].tobytes(), 1 << log_n, 32)
+    assert res["merkle_root"] == root
