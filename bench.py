@@ -35,13 +35,16 @@ import torch.distributed as dist  # noqa: E402
 S = None  # stark_amd, imported in main() once this process is known to be a rank
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# VALU bound of the modular product: every Montgomery product issues 128
-# v_mad_u64_u32 + 128 carry ops, all half-rate on gfx950 (4 cycles per wave64,
-# tools/microbench/isa_lat.hip): 1024 SIMDs x 2.4 GHz x 64 lanes / (256 x 4).
-MODMUL_PEAK = 1024 * 2.4e9 * 64 / (256 * 4)
+# Issue cost of these VALU streams (64-bit mads, carry chains, alignbit/xor mixes): 4.0 cycles per
+# wave64 instruction at the in-kernel clock (tools/microbench/mix_rates.hip, profiles/r02_mix_rates.txt).
+ISSUE_CYCLES = 4.0
+SIMDS = 1024
+# The Shoup constant product alone (tools/microbench/shoup_check.hip, 4 waves/SIMD like the pass
+# kernel): 148.7 G products/s (profiles/r02_shoup_product.txt).
+SHOUP_PRODUCT_PEAK = 148.69e9
 LOG_N = 24
-PROFILE = os.path.join(ROOT, "profiles", "r01_summary.json")
-SQ_PROFILE = os.path.join(ROOT, "profiles", "r01_ntt_sq_counters.json")
+PROFILE = os.path.join(ROOT, "profiles", "r02_summary.json")
+PMC = os.path.join(ROOT, "profiles", "r02_pmc.json")
 LARGE = os.path.join(ROOT, "tests", "golden", "large_digests.json")
 
 
@@ -289,19 +292,22 @@ MERKLE_SQ = os.path.join(ROOT, "profiles", "r02_merkle_sq_counters.json")
 def merkle_valu_roofline(n: int, ms: float) -> dict:
     """Blake2s issue roofline of a 2^log n x 32-B tree build: n leaf compressions (one 32-B block
     each) + n - 1 node compressions (64-B blocks) = 2n - 1.  The VALU instructions per compression
-    and the clock under load come from the committed rocprofv3 SQ pass (MERKLE_SQ); the issue
-    bound prices them at VOP2 2.3 / VOP3 4.6 cycles per wave64 instruction (tools/microbench)."""
+    (SQ_INSTS_VALU of the leaf-level kernel x 64 / its compressions) and the clock under load come
+    from the committed rocprofv3 pass (MERKLE_SQ); each wave64 instruction issues in ISSUE_CYCLES
+    (the Blake2s G stream, tools/microbench/mix_rates.hip).  `leaf_kernel_issue_frac` is the leaf
+    kernel's own issue-bound time over its measured time (same profile)."""
     comp = 2 * n - 1
     out = {"compressions": comp, "achieved_compressions_per_s": comp / (ms / 1000.0)}
     try:
         prof = json.load(open(MERKLE_SQ))
         per = prof["valu_insts_per_compression"]
-        cyc = prof["issue_cycles_per_compression"]
-        ghz = prof.get("effective_clock_ghz", 2.4)
-        peak = 1024 * ghz * 1e9 * 64 / cyc          # compressions/s at that clock, all SIMDs issuing
-        out.update({"valu_insts_per_compression": per, "issue_cycles_per_compression_wave64": cyc,
+        cyc = per * ISSUE_CYCLES / 64.0                  # SIMD cycles per compression (one lane's share)
+        ghz = prof["effective_clock_ghz"]
+        peak = SIMDS * ghz * 1e9 / cyc                   # compressions/s with every SIMD issuing
+        out.update({"valu_insts_per_compression": per, "issue_cycles_per_wave64_instruction": ISSUE_CYCLES,
                     "clock_ghz": ghz, "peak_compressions_per_s": peak,
                     "frac": round(out["achieved_compressions_per_s"] / peak, 4),
+                    "leaf_kernel_issue_frac": prof["leaf_kernel_issue_frac"],
                     "sq_profile": os.path.relpath(MERKLE_SQ, ROOT)})
     except (OSError, KeyError, ValueError):
         pass
@@ -606,19 +612,25 @@ def main():
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     plan = S.ntt_plan(log_n)
     passes = len(plan)
-    kname = f"stark::ntt_pass_kernel<{plan[-1]}, false>"
-    traffic = None
-    prof_avg = prof_med = None
+    # The pass kernels of this transform (csrc/ntt.hip: ntt_pass_kernel<LOG_R, persistent, COL>, COL =
+    # 0 first pass, 2 Shoup t16 column twiddles, 1 the last pass's full table): per-launch HBM bytes,
+    # rocprof times and SQ counters from the committed round-2 profiles of this exact command line.
+    knames = []
+    for i, r in enumerate(plan):
+        col = 0 if i == 0 else (1 if i == passes - 1 and 17 <= log_n <= 26 else 2)
+        knames.append(f"stark::ntt_pass_kernel<{r}, false, {col}>")
+    traffic = prof_avg = prof_med = None
+    sq = {}
     try:
         prof = json.load(open(PROFILE))
-        rec = prof["pmc_bytes_per_launch"].get(kname)
-        if rec and log_n == 24:
-            # HBM bytes of one transform: the PMC per-launch average (FETCH_SIZE x 2 + WRITE_SIZE,
-            # MI355X_MICROARCH.md) x the transform's launches.
-            traffic = passes * rec["hbm_bytes"]
-            k = prof["kernels"][kname]
-            prof_avg = k["avg_ns"] / 1e6
-            prof_med = k.get("steady_median_ns", 0) / 1e6 or None
+        pmc = json.load(open(PMC))["kernels"]
+        if log_n == 24 and all(k in prof["pmc_bytes_per_launch"] for k in knames):
+            # HBM bytes of one transform: per-launch FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md)
+            # summed over the transform's launches.
+            traffic = sum(prof["pmc_bytes_per_launch"][k]["hbm_bytes"] for k in knames)
+            prof_avg = sum(prof["kernels"][k]["avg_ns"] for k in knames) / 1e6
+            prof_med = sum(prof["kernels"][k]["steady_median_ns"] for k in knames) / 1e6
+            sq = {k: pmc[k] for k in knames}
     except (OSError, KeyError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -626,41 +638,27 @@ def main():
                 "traffic_over_algorithmic": round(traffic / ntt_bytes, 3) if traffic else None,
                 "kernel": f"ntt_pass_kernel x {passes} launches (radices 2^{plan}) per 2^{log_n} transform",
                 "ms_per_transform": round(ev_ms, 4), "avg_launch_ms": round(ev_ms / passes, 4),
-                "rocprof_avg_launch_ms": round(prof_avg, 4) if prof_avg else None,
-                "rocprof_steady_median_launch_ms": round(prof_med, 4) if prof_med else None,
+                "rocprof_ms_per_transform_avg": round(prof_avg, 4) if prof_avg else None,
+                "rocprof_ms_per_transform_steady_median": round(prof_med, 4) if prof_med else None,
                 "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
     modmuls = ntt_products(log_n, plan)
-    valu = {"bound": "valu (half-rate v_mad_u64_u32 + carry ops)", "modmuls_per_transform": modmuls,
-            "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0), "peak_modmul_per_s": MODMUL_PEAK}
-    valu["frac"] = round(valu["achieved_modmul_per_s"] / MODMUL_PEAK, 4)
-    try:
-        # The peak above assumes 2.4 GHz; the pass kernel's clock under load, from the committed
-        # GRBM_GUI_ACTIVE pass (profiles/r01_clock_counters.json), prices the bound at the real clock.
-        clk = json.load(open(os.path.join(ROOT, "profiles", "r01_clock_counters.json")))["kernels"]
-        ghz = next(v["effective_clock_ghz"] for k, v in clk.items() if "ntt_pass_kernel<8" in k)
-        valu["measured_clock_ghz"] = ghz
-        valu["frac_at_measured_clock"] = round(valu["frac"] * 2.4 / ghz, 4)
-        roofline["valu_frac_at_measured_clock"] = valu["frac_at_measured_clock"]
-    except (OSError, KeyError, ValueError, StopIteration):
-        pass
-    if world == 1:
-        # VALU issue occupancy of the dominant kernel.  Each product issues 128 v_mad_u64_u32 + 128
-        # v_addc_co_u32, measured at ~4.6 cycles per wave64 instruction (tools/microbench/isa_rates.hip);
-        # their share of the SIMD-cycles of the measured launches (1024 SIMDs x 2.4 GHz):
-        simd_cycles = 1024 * 2.4e9 * ev_ms / 1000.0
-        valu["mad_carry_issue_frac"] = round(modmuls * 256 / 64 * 4.6 / simd_cycles, 3)
-        try:
-            # All VALU instructions (committed rocprofv3 SQ_INSTS_VALU of the same kernel) at 2.3 cycles
-            # (VOP2) to 4.6 cycles (VOP3 / carry ops): the range of the whole issue occupancy.
-            sq = json.load(open(SQ_PROFILE))["kernels"][kname]
-            if log_n == 24:
-                insts = sq["SQ_INSTS_VALU"] * passes
-                valu["sq_insts_valu_per_launch"] = sq["SQ_INSTS_VALU"]
-                valu["all_valu_issue_frac_range"] = [round(insts * 2.3 / simd_cycles, 3),
-                                                     round(insts * 4.6 / simd_cycles, 3)]
-                valu["sq_profile"] = os.path.relpath(SQ_PROFILE, ROOT)
-        except (OSError, KeyError, ValueError):
-            pass
+    valu = {"bound": f"VALU issue ({ISSUE_CYCLES} cycles per wave64 instruction, measured)",
+            "modmuls_per_transform": modmuls, "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0),
+            "shoup_product_peak_per_s": SHOUP_PRODUCT_PEAK}
+    valu["product_frac"] = round(valu["achieved_modmul_per_s"] / SHOUP_PRODUCT_PEAK, 4)
+    if sq:
+        # Issue-bound time of the transform: each pass's SQ_INSTS_VALU x ISSUE_CYCLES over the chip's
+        # 1024 SIMDs at that pass's measured clock (GRBM_GUI_ACTIVE / 8 XCDs / duration); frac =
+        # that time over the measured transform time (HIP events above).
+        issue_ms = sum(v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS / (v["effective_clock_ghz"] * 1e9) * 1e3
+                       for v in sq.values())
+        insts = sum(v["SQ_INSTS_VALU"] for v in sq.values())
+        valu.update({"sq_insts_valu_per_transform": insts,
+                     "valu_lane_insts_per_element": round(insts * 64 / n, 1),
+                     "measured_clock_ghz": [round(v["effective_clock_ghz"], 3) for v in sq.values()],
+                     "issue_bound_ms_per_transform": round(issue_ms, 4),
+                     "frac": round(issue_ms / ev_ms, 4), "sq_profile": os.path.relpath(PMC, ROOT)})
+        roofline["valu_issue_frac"] = valu["frac"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
