@@ -50,10 +50,12 @@ struct Sparse {
 #endif
 // Shoup products stay one chain per block: the interleaved pair (fe_mul_shoup2 in the r02
 // experiment) measured 1.867 vs 1.843 ms per 2^24 transform.
+__device__ __forceinline__ fe shoup_a(const fe& a, const fe& w, const fe& wq) { return fe_mul_shoup(a, w, wq); }
+__device__ __forceinline__ fe shoup_b(const fe& a, const fe& w, const fe& wq) { return fe_mul_shoup(a, w, wq); }
 __device__ __forceinline__ void shoup2(fe& r, fe& s, const fe& a, const fe& w, const fe& wq, const fe& c,
                                        const fe& x, const fe& xq) {
-  r = fe_mul_shoup(a, w, wq);
-  s = fe_mul_shoup(c, x, xq);
+  r = shoup_a(a, w, wq);
+  s = shoup_b(c, x, xq);
 }
 __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, const fe& c, const fe& d) {
 #if STARK_NTT_DUAL
@@ -230,12 +232,12 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         fe t2;
         if (s != 0) {
           const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
-          t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
+          t2 = shoup_a(x2, sm[ib], sm[ib + 1]);
         } else {
           t2 = x2;
           fe_csub2p(t2);
         }
-        t3 = fe_mul_shoup(x3, tc, tcq);
+        t3 = shoup_b(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
         X[(base << log_b) + b] = x0;

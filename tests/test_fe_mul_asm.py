@@ -10,6 +10,8 @@ import random
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
@@ -159,24 +161,31 @@ def test_generated_dual_product():
         assert x % P == a * b * rinv % P and y % P == c * d * rinv % P
 
 
-def _shoup_ops():
-    r = [f"%{i}" for i in range(8)]
-    q = [f"%{8 + i}" for i in range(8)]
-    ops = G.shoup_stream(r, q, [f"%{18 + i}" for i in range(8)], [f"%{26 + i}" for i in range(8)],
-                         [f"%{34 + i}" for i in range(8)], [f"%{42 + i}" for i in range(8)], "%16",
-                         [(0, 1), (2, 3)], "%17")
-    return ops + G.csub2p_block(r, q, "a", "%17", G.P2)
+def _shoup_ops(qbase=None, rbase=None):
+    """emit_shoup's operand map: r = %0..%7 (or pinned v[rbase + 2c]), q = %8.. unless in place,
+    then cy, flag, a, w, wq, 2^256 - p."""
+    r = [f"%{i}" for i in range(8)] if rbase is None else [f"v{rbase + 2 * i}" for i in range(8)]
+    nq = 0 if qbase is not None else 8
+    q = [f"%{8 + i}" for i in range(nq)]
+    b = 8 + nq
+    ops = G.shoup_stream(r, q, [f"%{b + 2 + i}" for i in range(8)], [f"%{b + 10 + i}" for i in range(8)],
+                         [f"%{b + 18 + i}" for i in range(8)], [f"%{b + 26 + i}" for i in range(8)], f"%{b}",
+                         [(0, 1), (2, 3)], f"%{b + 1}", qbase, rbase)
+    tmp = q if qbase is None else [f"v{qbase + 2 * i}" for i in range(8)]
+    return ops + G.csub2p_block(r, tmp, "a", f"%{b + 1}", G.P2), r, b
 
 
-def _shoup(ops, a, w):
+def _shoup(opsr, a, w):
+    ops, r, b = opsr
     wq = w * R256 // P
     regs = {}
     for i in range(8):
-        regs[f"%{18 + i}"] = _limbs(a)[i]
-        regs[f"%{26 + i}"] = _limbs(w)[i]
-        regs[f"%{34 + i}"] = _limbs(wq)[i]
-        regs[f"%{42 + i}"] = G.NP[i]
-    return _out(_emulate([o.replace("%=", "") for o in ops], regs), 0)
+        regs[f"%{b + 2 + i}"] = _limbs(a)[i]
+        regs[f"%{b + 10 + i}"] = _limbs(w)[i]
+        regs[f"%{b + 18 + i}"] = _limbs(wq)[i]
+        regs[f"%{b + 26 + i}"] = G.NP[i]
+    R = _emulate([o.replace("%=", "") for o in ops], regs)
+    return sum(R[r[i]] << (32 * i) for i in range(8))
 
 
 def _short_quotient(a, w):
@@ -186,10 +195,11 @@ def _short_quotient(a, w):
     return (a * wq - lo) // R256 != a * wq // R256
 
 
-def test_generated_shoup_product():
+@pytest.mark.parametrize("qbase,rbase", [(None, None), (4, None), (4, 20), (4, 36)])
+def test_generated_shoup_product(qbase, rbase):
     assert sum(x << (32 * i) for i, x in enumerate(G.NP)) == R256 - P
     assert sum(x << (32 * i) for i, x in enumerate(G.P2)) == 2 * P
-    ops = _shoup_ops()
+    ops = _shoup_ops(qbase, rbase)
     rnd = random.Random(11)
     cases = [(0, 0), (R256 - 1, P - 1), (4 * P - 1, P - 1), (1, 1), (R256 - 1, 1)]
     cases += [(rnd.randrange(4 * P), rnd.randrange(P)) for _ in range(800)]

@@ -84,7 +84,7 @@ def stream(r, a, b, p, pinv, cy, pairs, carry="sgpr") -> list:
     return out
 
 
-def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
+def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag, qbase=None, rbase=None) -> list:
     """Instruction list of one Shoup product r = a*w mod p, r in [0, 2p), for a < 2^256 and a
     constant w < p with wq = floor(w 2^256 / p):
       1. q ~ floor(a wq / 2^256) from columns 6..15 of a*wq (43 word products; the dropped
@@ -93,16 +93,27 @@ def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
          exact q gives r in [0, 2p) (Shoup), a short one r in [p, 3p);
       3. q can only be short when the column-7 word of step 1 is >= 2^32 - 8 (probability 2^-29):
          `flag` (an SGPR pair) marks such lanes and the wave subtracts 2p where r >= 2p only then.
-    115 v_mad_u64_u32 + 99 v_addc_co_u32 against the Montgomery product's 128 + 128 + 8 v_mul_lo."""
-    out = []
-    st = {"first": True, "col_first": True, "k": 0, "count": True}
+    115 v_mad_u64_u32 + 99 v_addc_co_u32 against the Montgomery product's 128 + 128 + 8 v_mul_lo.
 
-    def pair(k):
+    Column k accumulates in the 64-bit pair colpair(k) and counts its carry-outs in the high word of
+    colpair(k + 1); the next column starts from (high word, carry count), one v_mov_b32 per column
+    (64-bit operands are even-aligned, so a column's high word never starts the next aligned pair).
+    qbase: q's columns 8..15 accumulate in their own pairs v[qbase + 2i : +1], so q_i is the low
+    word where it was summed (no copy); otherwise two pairs alternate and q is copied out.
+    rbase: likewise r_c is the low word of v[rbase + 2c : +1] (the caller pins r there)."""
+    out = []
+    st = {"first": True, "col_first": True, "k": 0, "count": True, "step": 1}
+
+    def colpair(k):
+        if st["step"] == 1 and qbase is not None and k >= 8:
+            return (qbase + 2 * (k - 8), qbase + 2 * (k - 8) + 1)
+        if st["step"] == 2 and rbase is not None:
+            return (rbase + 2 * k, rbase + 2 * k + 1)
         return pairs[k & 1]
 
     def mac(x, y):
-        lo, hi = pair(st["k"])
-        c = pair(st["k"] + 1)[1]
+        lo, hi = colpair(st["k"])
+        c = colpair(st["k"] + 1)[1]
         acc = f"v[{lo}:{hi}]"
         src2 = "0" if st["first"] else acc
         out.append(f"v_mad_u64_u32 {acc}, {cy}, {x}, {y}, {src2}")
@@ -115,10 +126,12 @@ def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
         st["first"] = False
 
     def shift():
-        lo, hi = pair(st["k"])
-        out.append(f"v_mov_b32 v{pair(st['k'] + 1)[0]}, v{hi}")
+        lo, hi = colpair(st["k"])
+        out.append(f"v_mov_b32 v{colpair(st['k'] + 1)[0]}, v{hi}")
         st["k"] += 1
 
+    if qbase is not None:
+        q = [f"v{qbase + 2 * i}" for i in range(8)]
     # 1. q from columns 6..15 of a * wq
     st["k"] = 6
     for c in range(6, 15):
@@ -126,13 +139,15 @@ def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
         for i in range(max(0, c - 7), min(7, c) + 1):
             mac(a[i], wq[c - i])
         if c == 7:
-            out.append(f"v_cmp_lt_u32 {flag}, -9, v{pair(7)[0]}")    # column-7 word >= 2^32 - 8
-        if c >= 8:
-            out.append(f"v_mov_b32 {q[c - 8]}, v{pair(c)[0]}")
-        if c < 14:
-            shift()
-    out.append(f"v_mov_b32 {q[7]}, v{pair(14)[1]}")   # column 15: q < 2^256, no carry beyond
+            out.append(f"v_cmp_lt_u32 {flag}, -9, v{colpair(7)[0]}")    # column-7 word >= 2^32 - 8
+        if c >= 8 and qbase is None:
+            out.append(f"v_mov_b32 {q[c - 8]}, v{colpair(c)[0]}")
+        if c < 14 or qbase is not None:
+            shift()                     # with qbase, column 15's pair receives q_7 = column 14's high word
+    if qbase is None:
+        out.append(f"v_mov_b32 {q[7]}, v{colpair(14)[1]}")   # column 15: q < 2^256, no carry beyond
     # 2. r = low 256 bits of a*w + q*(2^256 - p)
+    st["step"] = 2
     st["k"] = 0
     st["first"] = True
     for c in range(8):
@@ -141,7 +156,8 @@ def shoup_stream(r, q, a, w, wq, np, cy, pairs, flag) -> list:
         for i in range(c + 1):
             mac(a[i], w[c - i])
             mac(q[i], np[c - i])
-        out.append(f"v_mov_b32 {r[c]}, v{pair(c)[0]}")
+        if rbase is None:
+            out.append(f"v_mov_b32 {r[c]}, v{colpair(c)[0]}")
         if c < 7:
             shift()
     return out
@@ -242,34 +258,51 @@ NP = [0x0fffffff, 0xbc1e0a6c, 0x86468f6e, 0xd7cc17b7, 0x7e7ea7a2, 0x47afba49, 0x
 P2 = [0xe0000002, 0x87c3eb27, 0xf372e122, 0x5067d090, 0x0302b0ba, 0x70a08b6d, 0xc2634053, 0x60c89ce5]  # 2p
 
 
-def emit_shoup(name: str) -> str:
-    r = [f"%{i}" for i in range(8)]
-    q = [f"%{8 + i}" for i in range(8)]
-    cy, flag = "%16", "%17"
-    a = [f"%{18 + i}" for i in range(8)]
-    w = [f"%{26 + i}" for i in range(8)]
-    wq = [f"%{34 + i}" for i in range(8)]
-    np_ = [f"%{42 + i}" for i in range(8)]
-    body_l = shoup_stream(r, q, a, w, wq, np_, cy, [(0, 1), (2, 3)], flag)
-    body_l += csub2p_block(r, q, "a", flag, P2)    # q is dead by then: reuse it as the temporary
+def emit_shoup(name: str, qbase=None, rbase=None) -> str:
+    """fe_mul_shoup (see shoup_stream).  qbase: q summed in place in clobbered pairs v[qbase..+15];
+    rbase: r pinned to the even registers v[rbase + 2c] (the odd ones clobbered), so the result is
+    read where it was summed -- two call sites whose results are live together use two rbases."""
+    r = [f"%{i}" for i in range(8)] if rbase is None else [f"v{rbase + 2 * i}" for i in range(8)]
+    nq = 0 if qbase is not None else 8
+    q = [f"%{8 + i}" for i in range(nq)]
+    base = 8 + nq                      # r's 8 outputs are operands %0..%7 pinned or not
+    cy, flag = f"%{base}", f"%{base + 1}"
+    a = [f"%{base + 2 + i}" for i in range(8)]
+    w = [f"%{base + 10 + i}" for i in range(8)]
+    wq = [f"%{base + 18 + i}" for i in range(8)]
+    np_ = [f"%{base + 26 + i}" for i in range(8)]
+    body_l = shoup_stream(r, q, a, w, wq, np_, cy, [(0, 1), (2, 3)], flag, qbase, rbase)
+    tmp = q if qbase is None else [f"v{qbase + 2 * i}" for i in range(8)]
+    body_l += csub2p_block(r, tmp, "a", flag, P2)    # q is dead by then: reuse it as the temporary
     body = "\\n\\t".join(body_l)
-    outs = ", ".join([f'"=&v"(r.w[{i}])' for i in range(8)] + [f'"=&v"(q{i})' for i in range(8)])
+    outs = []
+    if rbase is None:
+        outs += [f'"=&v"(r.w[{i}])' for i in range(8)]
+    else:
+        outs += [f'"=&{{v{rbase + 2 * i}}}"(r.w[{i}])' for i in range(8)]
+    outs += [f'"=&v"(q{i})' for i in range(nq)]
+    clob = [f'"v{x}"' for x in range(4)]
+    if qbase is not None:
+        clob += [f'"v{x}"' for x in range(qbase, qbase + 16)]
+    if rbase is not None:
+        clob += [f'"v{rbase + 2 * i + 1}"' for i in range(8)]
+    clob += ['"vcc"', '"scc"']
     ins = ", ".join([f'"v"(a.w[{i}])' for i in range(8)] + [f'"v"(w.w[{i}])' for i in range(8)] +
                     [f'"v"(wq.w[{i}])' for i in range(8)])
     ins_np = ", ".join(f'"s"(N{i})' for i in range(8))
     decl_n = ", ".join(f"N{i} = {NP[i]:#010x}u" for i in range(8))
+    decl_q = f"  uint32_t {', '.join(f'q{i}' for i in range(nq))};\n" if nq else ""
     return f'''// Shoup product by a constant: r = a*w mod p in [0, 2p) for any a < 2^256, w < p canonical and
 // wq = floor(w 2^256 / p) (tools/gen_fe_mul_asm.py shoup_stream: 115 v_mad_u64_u32).
 __device__ __forceinline__ fe {name}(const fe& a, const fe& w, const fe& wq) {{
   fe r;
-  uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
-  uint64_t cy, flag;
+{decl_q}  uint64_t cy, flag;
   const uint32_t {decl_n};
   asm("{body}"
-      : {outs}, "=&s"(cy), "=&s"(flag)
+      : {", ".join(outs)}, "=&s"(cy), "=&s"(flag)
       : {ins},
         {ins_np}
-      : "v0", "v1", "v2", "v3", "vcc", "scc");
+      : {", ".join(clob)});
   (void)cy;
   (void)flag;
   return r;
@@ -283,4 +316,7 @@ if __name__ == "__main__":
     print(emit_dual("fe_mul_lazy2"))
     print("// The VCC-carry (VOP2 addc) form of fe_mul_lazy: A/B reference only (tools/microbench/mul_forms.hip).")
     print(emit_single("fe_mul_lazy_vcc", "vcc"))
+    # q summed in place (qbase=4) or r pinned (rbase) remove 8-16 v_mov_b32 per product but the
+    # 20-36 clobbered VGPRs make the pass kernel spill: 1.878 / 1.903 ms vs 1.831 ms per 2^24
+    # transform (r02 A/B), so the product keeps its copies.
     print(emit_shoup("fe_mul_shoup"))
