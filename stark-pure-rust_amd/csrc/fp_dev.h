@@ -205,41 +205,40 @@ __device__ __forceinline__ void fe_csub2p(fe& t) {
 __device__ __forceinline__ void fe_bfly_lazy(fe& x, fe& y, const fe& t) {
   fe_csub2p(x);
   const P2Limbs q = p2_vgprs();
-  fe s = x;
-  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
-      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
-      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
-      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
-      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
-      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
-      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
-      "v_addc_co_u32 %7, vcc, %7, %15, vcc"
-      : "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]), "+v"(s.w[3]), "+v"(s.w[4]), "+v"(s.w[5]), "+v"(s.w[6]),
-        "+v"(s.w[7])
-      : "v"(t.w[0]), "v"(t.w[1]), "v"(t.w[2]), "v"(t.w[3]), "v"(t.w[4]), "v"(t.w[5]), "v"(t.w[6]), "v"(t.w[7])
-      : "vcc");
-  // y = (X' + 2p) - T: X' + 2p < 4p < 2^256, and >= T, so neither chain carries out.
-  fe d = x;
-  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
-      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
-      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
-      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
-      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
-      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
-      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
-      "v_addc_co_u32 %7, vcc, %7, %15, vcc\n\t"
-      "v_sub_co_u32 %0, vcc, %0, %16\n\t"
-      "v_subb_co_u32 %1, vcc, %1, %17, vcc\n\t"
-      "v_subb_co_u32 %2, vcc, %2, %18, vcc\n\t"
-      "v_subb_co_u32 %3, vcc, %3, %19, vcc\n\t"
-      "v_subb_co_u32 %4, vcc, %4, %20, vcc\n\t"
-      "v_subb_co_u32 %5, vcc, %5, %21, vcc\n\t"
-      "v_subb_co_u32 %6, vcc, %6, %22, vcc\n\t"
-      "v_subb_co_u32 %7, vcc, %7, %23, vcc"
-      : "+v"(d.w[0]), "+v"(d.w[1]), "+v"(d.w[2]), "+v"(d.w[3]), "+v"(d.w[4]), "+v"(d.w[5]), "+v"(d.w[6]),
-        "+v"(d.w[7])
-      : "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7]),
-        "v"(t.w[0]), "v"(t.w[1]), "v"(t.w[2]), "v"(t.w[3]), "v"(t.w[4]), "v"(t.w[5]), "v"(t.w[6]), "v"(t.w[7])
+  // s = X' + T and d = (X' + 2p) - T written to fresh registers (an in-place form would copy X'
+  // into both first: 16 v_mov_b32 per butterfly).  X' + 2p < 4p < 2^256 and >= T, so neither
+  // chain carries out.
+  fe s, d;
+  asm("v_add_co_u32 %0, vcc, %16, %24\n\t"
+      "v_addc_co_u32 %1, vcc, %17, %25, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %18, %26, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %19, %27, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, %20, %28, vcc\n\t"
+      "v_addc_co_u32 %5, vcc, %21, %29, vcc\n\t"
+      "v_addc_co_u32 %6, vcc, %22, %30, vcc\n\t"
+      "v_addc_co_u32 %7, vcc, %23, %31, vcc\n\t"
+      "v_add_co_u32 %8, vcc, %16, %32\n\t"
+      "v_addc_co_u32 %9, vcc, %17, %33, vcc\n\t"
+      "v_addc_co_u32 %10, vcc, %18, %34, vcc\n\t"
+      "v_addc_co_u32 %11, vcc, %19, %35, vcc\n\t"
+      "v_addc_co_u32 %12, vcc, %20, %36, vcc\n\t"
+      "v_addc_co_u32 %13, vcc, %21, %37, vcc\n\t"
+      "v_addc_co_u32 %14, vcc, %22, %38, vcc\n\t"
+      "v_addc_co_u32 %15, vcc, %23, %39, vcc\n\t"
+      "v_sub_co_u32 %8, vcc, %8, %24\n\t"
+      "v_subb_co_u32 %9, vcc, %9, %25, vcc\n\t"
+      "v_subb_co_u32 %10, vcc, %10, %26, vcc\n\t"
+      "v_subb_co_u32 %11, vcc, %11, %27, vcc\n\t"
+      "v_subb_co_u32 %12, vcc, %12, %28, vcc\n\t"
+      "v_subb_co_u32 %13, vcc, %13, %29, vcc\n\t"
+      "v_subb_co_u32 %14, vcc, %14, %30, vcc\n\t"
+      "v_subb_co_u32 %15, vcc, %15, %31, vcc"
+      : "=&v"(s.w[0]), "=&v"(s.w[1]), "=&v"(s.w[2]), "=&v"(s.w[3]), "=&v"(s.w[4]), "=&v"(s.w[5]), "=&v"(s.w[6]),
+        "=&v"(s.w[7]), "=&v"(d.w[0]), "=&v"(d.w[1]), "=&v"(d.w[2]), "=&v"(d.w[3]), "=&v"(d.w[4]), "=&v"(d.w[5]),
+        "=&v"(d.w[6]), "=&v"(d.w[7])
+      : "v"(x.w[0]), "v"(x.w[1]), "v"(x.w[2]), "v"(x.w[3]), "v"(x.w[4]), "v"(x.w[5]), "v"(x.w[6]), "v"(x.w[7]),
+        "v"(t.w[0]), "v"(t.w[1]), "v"(t.w[2]), "v"(t.w[3]), "v"(t.w[4]), "v"(t.w[5]), "v"(t.w[6]), "v"(t.w[7]),
+        "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7])
       : "vcc");
   x = s;
   y = d;
