@@ -204,6 +204,32 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
       __syncthreads();
       s = 1;
     }
+    if (s == 0) {
+      // Radix-4 step s = 0 (peeled: its twiddles are 1 except w_4^1, and the loop below stays
+      // branch-free, so no register shuffles at merge points).
+      if (active) {
+        const uint32_t base = q << 2;
+        fe x0 = X[(base << log_b) + b];
+        fe x1 = X[((base + 1) << log_b) + b];
+        fe x2 = X[((base + 2) << log_b) + b];
+        fe x3 = X[((base + 3) << log_b) + b];
+        fe_csub2p(x1);
+        fe_csub2p(x3);
+        fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
+        fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
+        const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
+        const fe t3 = shoup_b(x3, sm[ic], sm[ic + 1]);
+        fe_csub2p(x2);
+        fe_bfly_lazy(x0, x2, x2);
+        fe_bfly_lazy(x1, x3, t3);
+        X[(base << log_b) + b] = x0;
+        X[((base + 2) << log_b) + b] = x2;
+        X[((base + 1) << log_b) + b] = x1;
+        X[((base + 3) << log_b) + b] = x3;
+      }
+      __syncthreads();
+      s = 2;
+    }
 #pragma unroll 1
     for (; s < LOG_R; s += 2) {
       if (active) {
@@ -215,28 +241,15 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         fe x2 = X[((base + 2 * m) << log_b) + b];
         fe x3 = X[((base + 3 * m) << log_b) + b];
         fe t1, t3;
-        if (s != 0) {
-          const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
-          const fe ta = sm[ia], taq = sm[ia + 1];
-          shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
-        } else {
-          t1 = x1;
-          t3 = x3;
-          fe_csub2p(t1);
-          fe_csub2p(t3);
-        }
+        const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
+        const fe ta = sm[ia], taq = sm[ia + 1];
+        shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
         fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
         fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
         const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
         const fe tc = sm[ic], tcq = sm[ic + 1];
-        fe t2;
-        if (s != 0) {
-          const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
-          t2 = shoup_a(x2, sm[ib], sm[ib + 1]);
-        } else {
-          t2 = x2;
-          fe_csub2p(t2);
-        }
+        const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
+        const fe t2 = shoup_a(x2, sm[ib], sm[ib + 1]);
         t3 = shoup_b(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);

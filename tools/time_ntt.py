@@ -1,6 +1,7 @@
 """Times stark_ntt_dev (2^log_n forward, HBM-resident) for one or more builds
 of libstark_hip.so given on the command line (A/B in one process)."""
 import ctypes
+import hashlib
 import os
 import sys
 import time
@@ -53,7 +54,13 @@ def main():
         lib.stark_ctx_synchronize(ctx)
         ms = (time.perf_counter() - t0) * 1000 / reps
         results[path] = ms
-        print(f"{path}: {ms:.3f} ms  ({n / ms / 1e6:.3f} G elems/s)", flush=True)
+        # Every build ran the same 23 in-place transforms of the same input: equal digests = equal outputs.
+        lib.stark_memcpy_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        back = np.empty_like(host)
+        lib.stark_memcpy_d2h(ctx, back.ctypes.data, d, n * 32)
+        lib.stark_ctx_synchronize(ctx)
+        dig = hashlib.sha256(back.tobytes()).hexdigest()[:16]
+        print(f"{path}: {ms:.3f} ms  ({n / ms / 1e6:.3f} G elems/s)  out {dig}", flush=True)
 
 
 if __name__ == "__main__":
