@@ -35,13 +35,6 @@ struct ColTw {
 // the next tile's 4 elements per thread into registers while it computes the
 // current one, so HBM traffic overlaps the modular arithmetic.
 // T = B*R/4 threads, each owning exactly 4 elements in every phase.
-// First pass of a transform whose input is zero beyond its first n >> zero_log
-// elements (best_fft's zero padding): skip = the number of leading radix-2
-// stages that are plain copies (<= zero_log, matching the pass's stage
-// pairing); log_in = log2 of the compact input's batch stride.
-struct Sparse {
-  uint32_t skip, zero_log, log_in;
-};
 
 // Two independent lazy products: interleaved in one asm block (fe_mul_lazy2) unless
 // STARK_NTT_DUAL=0 (A/B switch, tools/build_variant.sh).
@@ -354,7 +347,7 @@ PassPlan plan_passes(uint32_t log_n) {
 // Columns per workgroup (log2): 1024 elements (256 threads x 4) when the
 // transform has that many columns, so every global access is a run of
 // B*32 >= 128 contiguous bytes for R <= 256.
-uint32_t choose_log_b(uint32_t log_n, uint32_t log_r) {
+uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r) {
   uint32_t lb = log_r >= 10 ? 0 : 10 - log_r;
   if (lb > log_n - log_r) lb = log_n - log_r;
   return lb;
@@ -484,6 +477,7 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
       a = F.mul(a, w16);
     }
   }
+  tw->n_small_pairs = h_small.size() / 2;
   const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 4 * n16) * sizeof(fe);
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return STARK_ERR_OOM;
@@ -536,7 +530,7 @@ static stark_status full_table(stark_ctx* ctx, const Twiddles& tw_c, uint32_t lo
   return STARK_OK;
 }
 
-static bool full_table_enabled() {
+bool ntt_full_table_enabled() {
   static const bool on = [] {
     const char* e = getenv("STARK_NTT_FULL_TW");
     return !(e && e[0] == '0');
@@ -554,6 +548,8 @@ extern "C" uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap
 }
 
 namespace stark {
+
+uint32_t ntt_choose_log_b(uint32_t log_n, uint32_t log_r) { return choose_log_b_impl(log_n, log_r); }
 
 uint32_t ntt_first_log_r(uint32_t log_n) { return log_n < 2 ? log_n : plan_passes(log_n).log_r[0]; }
 
@@ -588,6 +584,8 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     return STARK_OK;
   }
   const PassPlan plan = plan_passes(log_n);
+  if (ntt29_enabled()) return ntt29_device_from(ctx, src, zero_log, d_data, log_n, batch, tw, inverse, stream,
+                                                plan.log_r, plan.n_pass);
   stark_status st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
   if (st != STARK_OK) return st;
   fe* scratch = (fe*)ctx->scratch.ptr;
@@ -607,7 +605,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
       if ((k & 1) != (lr & 1)) --k;
       sp = Sparse{k, zero_log, log_n - zero_log};
     }
-    const uint32_t lb = choose_log_b(log_n, lr);
+    const uint32_t lb = ntt_choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
     const size_t lds = ((size_t)elems + (1u << lr)) * sizeof(fe);  // data image + R/2 Shoup pairs
@@ -619,7 +617,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     // when that pass has them (log_ns > 0), else it is an explicit product.
     const bool fold = inverse && last && log_ns > 0;
     const fe* full = nullptr;
-    if (last && log_ns > 0 && log_n > tw.l16 && log_n >= 17 && log_n <= 26 && full_table_enabled()) {
+    if (last && log_ns > 0 && log_n > tw.l16 && log_n >= 17 && log_n <= 26 && ntt_full_table_enabled()) {
       st = full_table(ctx, tw, lr, fold, stream, &full);
       if (st != STARK_OK) return st;
     }
