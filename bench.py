@@ -145,6 +145,56 @@ def timed_events(fn, stream, reps):
     return start.elapsed_time(end) / reps
 
 
+def _smi_power():
+    """(socket power W, power cap W, sclk MHz) from rocm-smi, or None (a child process, never exec)."""
+    import re
+    try:
+        out = subprocess.run(["rocm-smi", "--showpower", "--showmaxpower", "--showclocks", "--json"],
+                             capture_output=True, text=True, timeout=15).stdout
+        card = next(iter(json.loads(out).values()))
+        pw = float(next(v for k, v in card.items() if "Package Power" in k and "Max" not in k))
+        cap = next((float(v) for k, v in card.items() if "Max" in k and "Power" in k), None)
+        sclk = int(re.search(r"\((\d+)Mhz", card["sclk clock speed:"]).group(1))
+        return pw, cap, sclk
+    except Exception:  # noqa: BLE001  (no rocm-smi or an unexpected format: no power figure)
+        return None
+
+
+def power_under_load(step, sync, secs=2.5):
+    """Board power and shader clock while `step` runs back to back (tools/power_probe.py): the NTT
+    pass kernels run at the package power limit, which is what sets their clock."""
+    import statistics
+    import threading
+    samples, stop = [], threading.Event()
+
+    def sampler():
+        time.sleep(0.8)
+        while not stop.is_set():
+            r = _smi_power()
+            if r:
+                samples.append(r)
+            time.sleep(0.3)
+
+    th = threading.Thread(target=sampler)
+    th.start()
+    t0 = time.time()
+    while time.time() - t0 < secs:
+        for _ in range(20):
+            step()
+        sync()
+    stop.set()
+    th.join()
+    if not samples:
+        return None
+    pw = statistics.median(x[0] for x in samples)
+    cap = samples[0][1]
+    out = {"board_power_w": pw, "power_cap_w": cap, "sclk_mhz": statistics.median(x[2] for x in samples),
+           "samples": len(samples), "source": "rocm-smi --showpower --showmaxpower --showclocks"}
+    if cap:
+        out["power_frac"] = round(pw / cap, 3)
+    return out
+
+
 def end_to_end(ctx):
     """prove_with_witness wall-clock on the reference's pedersen_test fixture and on a
     synthetic 2^20-step circuit (stand-in for sha256_2_test, whose .r1cs is not shipped)."""
@@ -560,6 +610,16 @@ def main():
             extras.update(end_to_end(ctx))
         except Exception as e:  # the headline line is still printed; the failure is reported in it
             extras["end_to_end_error"] = repr(e)[:300]
+        # Board power while the NTT and the Merkle build run back to back (after every timing above, so
+        # the heat does not skew them): the NTT sits at the package power limit, which sets its clock.
+        pwr = power_under_load(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr), stream.synchronize)
+        if pwr:
+            extras["power_during_ntt"] = pwr
+        ptree = S.MerkleProofInPlace(ctx)
+        pwr = power_under_load(lambda: ptree.update_dev(dptr, n, 32, stream=sptr), stream.synchronize)
+        if pwr:
+            extras["power_during_merkle"] = pwr
+        del ptree
 
     if not args.no_extras and world > 1:
         # Distributed Merkle commitment (north star: per-GPU subtrees combined across ranks):
@@ -659,6 +719,8 @@ def main():
                      "issue_bound_ms_per_transform": round(issue_ms, 4),
                      "frac": round(issue_ms / ev_ms, 4), "sq_profile": os.path.relpath(PMC, ROOT)})
         roofline["valu_issue_frac"] = valu["frac"]
+    if "power_during_ntt" in extras:
+        roofline["power_during_ntt"] = extras["power_during_ntt"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
