@@ -1,0 +1,92 @@
+// Digit-basis constant product for BN254 Fr on gfx950 VALU.
+//
+// a * w mod p for a constant w without a quotient product: the constant is
+// stored as its eight "digit images" W_i = w * 2^(32 i) mod p, each in nine
+// 29-bit limbs, so for a = sum a_i 2^(32 i) (a < 4p)
+//   S = sum_i a_i W_i = sum_j acc_j 2^(29 j),   acc_j = sum_i a_i W_i[j]
+// is congruent to a w and every column sum acc_j fits 64 bits with no carry
+// out (8 (2^32 - 1)(2^29 - 1) < 2^64): 72 v_mad_u64_u32, no carry counting.
+// S < 8 * 2^32 * p, so q = floor(S / p) < 2^36 comes from the top two columns
+// in double precision (underestimated by a margin, so q is exact or one short)
+// and r = S - q p = (S + q (2^261 - p)) mod 2^261 lies in [0, 2p): 18 more
+// v_mad_u64_u32 and one carry pass over the nine columns.  The Shoup product
+// needs 115 word products and ~99 carry counts for the same result range.
+//
+// Table layout (per constant): 72 u32, W[9 i + j] = limb j of W_i.
+#pragma once
+#include "fp_dev.h"
+
+namespace stark {
+
+#define STARK_DB_M29 0x1fffffffu
+// N = 2^261 - p in 29-bit limbs.
+#define STARK_DB_N0 0x0fffffffu
+#define STARK_DB_N1 0x00f05360u
+#define STARK_DB_N2 0x11a3dbafu
+#define STARK_DB_N3 0x182f6f0cu
+#define STARK_DB_N4 0x0a7a2d7cu
+#define STARK_DB_N5 0x1d24bf3fu
+#define STARK_DB_N6 0x1f591ebeu
+#define STARK_DB_N7 0x11a3d9cbu
+#define STARK_DB_N8 0x1fcf9bb1u
+
+__device__ __forceinline__ uint32_t db_n(int j) {
+  switch (j) {
+    case 0: return STARK_DB_N0; case 1: return STARK_DB_N1; case 2: return STARK_DB_N2;
+    case 3: return STARK_DB_N3; case 4: return STARK_DB_N4; case 5: return STARK_DB_N5;
+    case 6: return STARK_DB_N6; case 7: return STARK_DB_N7; default: return STARK_DB_N8;
+  }
+}
+
+// 2^232 / p and 2^235 / p (nearest doubles) and the quotient margin 2^-12
+// (tests/test_fe_db.py checks every constant).
+#define STARK_DB_C8 3.153175148504101e-07
+#define STARK_DB_C7 2.5225401188032808e-06
+#define STARK_DB_MARGIN 2.44140625e-4
+
+// r = a * w mod p in [0, 2p) for a < 4p (the NTT's lazy range), W the constant's digit-basis table.
+//   acc_j = sum_i a_i W_i[j]: 72 v_mad_u64_u32 into nine 64-bit columns;
+//   q: f = acc_8 2^232 / p + hi(acc_7) 2^235 / p - 2^-12 in doubles (the dropped terms are < 2^-15,
+//      the rounding < 2^-15, so floor(f) is floor(S / p) or one less), q = qh 2^29 + ql;
+//   acc_j += ql N_j + qh N_{j-1} (17 mads; a < 4p bounds a_7 < 2^31.6, so every column stays below
+//      7 2^61 + 2^60.6 + 2^58 < 2^64 with the carry added);
+//   one carry pass to 29-bit limbs (mod 2^261) and the repack to 32-bit words.
+__device__ __forceinline__ fe fe_mul_db(const fe& a, const uint32_t* __restrict__ W) {
+  uint64_t acc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = (uint64_t)a.w[0] * W[j];
+#pragma unroll
+  for (int i = 1; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[j] += (uint64_t)a.w[i] * W[9 * i + j];
+  const double d8 = fma((double)(uint32_t)(acc[8] >> 32), 0x1p32, (double)(uint32_t)acc[8]);
+  const double d7 = (double)(uint32_t)(acc[7] >> 32);
+  const double f = fmax(fma(d8, STARK_DB_C8, fma(d7, STARK_DB_C7, -STARK_DB_MARGIN)), 0.0);
+  const uint32_t qh = (uint32_t)(f * 0x1p-29);
+  const uint32_t ql = (uint32_t)fma((double)qh, -0x1p29, f);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    acc[j] += (uint64_t)ql * db_n(j);
+    if (j) acc[j] += (uint64_t)qh * db_n(j - 1);
+  }
+  uint32_t r[9];
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const uint64_t t = acc[j] + c;
+    r[j] = (uint32_t)t & STARK_DB_M29;
+    c = t >> 29;
+  }
+  fe o;
+  o.w[0] = r[0] | (r[1] << 29);
+  o.w[1] = (r[1] >> 3) | (r[2] << 26);
+  o.w[2] = (r[2] >> 6) | (r[3] << 23);
+  o.w[3] = (r[3] >> 9) | (r[4] << 20);
+  o.w[4] = (r[4] >> 12) | (r[5] << 17);
+  o.w[5] = (r[5] >> 15) | (r[6] << 14);
+  o.w[6] = (r[6] >> 18) | (r[7] << 11);
+  o.w[7] = (r[7] >> 21) | (r[8] << 8);
+  return o;
+}
+
+}  // namespace stark

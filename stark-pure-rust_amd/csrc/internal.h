@@ -78,6 +78,10 @@ struct Twiddles {
   fe* d_full = nullptr;
   fe* d_full_s = nullptr;
   size_t n_small_pairs = 0;      // Shoup pairs in d_small
+  // Digit-basis tables (fe_db.h) of w_R^(4k), k < R/8, for every radix R = 2^l >= 16: the constants of
+  // the radix-4 steps before a pass's last one.  db_off[l] = offset in u32 into d_db (72 u32 per root).
+  uint32_t* d_db = nullptr;
+  uint32_t db_off[16] = {0};
   Tw29* t29 = nullptr;    // radix-2^29 images of these tables (ntt29.hip), built on first use
   HostFp root;      // the root these tables were built for (Montgomery)
   HostFp inv_n;     // n^-1 (Montgomery)
@@ -315,6 +319,24 @@ inline void shoup_pair(const HostFp& x, fe out[2]) {
   }
   memcpy(out[0].w, c, 32);
   memcpy(out[1].w, q, 32);
+}
+
+// Digit-basis table of a constant w (fe_db.h): out[9 i + j] = 29-bit limb j of w 2^(32 i) mod p.
+inline void db_table(const HostFp& x, uint32_t out[72]) {
+  const FieldHost& F = FieldHost::get();
+  const HostFp two32 = F.from_u64((uint64_t)1 << 32);
+  HostFp cur = x;
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c[4];
+    F.to_canonical(cur, c);
+    for (int j = 0; j < 9; ++j) {
+      const int bit = 29 * j, word = bit >> 6, sh = bit & 63;
+      uint64_t v = c[word] >> sh;
+      if (sh > 35 && word < 3) v |= c[word + 1] << (64 - sh);
+      out[9 * i + j] = (uint32_t)v & 0x1fffffffu;
+    }
+    cur = F.mul(cur, two32);
+  }
 }
 
 }  // namespace stark

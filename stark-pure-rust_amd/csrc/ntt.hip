@@ -16,6 +16,7 @@
 // the last pass's store.
 #include <stdlib.h>
 
+#include "fe_db.h"
 #include "internal.h"
 
 namespace stark {
@@ -59,20 +60,58 @@ __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, con
 #endif
 }
 
+// The digit-basis table of constant k in LDS: 72 u32 per constant, 16-B aligned.  Constants 8 apart
+// would share banks (72 * 8 = 0 mod 64 banks) and a radix-4 step reads k, k + 8, k + 16, k + 24 in
+// one ds_read_b128 lane group, so each group of 8 constants starts 4 banks after the previous one.
+__device__ __forceinline__ const uint32_t* dbt(const uint32_t* sdb, uint32_t k) {
+  return static_cast<const uint32_t*>(__builtin_assume_aligned(sdb + 72 * k + 4 * (k >> 3), 16));
+}
+
 // COL: the pass's column-twiddle source, fixed per launch so each instance carries one product
 // form (kColNone: first pass; kColFull: last-pass full table, Montgomery; kColT16: Shoup pairs;
 // kColTwoLevel: lo * hi, Montgomery).
 enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 
+// Radix-4 steps before a pass's last one multiply by the digit-basis product (fe_db.h): their
+// constants are w_R^(4k), k < R/8 (32 for R = 256, 9 KB of LDS), and the last step, whose R/2
+// constants would need 36 KB, keeps the Shoup pairs.  STARK_NTT_DB=0 builds the Shoup-only pass.
+#ifndef STARK_NTT_DB
+#define STARK_NTT_DB 1
+#endif
+// STARK_NTT_DB_GLOBAL=1: the tables are read through the vector L1 (9 KB, cache-resident) instead of
+// being copied to LDS, which keeps the pass at 40 KB of LDS (four workgroups per CU).
+#ifndef STARK_NTT_DB_GLOBAL
+#define STARK_NTT_DB_GLOBAL 0
+#endif
+// The first pass (no column twiddle) keeps the Shoup-only form at four workgroups per CU unless
+// STARK_NTT_DB_FIRST=1: with 49 KB of LDS (three per CU) it measured slower there.
+#ifndef STARK_NTT_DB_FIRST
+#define STARK_NTT_DB_FIRST 0
+#endif
+template <int LOG_R, int COL>
+struct DbPlan {
+  static constexpr bool on = STARK_NTT_DB && LOG_R >= 4 && (COL != 0 || STARK_NTT_DB_FIRST);
+  static constexpr uint32_t entries = on ? (1u << LOG_R) / 8 : 0;
+  // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
+  static constexpr uint32_t lds_fe = STARK_NTT_DB_GLOBAL || !on ? 0 : entries * 9 + entries / 16;
+};
+
 template <int LOG_R, bool PERSIST, int COL>
-__global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
+__global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
-                                                          const fe* __restrict__ small, fe scale, int do_scale,
+                                                          const fe* __restrict__ small, const uint32_t* __restrict__ db,
+                                                          fe scale, int do_scale,
                                                           uint32_t log_tiles, uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
+  using DB = DbPlan<LOG_R, COL>;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
   fe* sm = lds;          // R/2 small roots w_R^k as Shoup pairs: sm[2k] = w_R^k, sm[2k + 1] = its quotient
-  fe* X = lds + R;       // [R][B] data image
+#if STARK_NTT_DB_GLOBAL
+  const uint32_t* sdb = db;  // digit-basis tables of w_R^(4k), k < R/8 (L1-resident)
+#else
+  uint32_t* sdb = reinterpret_cast<uint32_t*>(lds + R);  // digit-basis tables of w_R^(4k), k < R/8
+#endif
+  fe* X = lds + R + DB::lds_fe;  // [R][B] data image
   const uint32_t B = 1u << log_b;
   const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
   const uint32_t tid = threadIdx.x;
@@ -82,6 +121,9 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
   const uint32_t tile_mask = (1u << log_tiles) - 1;
 
   for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
+  if (DB::on && !STARK_NTT_DB_GLOBAL)
+    for (uint32_t k = tid; k < DB::entries * 18; k += blockDim.x)
+      reinterpret_cast<uint4*>(lds + R)[k + ((k / 18) >> 3)] = reinterpret_cast<const uint4*>(db)[k];
 
   // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row).
   uint32_t eb[4], er[4];
@@ -210,8 +252,13 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
         fe_csub2p(x3);
         fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
         fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
-        const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
-        const fe t3 = shoup_b(x3, sm[ic], sm[ic + 1]);
+        fe t3;
+        if (DB::on) {
+          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) >> 2));  // w_4^1 = w_R^(R/4)
+        } else {
+          const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
+          t3 = shoup_b(x3, sm[ic], sm[ic + 1]);
+        }
         fe_csub2p(x2);
         fe_bfly_lazy(x0, x2, x2);
         fe_bfly_lazy(x1, x3, t3);
@@ -222,6 +269,35 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : 4) void ntt_pass_kernel(const fe
       }
       __syncthreads();
       s = 2;
+    }
+    if (DB::on) {
+#pragma unroll 1
+      for (; s < (int)LOG_R - 2; s += 2) {
+        if (active) {
+          const uint32_t m = 1u << s;
+          const uint32_t jj = q & (m - 1);
+          const uint32_t base = ((q >> s) << (s + 2)) + jj;
+          fe x0 = X[(base << log_b) + b];
+          fe x1 = X[((base + m) << log_b) + b];
+          fe x2 = X[((base + 2 * m) << log_b) + b];
+          fe x3 = X[((base + 3 * m) << log_b) + b];
+          // exponents (in w_R units) jj R/2m, jj R/4m, (jj + m) R/4m: multiples of 4 before the last step
+          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) >> 2);  // w_{2m}^jj
+          const fe t1 = fe_mul_db(x1, wa);
+          fe t3 = fe_mul_db(x3, wa);
+          fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
+          fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
+          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) >> 2));  // w_{4m}^jj
+          t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) >> 2));   // w_{4m}^(jj+m)
+          fe_bfly_lazy(x0, x2, t2);
+          fe_bfly_lazy(x1, x3, t3);
+          X[(base << log_b) + b] = x0;
+          X[((base + 2 * m) << log_b) + b] = x2;
+          X[((base + m) << log_b) + b] = x1;
+          X[((base + 3 * m) << log_b) + b] = x3;
+        }
+        __syncthreads();
+      }
     }
 #pragma unroll 1
     for (; s < LOG_R; s += 2) {
@@ -353,8 +429,29 @@ uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r) {
   return lb;
 }
 
-typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, fe, int, uint32_t,
-                        uint32_t, Sparse);
+typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, const uint32_t*, fe, int,
+                        uint32_t, uint32_t, Sparse);
+
+template <int COL>
+size_t db_lds_fe_c(uint32_t log_r) {
+  switch (log_r) {
+    case 4: return DbPlan<4, COL>::lds_fe;
+    case 5: return DbPlan<5, COL>::lds_fe;
+    case 6: return DbPlan<6, COL>::lds_fe;
+    case 7: return DbPlan<7, COL>::lds_fe;
+    case 8: return DbPlan<8, COL>::lds_fe;
+    case 9: return DbPlan<9, COL>::lds_fe;
+    default: return 0;
+  }
+}
+size_t db_lds_fe(uint32_t log_r, int col) {
+  switch (col) {
+    case kColNone: return db_lds_fe_c<kColNone>(log_r);
+    case kColFull: return db_lds_fe_c<kColFull>(log_r);
+    case kColT16: return db_lds_fe_c<kColT16>(log_r);
+    default: return db_lds_fe_c<kColTwoLevel>(log_r);
+  }
+}
 
 template <int LOG_R>
 pass_fn pass_kernel_r(bool persist, int col) {
@@ -478,7 +575,22 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     }
   }
   tw->n_small_pairs = h_small.size() / 2;
-  const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 4 * n16) * sizeof(fe);
+  // Digit-basis tables: w_R^(4k), k < R/8, for R = 2^l, 4 <= l <= min(log_n, 9).
+  std::vector<uint32_t> h_db;
+  for (uint32_t l = 4; l <= kMaxLogR && l <= log_n; ++l) {
+    tw->db_off[l] = (uint32_t)h_db.size();
+    const HostFp w4 = F.pow_u64(w, (uint64_t)4 << (log_n - l));
+    HostFp a = F.one();
+    for (uint32_t k = 0; k < (1u << (l - 3)); ++k) {
+      uint32_t t[72];
+      db_table(a, t);
+      h_db.insert(h_db.end(), t, t + 72);
+      a = F.mul(a, w4);
+    }
+  }
+  if (h_db.empty()) h_db.resize(72, 0);
+  const size_t db_fe = h_db.size() / 8;  // 72 u32 = 9 fe per constant
+  const size_t bytes = (n_lo + 2 * n_hi + h_small.size() + 4 * n16 + db_fe) * sizeof(fe);
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return STARK_ERR_OOM;
   tw->d_lo = (fe*)d;
@@ -487,12 +599,14 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
   tw->d_t16 = tw->d_small + h_small.size();
   tw->d_hi_s = tw->d_t16 + 2 * n16;
   tw->d_t16_s = tw->d_hi_s + n_hi;
+  tw->d_db = reinterpret_cast<uint32_t*>(tw->d_t16_s + 2 * n16);
   STARK_HIP(ctx, hipMemcpy(tw->d_lo, h_lo.data(), n_lo * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi, h_hi.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_small, h_small.data(), h_small.size() * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_t16, h_t16.data(), 2 * n16 * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi_s, h_hi_s.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_t16_s, h_t16_s.data(), 2 * n16 * sizeof(fe), hipMemcpyHostToDevice));
+  STARK_HIP(ctx, hipMemcpy(tw->d_db, h_db.data(), h_db.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   *out = tw.get();
   ctx->tw.emplace(key, std::move(tw));
   return STARK_OK;
@@ -608,7 +722,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     const uint32_t lb = ntt_choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
-    const size_t lds = ((size_t)elems + (1u << lr)) * sizeof(fe);  // data image + R/2 Shoup pairs
+    // (data image + R/2 Shoup pairs + the digit-basis tables: sized below, once the pass's column source is known)
     const uint32_t log_tiles = log_n - lr - lb;
     const uint64_t total = (uint64_t)batch << log_tiles;
     const bool persist = kPersistent && total > kPersistentGrid;
@@ -623,8 +737,10 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     }
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
     const int col = log_ns == 0 ? kColNone : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
+    const size_t lds = ((size_t)elems + (1u << lr) + db_lds_fe(lr, col)) * sizeof(fe);
     hipLaunchKernelGGL(pass_kernel(lr, persist, col), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
-                       tw.d_small + tw.small_off[lr], scale, (inverse && last && !fold) ? 1 : 0, log_tiles,
+                       tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
+                       (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total, sp);
     STARK_HIP(ctx, hipGetLastError());
     cur = dst;

@@ -1,6 +1,6 @@
 """Workload for rocprofv3 counter passes (tools/pmc_round.sh): the bench's dominant kernels on
 device-resident synthetic data, a few dispatches each, nothing else.
-    WHAT=ntt|merkle|all (default all); REPS=5
+    WHAT=ntt|merkle|all (default all); REPS=5; STARK_LIB=<path> times another build of the library
 """
 import ctypes
 import os
@@ -20,6 +20,8 @@ def main():
     reps = int(os.environ.get("REPS", "5"))
     log_n = 24
     n = 1 << log_n
+    if os.environ.get("STARK_LIB"):
+        S.load_library(os.path.abspath(os.environ["STARK_LIB"]))
     ctx = S.Context(0)
     host = O.random_elements(n, 0x5EED0000 + log_n)
     d = ctx.alloc(n * 32)
