@@ -39,9 +39,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARC
 # wave64 instruction at the in-kernel clock (tools/microbench/mix_rates.hip, profiles/r02_mix_rates.txt).
 ISSUE_CYCLES = 4.0
 SIMDS = 1024
-# The Shoup constant product alone (tools/microbench/shoup_check.hip, 4 waves/SIMD like the pass
-# kernel): 148.7 G products/s (profiles/r02_shoup_product.txt).
-SHOUP_PRODUCT_PEAK = 148.69e9
+# The constant products alone with their constants in LDS, 4 waves/SIMD, same run
+# (tools/microbench/db_rate.hip, profiles/r02_db_product.txt): Shoup 138.7 G/s, digit basis 200.0 G/s.
+SHOUP_PRODUCT_PEAK = 138.71e9
+DB_PRODUCT_PEAK = 199.98e9
 LOG_N = 24
 PROFILE = os.path.join(ROOT, "profiles", "r02_summary.json")
 PMC = os.path.join(ROOT, "profiles", "r02_pmc.json")
@@ -364,27 +365,32 @@ def merkle_valu_roofline(n: int, ms: float) -> dict:
     return out
 
 
-def ntt_products(log_n: int, plan: list) -> int:
+def ntt_products(log_n: int, plan: list) -> tuple:
     """Modular products of one forward 2^log_n transform, counted from csrc/ntt.hip's pass kernel:
     each radix-4 step multiplies 4 of every 4 elements (w_{2m}^jj twice, w_{4m}^jj, w_{4m}^(jj+m)),
     the s = 0 step of an even radix only by w_{4m}^(jj+m) (n/4), an odd radix runs a product-free
     radix-2 stage 0 first; every pass after the first multiplies each element by its column twiddle,
     one product from a table (t16 when Ns R <= 2^l16, or the last pass's full table for 2^17..2^26)
-    or two in the lo * hi form."""
+    or two in the lo * hi form.  Returns (all products, digit-basis products): the radix-4 steps
+    before the last one of every pass after the first use the digit-basis product (ntt.hip DbPlan,
+    radices >= 2^4)."""
     n = 1 << log_n
     l16 = 18 if log_n >= 25 else min(log_n, 16)
-    total, ns = 0, 0
+    total, db, ns = 0, 0, 0
     for i, r in enumerate(plan):
         if r % 2:
-            total += n * ((r - 1) // 2)
+            steps = n * ((r - 1) // 2)
         else:
-            total += n * (r // 2 - 1) + n // 4
+            steps = n * (r // 2 - 1) + n // 4
+        total += steps
         if ns:
+            if r >= 4:
+                db += steps - n  # all but the last radix-4 step
             last = i == len(plan) - 1
             table = ns + r <= l16 or (last and log_n > l16 and 17 <= log_n <= 26)
             total += n * (1 if table else 2)
         ns += r
-    return total
+    return total, db
 
 
 def main():
@@ -701,11 +707,16 @@ def main():
                 "rocprof_ms_per_transform_avg": round(prof_avg, 4) if prof_avg else None,
                 "rocprof_ms_per_transform_steady_median": round(prof_med, 4) if prof_med else None,
                 "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
-    modmuls = ntt_products(log_n, plan)
+    modmuls, db_muls = ntt_products(log_n, plan)
+    # The transform's products at the standalone rates of their two forms (the rest of the pass, the
+    # butterflies, LDS traffic and the Montgomery full-table column twiddle, priced at nothing).
+    peak = modmuls / (db_muls / DB_PRODUCT_PEAK + (modmuls - db_muls) / SHOUP_PRODUCT_PEAK)
     valu = {"bound": f"VALU issue ({ISSUE_CYCLES} cycles per wave64 instruction, measured)",
-            "modmuls_per_transform": modmuls, "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0),
-            "shoup_product_peak_per_s": SHOUP_PRODUCT_PEAK}
-    valu["product_frac"] = round(valu["achieved_modmul_per_s"] / SHOUP_PRODUCT_PEAK, 4)
+            "modmuls_per_transform": modmuls, "digit_basis_modmuls_per_transform": db_muls,
+            "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0),
+            "product_peak_per_s": round(peak), "shoup_product_peak_per_s": SHOUP_PRODUCT_PEAK,
+            "digit_basis_product_peak_per_s": DB_PRODUCT_PEAK}
+    valu["product_frac"] = round(valu["achieved_modmul_per_s"] / peak, 4)
     if sq:
         # Issue-bound time of the transform: each pass's SQ_INSTS_VALU x ISSUE_CYCLES over the chip's
         # 1024 SIMDs at that pass's measured clock (GRBM_GUI_ACTIVE / 8 XCDs / duration); frac =

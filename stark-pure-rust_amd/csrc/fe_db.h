@@ -69,23 +69,38 @@ __device__ __forceinline__ fe fe_mul_db(const fe& a, const uint32_t* __restrict_
     acc[j] += (uint64_t)ql * db_n(j);
     if (j) acc[j] += (uint64_t)qh * db_n(j - 1);
   }
-  uint32_t r[9];
+  // Carry pass: t_j = acc_j + (t_{j-1} >> 29); limb j is t_j mod 2^29 (the result mod 2^261).  Each output
+  // word is one bit-field extract of a limb and one shift-or of the next limb's low word, whose bits
+  // above the word are shifted out, so the limbs are never masked separately.
+  uint32_t lo[9];
   uint64_t c = 0;
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
     const uint64_t t = acc[j] + c;
-    r[j] = (uint32_t)t & STARK_DB_M29;
+    lo[j] = (uint32_t)t;
     c = t >> 29;
   }
+  // (asm: the compiler turns a constant bit-field extract back into a shift and a mask)
   fe o;
-  o.w[0] = r[0] | (r[1] << 29);
-  o.w[1] = (r[1] >> 3) | (r[2] << 26);
-  o.w[2] = (r[2] >> 6) | (r[3] << 23);
-  o.w[3] = (r[3] >> 9) | (r[4] << 20);
-  o.w[4] = (r[4] >> 12) | (r[5] << 17);
-  o.w[5] = (r[5] >> 15) | (r[6] << 14);
-  o.w[6] = (r[6] >> 18) | (r[7] << 11);
-  o.w[7] = (r[7] >> 21) | (r[8] << 8);
+  asm("v_bfe_u32 %0, %8, 0, 29\n\t"
+      "v_lshl_or_b32 %0, %9, 29, %0\n\t"
+      "v_bfe_u32 %1, %9, 3, 26\n\t"
+      "v_lshl_or_b32 %1, %10, 26, %1\n\t"
+      "v_bfe_u32 %2, %10, 6, 23\n\t"
+      "v_lshl_or_b32 %2, %11, 23, %2\n\t"
+      "v_bfe_u32 %3, %11, 9, 20\n\t"
+      "v_lshl_or_b32 %3, %12, 20, %3\n\t"
+      "v_bfe_u32 %4, %12, 12, 17\n\t"
+      "v_lshl_or_b32 %4, %13, 17, %4\n\t"
+      "v_bfe_u32 %5, %13, 15, 14\n\t"
+      "v_lshl_or_b32 %5, %14, 14, %5\n\t"
+      "v_bfe_u32 %6, %14, 18, 11\n\t"
+      "v_lshl_or_b32 %6, %15, 11, %6\n\t"
+      "v_bfe_u32 %7, %15, 21, 8\n\t"
+      "v_lshl_or_b32 %7, %16, 8, %7"  // r < 2p < 2^255: limb 8 < 2^23
+      : "=&v"(o.w[0]), "=&v"(o.w[1]), "=&v"(o.w[2]), "=&v"(o.w[3]), "=&v"(o.w[4]), "=&v"(o.w[5]), "=&v"(o.w[6]),
+        "=&v"(o.w[7])
+      : "v"(lo[0]), "v"(lo[1]), "v"(lo[2]), "v"(lo[3]), "v"(lo[4]), "v"(lo[5]), "v"(lo[6]), "v"(lo[7]), "v"(lo[8]));
   return o;
 }
 

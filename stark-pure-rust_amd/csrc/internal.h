@@ -78,8 +78,8 @@ struct Twiddles {
   fe* d_full = nullptr;
   fe* d_full_s = nullptr;
   size_t n_small_pairs = 0;      // Shoup pairs in d_small
-  // Digit-basis tables (fe_db.h) of w_R^(4k), k < R/8, for every radix R = 2^l >= 16: the constants of
-  // the radix-4 steps before a pass's last one.  db_off[l] = offset in u32 into d_db (72 u32 per root).
+  // Digit-basis tables (fe_db.h) of w_R^k, k < R/2, for every radix R = 2^l >= 16: the constants of the
+  // radix-4 steps (ntt.hip DbPlan).  db_off[l] = offset in u32 into d_db (72 u32 per root).
   uint32_t* d_db = nullptr;
   uint32_t db_off[16] = {0};
   Tw29* t29 = nullptr;    // radix-2^29 images of these tables (ntt29.hip), built on first use

@@ -78,26 +78,31 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #ifndef STARK_NTT_DB
 #define STARK_NTT_DB 1
 #endif
-// STARK_NTT_DB_GLOBAL=1: the tables are read through the vector L1 (9 KB, cache-resident) instead of
-// being copied to LDS, which keeps the pass at 40 KB of LDS (four workgroups per CU).
-#ifndef STARK_NTT_DB_GLOBAL
-#define STARK_NTT_DB_GLOBAL 0
-#endif
 // The first pass (no column twiddle) keeps the Shoup-only form at four workgroups per CU unless
 // STARK_NTT_DB_FIRST=1: with 49 KB of LDS (three per CU) it measured slower there.
 #ifndef STARK_NTT_DB_FIRST
 #define STARK_NTT_DB_FIRST 0
 #endif
+// STARK_NTT_DB_FULL=1: every radix-4 step, the last one included, uses the digit-basis product from a
+// table of all R/2 constants (36 KB for R = 256; the Shoup pairs are then not staged), two workgroups
+// per CU.
+#ifndef STARK_NTT_DB_FULL
+#define STARK_NTT_DB_FULL 0
+#endif
 template <int LOG_R, int COL>
 struct DbPlan {
   static constexpr bool on = STARK_NTT_DB && LOG_R >= 4 && (COL != 0 || STARK_NTT_DB_FIRST);
-  static constexpr uint32_t entries = on ? (1u << LOG_R) / 8 : 0;
+  static constexpr bool full = on && STARK_NTT_DB_FULL;
+  static constexpr uint32_t stride = full ? 1 : 4;  // the table holds w_R^(stride k), k < R / (2 stride)
+  static constexpr uint32_t entries = on ? (1u << LOG_R) / (2 * stride) : 0;
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
-  static constexpr uint32_t lds_fe = STARK_NTT_DB_GLOBAL || !on ? 0 : entries * 9 + entries / 16;
+  static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
+  static constexpr uint32_t shoup_fe = full ? 0 : (1u << LOG_R);  // staged Shoup pairs (R/2 roots)
+  static constexpr int occupancy = !on ? 4 : full ? 2 : 3;        // workgroups per CU the LDS allows
 };
 
 template <int LOG_R, bool PERSIST, int COL>
-__global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
+__global__ __launch_bounds__(256, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
                                                           const fe* __restrict__ small, const uint32_t* __restrict__ db,
                                                           fe scale, int do_scale,
@@ -106,12 +111,8 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)
   using DB = DbPlan<LOG_R, COL>;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
   fe* sm = lds;          // R/2 small roots w_R^k as Shoup pairs: sm[2k] = w_R^k, sm[2k + 1] = its quotient
-#if STARK_NTT_DB_GLOBAL
-  const uint32_t* sdb = db;  // digit-basis tables of w_R^(4k), k < R/8 (L1-resident)
-#else
-  uint32_t* sdb = reinterpret_cast<uint32_t*>(lds + R);  // digit-basis tables of w_R^(4k), k < R/8
-#endif
-  fe* X = lds + R + DB::lds_fe;  // [R][B] data image
+  uint32_t* sdb = reinterpret_cast<uint32_t*>(lds + DB::shoup_fe);  // digit-basis tables (DbPlan)
+  fe* X = lds + DB::shoup_fe + DB::lds_fe;  // [R][B] data image
   const uint32_t B = 1u << log_b;
   const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
   const uint32_t tid = threadIdx.x;
@@ -120,10 +121,15 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
   const uint32_t tile_mask = (1u << log_tiles) - 1;
 
-  for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
-  if (DB::on && !STARK_NTT_DB_GLOBAL)
-    for (uint32_t k = tid; k < DB::entries * 18; k += blockDim.x)
-      reinterpret_cast<uint4*>(lds + R)[k + ((k / 18) >> 3)] = reinterpret_cast<const uint4*>(db)[k];
+  if (!DB::full)
+    for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
+  // The global table holds every w_R^k, k < R/2; the LDS copy every stride-th one.
+  if (DB::on)
+    for (uint32_t k = tid; k < DB::entries * 18; k += blockDim.x) {
+      const uint32_t e = k / 18;
+      reinterpret_cast<uint4*>(sdb)[k + (e >> 3)] =
+          reinterpret_cast<const uint4*>(db)[(e * DB::stride) * 18 + (k - e * 18)];
+    }
 
   // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row).
   uint32_t eb[4], er[4];
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)
         fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
         fe t3;
         if (DB::on) {
-          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) >> 2));  // w_4^1 = w_R^(R/4)
+          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
         } else {
           const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
           t3 = shoup_b(x3, sm[ic], sm[ic + 1]);
@@ -272,7 +278,7 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)
     }
     if (DB::on) {
 #pragma unroll 1
-      for (; s < (int)LOG_R - 2; s += 2) {
+      for (; s < (int)LOG_R - (DB::full ? 0 : 2); s += 2) {
         if (active) {
           const uint32_t m = 1u << s;
           const uint32_t jj = q & (m - 1);
@@ -282,13 +288,14 @@ __global__ __launch_bounds__(256, PERSIST ? 2 : (DbPlan<LOG_R, COL>::on ? 3 : 4)
           fe x2 = X[((base + 2 * m) << log_b) + b];
           fe x3 = X[((base + 3 * m) << log_b) + b];
           // exponents (in w_R units) jj R/2m, jj R/4m, (jj + m) R/4m: multiples of 4 before the last step
-          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) >> 2);  // w_{2m}^jj
+          constexpr uint32_t S = DB::stride;
+          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) / S);  // w_{2m}^jj
           const fe t1 = fe_mul_db(x1, wa);
           fe t3 = fe_mul_db(x3, wa);
           fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
           fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
-          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) >> 2));  // w_{4m}^jj
-          t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) >> 2));   // w_{4m}^(jj+m)
+          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) / S));  // w_{4m}^jj
+          t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) / S));   // w_{4m}^(jj+m)
           fe_bfly_lazy(x0, x2, t2);
           fe_bfly_lazy(x1, x3, t3);
           X[(base << log_b) + b] = x0;
@@ -401,8 +408,7 @@ constexpr uint32_t kMaxLogR = 9;  // largest radix with a kernel instance and sm
 // so 2^25 and 2^26 take three passes, not four (2^26: 13.25 n products instead of 14.5 n, with the
 // column-twiddle table of 2^18 entries below).
 inline uint32_t max_log_r(uint32_t log_n) { return log_n >= 25 ? 9 : 8; }
-// Workgroups of a persistent pass: 256 CUs x 2 resident 256-thread groups.
-constexpr uint64_t kPersistentGrid = 256 * 2;
+// Workgroups of a persistent pass: 256 CUs x the resident 256-thread groups its LDS allows.
 #ifndef STARK_NTT_PERSISTENT
 #define STARK_NTT_PERSISTENT 0
 #endif
@@ -432,16 +438,37 @@ uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r) {
 typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, const uint32_t*, fe, int,
                         uint32_t, uint32_t, Sparse);
 
+// LDS of a pass instance beyond its data image: staged Shoup pairs + digit-basis tables (in fe).
 template <int COL>
 size_t db_lds_fe_c(uint32_t log_r) {
   switch (log_r) {
-    case 4: return DbPlan<4, COL>::lds_fe;
-    case 5: return DbPlan<5, COL>::lds_fe;
-    case 6: return DbPlan<6, COL>::lds_fe;
-    case 7: return DbPlan<7, COL>::lds_fe;
-    case 8: return DbPlan<8, COL>::lds_fe;
-    case 9: return DbPlan<9, COL>::lds_fe;
-    default: return 0;
+    case 4: return DbPlan<4, COL>::lds_fe + DbPlan<4, COL>::shoup_fe;
+    case 5: return DbPlan<5, COL>::lds_fe + DbPlan<5, COL>::shoup_fe;
+    case 6: return DbPlan<6, COL>::lds_fe + DbPlan<6, COL>::shoup_fe;
+    case 7: return DbPlan<7, COL>::lds_fe + DbPlan<7, COL>::shoup_fe;
+    case 8: return DbPlan<8, COL>::lds_fe + DbPlan<8, COL>::shoup_fe;
+    case 9: return DbPlan<9, COL>::lds_fe + DbPlan<9, COL>::shoup_fe;
+    default: return (size_t)1 << log_r;
+  }
+}
+template <int COL>
+int occupancy_c(uint32_t log_r) {
+  switch (log_r) {
+    case 4: return DbPlan<4, COL>::occupancy;
+    case 5: return DbPlan<5, COL>::occupancy;
+    case 6: return DbPlan<6, COL>::occupancy;
+    case 7: return DbPlan<7, COL>::occupancy;
+    case 8: return DbPlan<8, COL>::occupancy;
+    case 9: return DbPlan<9, COL>::occupancy;
+    default: return 4;
+  }
+}
+int pass_occupancy(uint32_t log_r, int col) {
+  switch (col) {
+    case kColNone: return occupancy_c<kColNone>(log_r);
+    case kColFull: return occupancy_c<kColFull>(log_r);
+    case kColT16: return occupancy_c<kColT16>(log_r);
+    default: return occupancy_c<kColTwoLevel>(log_r);
   }
 }
 size_t db_lds_fe(uint32_t log_r, int col) {
@@ -575,17 +602,18 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     }
   }
   tw->n_small_pairs = h_small.size() / 2;
-  // Digit-basis tables: w_R^(4k), k < R/8, for R = 2^l, 4 <= l <= min(log_n, 9).
+  // Digit-basis tables: w_R^k, k < R/2, for R = 2^l, 4 <= l <= min(log_n, 9) (a pass stages every
+  // stride-th one, DbPlan).
   std::vector<uint32_t> h_db;
   for (uint32_t l = 4; l <= kMaxLogR && l <= log_n; ++l) {
     tw->db_off[l] = (uint32_t)h_db.size();
-    const HostFp w4 = F.pow_u64(w, (uint64_t)4 << (log_n - l));
+    const HostFp wr = F.pow_u64(w, (uint64_t)1 << (log_n - l));
     HostFp a = F.one();
-    for (uint32_t k = 0; k < (1u << (l - 3)); ++k) {
+    for (uint32_t k = 0; k < (1u << (l - 1)); ++k) {
       uint32_t t[72];
       db_table(a, t);
       h_db.insert(h_db.end(), t, t + 72);
-      a = F.mul(a, w4);
+      a = F.mul(a, wr);
     }
   }
   if (h_db.empty()) h_db.resize(72, 0);
@@ -722,11 +750,8 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     const uint32_t lb = ntt_choose_log_b(log_n, lr);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
-    // (data image + R/2 Shoup pairs + the digit-basis tables: sized below, once the pass's column source is known)
     const uint32_t log_tiles = log_n - lr - lb;
     const uint64_t total = (uint64_t)batch << log_tiles;
-    const bool persist = kPersistent && total > kPersistentGrid;
-    const unsigned grid = (unsigned)(persist ? kPersistentGrid : total);
     // Inverse: n^-1 rides on the last pass's column twiddles (scaled tables)
     // when that pass has them (log_ns > 0), else it is an explicit product.
     const bool fold = inverse && last && log_ns > 0;
@@ -737,7 +762,11 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     }
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
     const int col = log_ns == 0 ? kColNone : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
-    const size_t lds = ((size_t)elems + (1u << lr) + db_lds_fe(lr, col)) * sizeof(fe);
+    // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
+    const size_t lds = ((size_t)elems + db_lds_fe(lr, col)) * sizeof(fe);
+    const uint64_t persistent_grid = 256 * (uint64_t)pass_occupancy(lr, col);
+    const bool persist = kPersistent && total > persistent_grid;
+    const unsigned grid = (unsigned)(persist ? persistent_grid : total);
     hipLaunchKernelGGL(pass_kernel(lr, persist, col), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
                        (inverse && last && !fold) ? 1 : 0, log_tiles,
