@@ -238,7 +238,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (void* p : ctx->pinned)
     if (p) hipHostFree(p);
   ctx->fri_trees.clear();
-  for (DevBuf* b : {&ctx->scratch, &ctx->scratch2, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->fri_misc,
+  for (DevBuf* b : {&ctx->scratch, &ctx->scratch2, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);

@@ -100,6 +100,7 @@ struct stark_ctx {
   stark::DevBuf fri_cols;    // folded FRI columns (prove_low_degree)
   stark::DevBuf r1cs_arena;  // mk_r1cs_proof working set
   stark::DevBuf trace_arena;  // device trace builder working set (r1cs_trace_dev.hip)
+  stark::DevBuf trace_raw;    // the raw constraint section and witness bytes it reads
   stark::DevBuf lde_tmp;      // circuit_lde's step columns and Zb values
   stark::DevBuf verify_arena, verify_lde;  // the verifier's circuit, kept for the next call
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
@@ -107,8 +108,8 @@ struct stark_ctx {
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<stark_merkle_tree*> fri_trees;  // one per FRI layer (+ the input's), reused across proofs
   stark::DevBuf fri_misc;                     // per-layer special_x (device transcript)
-  void* pinned[2] = {nullptr, nullptr};       // pinned host scratch (ctx_pinned)
-  size_t pinned_bytes[2] = {0, 0};
+  void* pinned[3] = {nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
+  size_t pinned_bytes[3] = {0, 0, 0};
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
 };
@@ -124,7 +125,8 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
 
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
 // Context-owned pinned host scratch of at least `bytes` (async copy target).
-// Slot 0: gather batches; slot 1: transcript values and roots.
+// Slot 0: gather batches; slot 1: transcript values and roots; slot 2: the device trace builder's
+// record-walk tables.
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
 
 // Host worker threads shared by the host-side stages (trace build, proof

@@ -159,14 +159,14 @@ unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 // One host pass over the constraint records' counts: fac = fac_rec[3 n_c] (byte
 // offset of each factor's first record) | fac_cnt[3 n_c] | pad, and base[ci] = the
-// first slot of constraint ci (n_c + 1 entries; run.rs:109-137 slot counts).
-stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, std::vector<uint32_t>& fac,
-                          std::vector<uint32_t>& base) {
+// first slot of constraint ci (n_c + 1 entries; run.rs:109-137 slot counts).  Every
+// entry is written (no zero fill), so the arrays may be reused uninitialised memory.
+stark_status walk_records_into(const uint8_t* cons, size_t cons_len, uint32_t n_c, uint32_t* fac, uint32_t* base) {
   if (cons_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
-  fac.assign((size_t)6 * n_c + 1, 0);
-  base.assign((size_t)n_c + 1, 0);
-  uint32_t* fac_rec = fac.data();
-  uint32_t* fac_cnt = fac.data() + (size_t)3 * n_c;
+  uint32_t* fac_rec = fac;
+  uint32_t* fac_cnt = fac + (size_t)3 * n_c;
+  fac[(size_t)6 * n_c] = 0;
+  base[0] = 0;
   size_t pos = 0;
   uint64_t b = 0;
   for (uint32_t ci = 0; ci < n_c; ++ci) {
@@ -187,6 +187,13 @@ stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, st
     base[ci + 1] = (uint32_t)b;
   }
   return STARK_OK;
+}
+
+stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, std::vector<uint32_t>& fac,
+                          std::vector<uint32_t>& base) {
+  fac.resize((size_t)6 * n_c + 1);
+  base.resize((size_t)n_c + 1);
+  return walk_records_into(cons, cons_len, n_c, fac.data(), base.data());
 }
 
 }  // namespace
@@ -216,16 +223,39 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
     memcpy(&out->public_wires[4 * i], v.v, 32);
   }
 
-  // Host walk: record counts only (the records themselves are read on the GPU).
+  // Host walk: record counts only (the records themselves are read on the GPU).  It runs on a host
+  // worker while this thread uploads the raw constraint section and witness (pageable memory: the
+  // copies block), and it writes straight into pinned memory, so its tables go up asynchronously.
   const uint8_t* cons = r1cs + hd.cons_off;
   const size_t cons_len = r1cs_len - hd.cons_off;
-  std::vector<uint32_t> fac, base;
-  st = walk_records(cons, cons_len, n_c, fac, base);
+  const size_t wbytes = (size_t)n_wit * wh.field_size;
+  const size_t fac_n = (size_t)6 * n_c + 1, base_n = (size_t)n_c + 1;
+  uint32_t* walk = nullptr;
+  st = ctx_pinned(ctx, 2, (fac_n + base_n) * 4, (void**)&walk);
   if (st != STARK_OK) return st;
+  uint32_t* fac = walk;
+  uint32_t* base = walk + fac_n;
+  const size_t o_raw_w = (cons_len + 255) & ~(size_t)255;
+  st = ensure_buf(ctx, ctx->trace_raw, o_raw_w + wbytes);
+  if (st != STARK_OK) return st;
+  uint8_t* RAW = (uint8_t*)ctx->trace_raw.ptr;
+  hipStream_t s = ctx->stream;
+  stark_status walk_st = STARK_OK, up_st = STARK_OK;
+  host_parallel(2, [&](unsigned t) {
+    if (t == 1) {
+      walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
+      return;
+    }
+    if (hipMemcpyAsync(RAW, cons, cons_len, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(RAW + o_raw_w, wv, wbytes, hipMemcpyHostToDevice, s) != hipSuccess)
+      up_st = STARK_ERR_HIP;
+  });
+  if (up_st != STARK_OK) return hip_fail(ctx, hipGetLastError(), "r1cs/wtns upload");
+  if (walk_st != STARK_OK) return walk_st;
   const uint64_t a_len = base[n_c];
   const uint64_t os = 3 * a_len;
   if (a_len == 0) return STARK_ERR_BAD_ARG;
-  clk.mark("headers + record walk");
+  clk.mark("headers + record walk || uploads");
 
   // Device buffers (context-owned arena).
   uint32_t key_bits = 1;
@@ -234,27 +264,22 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
                                                    (int)key_bits, ctx->stream));
-  const size_t wbytes = (size_t)n_wit * wh.field_size;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
     off += (bytes + 255) & ~(size_t)255;
     return o;
   };
-  const size_t o_cons = take(cons_len), o_w = take(wbytes), o_fac = take(fac.size() * 4),
-               o_base = take(base.size() * 4), o_wcan = take((size_t)n_wit * 32), o_wmont = take((size_t)n_wit * 32),
-               o_coef = take(os * 32), o_wit = take(os * 32), o_comp = take(os * 32), o_flags = take(3 * os),
-               o_perm = take(os * 8), o_k = take(os * 4), o_v = take(os * 4), o_k2 = take(os * 4),
-               o_v2 = take(os * 4), o_last = take((size_t)n_wires * 4), o_pf = take(n_public * 8), o_err = take(4),
-               o_tmp = take(sort_tmp);
+  const size_t o_fac = take(fac_n * 4), o_base = take(base_n * 4), o_wcan = take((size_t)n_wit * 32),
+               o_wmont = take((size_t)n_wit * 32), o_coef = take(os * 32), o_wit = take(os * 32),
+               o_comp = take(os * 32), o_flags = take(3 * os), o_perm = take(os * 8), o_k = take(os * 4),
+               o_v = take(os * 4), o_k2 = take(os * 4), o_v2 = take(os * 4), o_last = take((size_t)n_wires * 4),
+               o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp);
   st = ensure_buf(ctx, ctx->trace_arena, off);
   if (st != STARK_OK) return st;
   uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
-  hipStream_t s = ctx->stream;
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_cons, cons, cons_len, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_w, wv, wbytes, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac.data(), fac.size() * 4, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base.data(), base.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac, fac_n * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base, base_n * 4, hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
   STARK_HIP(ctx, hipMemsetAsync(A + o_pf, 0xFF, n_public * 8, s));
   fe* wcan = (fe*)(A + o_wcan);
@@ -263,11 +288,11 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   {
     uint64_t one_r[4];  // Montgomery image of R = R^2 mod p
     memcpy(one_r, F.one().v, 32);
-    hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
+    hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(RAW + o_raw_w),
                        wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), wcan, wmont);
   }
   FillArgs fa;
-  fa.cons = A + o_cons;
+  fa.cons = RAW;
   fa.fac_rec = (const uint32_t*)(A + o_fac);
   fa.fac_cnt = (const uint32_t*)(A + o_fac) + (size_t)3 * n_c;
   fa.base = (const uint32_t*)(A + o_base);
