@@ -60,43 +60,69 @@ struct FillArgs {
   uint32_t* err;
 };
 
-// calc_coefficients_and_witness (run.rs:109-281): factor f of constraint ci
-// owns slots base[ci] .. base[ci+1]-1 of third f; a slot past the factor's
-// records is padding (last wire, coefficient 0, running sum unchanged).
+// The constraint whose slots contain slot j of a third: the last ci with base[ci] <= j (empty
+// constraints share their base with the next one, so the last is the owner).
+__device__ __forceinline__ uint32_t owner_of(const uint32_t* __restrict__ base, uint32_t n_constraints, uint32_t j) {
+  uint32_t lo = 0, hi = n_constraints;  // base[lo] <= j < base[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (base[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// calc_coefficients_and_witness (run.rs:109-281), one thread per slot: factor f of constraint ci
+// owns slots base[ci] .. base[ci+1]-1 of third f; a slot past the factor's records is padding
+// (last wire, coefficient 0).  The slot's term coefficient * witness goes to comp; running_sum_kernel
+// then forms the running sums, so the products run in parallel and only additions are serial
+// (a factor may hold a thousand terms: bits.r1cs).
 __global__ void slot_fill_kernel(FillArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 3 * (uint64_t)a.n_constraints) return;
-  const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
-  const uint32_t b0 = a.base[ci], n_coeff = a.base[ci + 1] - b0;
-  const uint32_t cnt = a.fac_cnt[t];
-  const uint8_t* rec = a.cons + a.fac_rec[t];
-  fe tacc = fe_zero();
-  const uint64_t push0 = 3 * (uint64_t)b0 + (uint64_t)f * n_coeff;
-  for (uint32_t i = 0; i < n_coeff; ++i) {
-    const uint64_t slot = (uint64_t)f * a.a_len + b0 + i;
-    uint32_t wire = a.n_wires - 1;
-    fe cf = fe_zero();
-    if (i < cnt) {
-      const uint32_t* r = reinterpret_cast<const uint32_t*>(rec + 36 * (uint64_t)i);
-      wire = r[0];
-      if (wire >= a.n_wires) {
-        atomicOr(a.err, 1u);
-        wire = a.n_wires - 1;
-      }
-      fe v;
+  if (t >= 3 * a.a_len) return;
+  const uint32_t f = (uint32_t)(t / a.a_len), j = (uint32_t)(t - (uint64_t)f * a.a_len);
+  const uint32_t ci = owner_of(a.base, a.n_constraints, j);
+  const uint32_t b0 = a.base[ci], n_coeff = a.base[ci + 1] - b0, i = j - b0;
+  const uint64_t fi = 3 * (uint64_t)ci + f;
+  const uint32_t cnt = a.fac_cnt[fi];
+  const uint64_t slot = t;  // f a_len + b0 + i
+  uint32_t wire = a.n_wires - 1;
+  fe cf = fe_zero();
+  if (i < cnt) {
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(a.cons + a.fac_rec[fi] + 36 * (uint64_t)i);
+    wire = r[0];
+    if (wire >= a.n_wires) {
+      atomicOr(a.err, 1u);
+      wire = a.n_wires - 1;
+    }
+    fe v;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v.w[k] = r[1 + k];
-      cf = reduce_any(v);                                       // canonical from_bytes_le
-      if (a.wmont) tacc = fe_add(tacc, fe_mul(cf, fe_load(a.wmont + wire)));  // canonical * Montgomery
-    }
-    fe_store(a.coef + slot, cf);
-    if (a.wmont) {  // no witness: circuit columns only
-      fe_store(a.wit + slot, fe_load(a.wcan + wire));
-      fe_store(a.comp + slot, tacc);
-    }
-    if (a.slot_wire) a.slot_wire[slot] = wire;
-    a.keys[push0 + i] = wire;
-    a.vals[push0 + i] = (uint32_t)slot;
+    for (int k = 0; k < 8; ++k) v.w[k] = r[1 + k];
+    cf = reduce_any(v);  // canonical from_bytes_le
+  }
+  fe_store(a.coef + slot, cf);
+  if (a.wmont) {  // no witness: circuit columns only
+    fe_store(a.wit + slot, fe_load(a.wcan + wire));
+    fe_store(a.comp + slot, i < cnt ? fe_mul(cf, fe_load(a.wmont + wire)) : fe_zero());  // canonical * Montgomery
+  }
+  if (a.slot_wire) a.slot_wire[slot] = wire;
+  const uint64_t push = 3 * (uint64_t)b0 + (uint64_t)f * n_coeff + i;
+  a.keys[push] = wire;
+  a.vals[push] = (uint32_t)slot;
+}
+
+// comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels).
+__global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
+                                   fe* __restrict__ comp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 3 * (uint64_t)n_constraints) return;
+  const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
+  const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
+  fe* c = comp + (uint64_t)f * a_len + b0;
+  fe acc = fe_zero();
+  for (uint32_t i = 0; i < n_coeff; ++i) {
+    acc = fe_add(acc, fe_load(c + i));
+    fe_store(c + i, acc);
   }
 }
 
@@ -135,24 +161,16 @@ __global__ void perm_kernel(const uint32_t* __restrict__ keys, const uint32_t* _
   if (start && k < n_public) pf[k] = vals[j];
 }
 
-// The witness columns of a prepared circuit: the slot fill's witness / running-sum
-// part (run.rs:109-281) from the stored slot wires and coefficients.
-__global__ void wit_fill_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
-                                const uint32_t* __restrict__ slot_wire, const fe* __restrict__ coef,
+// The witness columns of a prepared circuit: the slot fill's witness / term part (run.rs:109-281) from
+// the stored slot wires and coefficients, one thread per slot (running_sum_kernel follows).
+__global__ void wit_fill_kernel(uint64_t n_slots, const uint32_t* __restrict__ slot_wire, const fe* __restrict__ coef,
                                 const fe* __restrict__ wcan, const fe* __restrict__ wmont, fe* __restrict__ wit,
                                 fe* __restrict__ comp) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 3 * (uint64_t)n_constraints) return;
-  const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
-  const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
-  fe tacc = fe_zero();
-  for (uint32_t i = 0; i < n_coeff; ++i) {
-    const uint64_t slot = (uint64_t)f * a_len + b0 + i;
-    const uint32_t wire = slot_wire[slot];
-    tacc = fe_add(tacc, fe_mul(fe_load(coef + slot), fe_load(wmont + wire)));  // padding slots: coefficient 0
-    fe_store(wit + slot, fe_load(wcan + wire));
-    fe_store(comp + slot, tacc);
-  }
+  const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= n_slots) return;
+  const uint32_t wire = slot_wire[slot];
+  fe_store(comp + slot, fe_mul(fe_load(coef + slot), fe_load(wmont + wire)));  // padding slots: coefficient 0
+  fe_store(wit + slot, fe_load(wcan + wire));
 }
 
 unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
@@ -308,7 +326,10 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   fa.vals = (uint32_t*)(A + o_v);
   fa.slot_wire = nullptr;
   fa.err = err;
-  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa);
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * a_len)), dim3(256), 0, s, fa);
+  if (fa.wmont)
+    hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
+                       fa.comp);
   uint8_t* flags = A + o_flags;
   STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));  // flag0, flag1 = 1
   STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
@@ -419,7 +440,10 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   fa.vals = (uint32_t*)(A + o_v);
   fa.slot_wire = (uint32_t*)(A + o_sw);
   fa.err = (uint32_t*)(A + o_err);
-  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa);
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * a_len)), dim3(256), 0, s, fa);
+  if (fa.wmont)
+    hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
+                       fa.comp);
   uint8_t* flags = A + o_flags;
   STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));
   STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
@@ -499,8 +523,9 @@ static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, co
   hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
                      wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), (fe*)(A + o_wcan),
                      (fe*)(A + o_wmont));
-  hipLaunchKernelGGL(wit_fill_kernel, dim3(blocks(3 * (uint64_t)c.n_c)), dim3(256), 0, s, c.base, c.n_c, c.a_len,
-                     c.slot_wire, c.coef, (const fe*)(A + o_wcan), (const fe*)(A + o_wmont), (fe*)(A + o_wit),
+  hipLaunchKernelGGL(wit_fill_kernel, dim3(blocks(3 * c.a_len)), dim3(256), 0, s, 3 * c.a_len, c.slot_wire, c.coef,
+                     (const fe*)(A + o_wcan), (const fe*)(A + o_wmont), (fe*)(A + o_wit), (fe*)(A + o_comp));
+  hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)c.n_c)), dim3(256), 0, s, c.base, c.n_c, c.a_len,
                      (fe*)(A + o_comp));
   STARK_HIP(ctx, hipGetLastError());
   out->os = c.os;
