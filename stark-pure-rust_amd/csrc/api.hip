@@ -48,7 +48,7 @@ class HostWorkers {
   unsigned threads() const { return (unsigned)workers_ + 1; }
   void run(unsigned n, const std::function<void(unsigned)>& fn) {
     if (n == 0) return;
-    if (n == 1 || workers_ == 0) {
+    if (n == 1 || workers_ == 0 || in_job()) {  // a job that calls host_parallel runs the inner one serially
       for (unsigned k = 0; k < n; ++k) fn(k);
       return;
     }
@@ -62,8 +62,10 @@ class HostWorkers {
       ++gen_;
     }
     cv_.notify_all();
+    in_job() = true;
     fn(0);
     drain();
+    in_job() = false;
     std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [&] { return pending_ == 0; });
     job_ = nullptr;
@@ -75,6 +77,10 @@ class HostWorkers {
     hw = hw < 1 ? 1 : (hw > 16 ? 16 : hw);
     workers_ = hw - 1;
     for (unsigned i = 0; i < workers_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  static bool& in_job() {
+    thread_local bool flag = false;
+    return flag;
   }
   void drain() {
     for (unsigned k; (k = next_.fetch_add(1)) < n_;) {
@@ -91,7 +97,9 @@ class HostWorkers {
         cv_.wait(g, [&] { return gen_ != seen; });
         seen = gen_;
       }
+      in_job() = true;
       drain();
+      in_job() = false;
     }
   }
   size_t workers_ = 0;

@@ -485,37 +485,101 @@ static uint32_t log2_ceil_ref(size_t v) {
 
 static HostFp host_fe(const uint64_t* c) { return FieldHost::get().from_canonical(c); }
 
-// lagrange_interp (fri/src/poly_utils.rs:409-439): the unique interpolant,
-// n coefficients, Montgomery on the host.
+// c = a * b (coefficient lists, low degree first); the output coefficients are split over the
+// host workers when the product is large.
+static std::vector<HostFp> poly_mul(const std::vector<HostFp>& a, const std::vector<HostFp>& b) {
+  const FieldHost& F = FieldHost::get();
+  std::vector<HostFp> c(a.size() + b.size() - 1, F.zero());
+  const size_t nc = c.size();
+  const unsigned T = a.size() * b.size() > 20000 ? host_threads() : 1;
+  host_parallel(T, [&](unsigned t) {
+    for (size_t k = t; k < nc; k += T) {
+      const size_t lo = k >= b.size() ? k - (b.size() - 1) : 0, hi = k < a.size() ? k : a.size() - 1;
+      HostFp acc = F.zero();
+      for (size_t i = lo; i <= hi; ++i) acc = F.add(acc, F.mul(a[i], b[k - i]));
+      c[k] = acc;
+    }
+  });
+  return c;
+}
+
+// lagrange_interp (fri/src/poly_utils.rs:409-439): the unique interpolant, n coefficients, Montgomery on
+// the host.  The same polynomial as the reference's, by another O(n^2) route that parallelises:
+//   root = prod (X - x_i) by a product tree (leaves on the host workers),
+//   den_i = root'(x_i) = prod_{j != i} (x_i - x_j), one batch inverse (0 -> 0, as F.inv),
+//   b = sum_i (y_i / den_i) root / (X - x_i), each worker summing its share of the i.
+// (A public-input list of 1,062 wires, bits.r1cs, took 70 ms serially.)
 std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys) {
   const FieldHost& F = FieldHost::get();
   const size_t n = xs.size();
-  std::vector<HostFp> root(1, F.one());
-  for (size_t i = 0; i < n; ++i) {  // prod (X - x_i), low degree first
-    std::vector<HostFp> nxt(root.size() + 1, F.zero());
-    for (size_t j = 0; j < root.size(); ++j) {
-      nxt[j + 1] = F.add(nxt[j + 1], root[j]);
-      nxt[j] = F.sub(nxt[j], F.mul(root[j], xs[i]));
+  if (n == 0) return {};
+  const unsigned T = n >= 64 ? host_threads() : 1;
+  // Product tree: T leaf products, then pairwise merges.
+  std::vector<std::vector<HostFp>> parts(T);
+  host_parallel(T, [&](unsigned t) {
+    const size_t i0 = n * t / T, i1 = n * (t + 1) / T;
+    std::vector<HostFp> r(1, F.one());
+    for (size_t i = i0; i < i1; ++i) {
+      std::vector<HostFp> nxt(r.size() + 1, F.zero());
+      for (size_t j = 0; j < r.size(); ++j) {
+        nxt[j + 1] = F.add(nxt[j + 1], r[j]);
+        nxt[j] = F.sub(nxt[j], F.mul(r[j], xs[i]));
+      }
+      r.swap(nxt);
     }
-    root.swap(nxt);
+    parts[t] = std::move(r);
+  });
+  while (parts.size() > 1) {
+    std::vector<std::vector<HostFp>> next;
+    for (size_t i = 0; i + 1 < parts.size(); i += 2) next.push_back(poly_mul(parts[i], parts[i + 1]));
+    if (parts.size() & 1) next.push_back(std::move(parts.back()));
+    parts.swap(next);
   }
-  std::vector<HostFp> b(n, F.zero()), num(n), den(n);
-  std::vector<std::vector<HostFp>> nums(n);
-  for (size_t i = 0; i < n; ++i) {
-    HostFp carry = F.zero();
-    for (size_t d = n; d >= 1; --d) {  // root / (X - x_i), synthetic division
-      carry = d == n ? root[d] : F.add(root[d], F.mul(carry, xs[i]));
-      num[d - 1] = carry;
+  const std::vector<HostFp>& root = parts[0];  // n + 1 coefficients, root[n] = 1
+  std::vector<HostFp> droot(n);
+  for (size_t d = 1; d <= n; ++d) droot[d - 1] = F.mul(root[d], F.from_u64(d));
+  std::vector<HostFp> den(n);
+  host_parallel(T, [&](unsigned t) {
+    for (size_t i = t; i < n; i += T) {
+      HostFp y = F.zero();
+      for (size_t d = n; d-- > 0;) y = F.add(F.mul(y, xs[i]), droot[d]);
+      den[i] = y;
     }
-    HostFp y = F.zero();
-    for (size_t d = n; d-- > 0;) y = F.add(F.mul(y, xs[i]), num[d]);
-    den[i] = y;
-    nums[i] = num;
-  }
+  });
+  // Batch inverse with zeros kept (F.inv(0) = 0).
+  std::vector<HostFp> pre(n);
+  HostFp acc = F.one();
   for (size_t i = 0; i < n; ++i) {
-    const HostFp s = F.mul(ys[i], F.inv(den[i]));
-    for (size_t j = 0; j < n; ++j) b[j] = F.add(b[j], F.mul(nums[i][j], s));
+    pre[i] = acc;
+    if (!FieldHost::eq(den[i], F.zero())) acc = F.mul(acc, den[i]);
   }
+  HostFp inv_acc = F.inv(acc);
+  std::vector<HostFp> s(n);
+  for (size_t i = n; i-- > 0;) {
+    if (FieldHost::eq(den[i], F.zero())) {
+      s[i] = F.zero();
+      continue;
+    }
+    s[i] = F.mul(ys[i], F.mul(inv_acc, pre[i]));
+    inv_acc = F.mul(inv_acc, den[i]);
+  }
+  std::vector<std::vector<HostFp>> partial(T, std::vector<HostFp>(n, F.zero()));
+  host_parallel(T, [&](unsigned t) {
+    std::vector<HostFp>& b = partial[t];
+    std::vector<HostFp> num(n);
+    for (size_t i = t; i < n; i += T) {
+      HostFp carry = root[n];
+      num[n - 1] = carry;
+      for (size_t d = n - 1; d >= 1; --d) {  // root / (X - x_i), synthetic division
+        carry = F.add(root[d], F.mul(carry, xs[i]));
+        num[d - 1] = carry;
+      }
+      for (size_t j = 0; j < n; ++j) b[j] = F.add(b[j], F.mul(num[j], s[i]));
+    }
+  });
+  std::vector<HostFp> b = std::move(partial[0]);
+  for (unsigned t = 1; t < T; ++t)
+    for (size_t j = 0; j < n; ++j) b[j] = F.add(b[j], partial[t][j]);
   return b;
 }
 
