@@ -72,33 +72,33 @@ __device__ __forceinline__ const uint32_t* dbt(const uint32_t* sdb, uint32_t k) 
 // kColTwoLevel: lo * hi, Montgomery).
 enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 
-// Radix-4 steps before a pass's last one multiply by the digit-basis product (fe_db.h): their
-// constants are w_R^(4k), k < R/8 (32 for R = 256, 9 KB of LDS), and the last step, whose R/2
-// constants would need 36 KB, keeps the Shoup pairs.  STARK_NTT_DB=0 builds the Shoup-only pass.
-#ifndef STARK_NTT_DB
-#define STARK_NTT_DB 1
+// Which radix-4 steps multiply by the digit-basis product (fe_db.h), STARK_NTT_DB_MODE:
+//   0  none: Shoup pairs of all R/2 roots staged in LDS (40 KB with the data image, 4 workgroups/CU);
+//   1  (default) the steps before a pass's last one, in passes with a column twiddle: their constants
+//      are w_R^(4k), k < R/8 (32 for R = 256, 9 KB); the last step keeps the staged Shoup pairs
+//      (49 KB, 3 workgroups/CU).  The first pass stays Shoup-only unless STARK_NTT_DB_FIRST=1;
+//   2  the steps with m <= 4 in every pass (8 constants w_R^(16k), 2.3 KB); the later steps read
+//      their Shoup pairs from global memory (L1/L2), so nothing else is staged (34 KB, 4/CU);
+//   3  every step, a table of all R/2 constants (36 KB, 2/CU).
+#ifndef STARK_NTT_DB_MODE
+#define STARK_NTT_DB_MODE 1
 #endif
-// The first pass (no column twiddle) keeps the Shoup-only form at four workgroups per CU unless
-// STARK_NTT_DB_FIRST=1: with 49 KB of LDS (three per CU) it measured slower there.
 #ifndef STARK_NTT_DB_FIRST
 #define STARK_NTT_DB_FIRST 0
 #endif
-// STARK_NTT_DB_FULL=1: every radix-4 step, the last one included, uses the digit-basis product from a
-// table of all R/2 constants (36 KB for R = 256; the Shoup pairs are then not staged), two workgroups
-// per CU.
-#ifndef STARK_NTT_DB_FULL
-#define STARK_NTT_DB_FULL 0
-#endif
 template <int LOG_R, int COL>
 struct DbPlan {
-  static constexpr bool on = STARK_NTT_DB && LOG_R >= 4 && (COL != 0 || STARK_NTT_DB_FIRST);
-  static constexpr bool full = on && STARK_NTT_DB_FULL;
-  static constexpr uint32_t stride = full ? 1 : 4;  // the table holds w_R^(stride k), k < R / (2 stride)
+  static constexpr int mode = STARK_NTT_DB_MODE;
+  static constexpr bool on = mode != 0 && LOG_R >= 4 && (COL != 0 || STARK_NTT_DB_FIRST || mode == 2);
+  static constexpr int s_end = !on ? 0 : mode == 1 ? LOG_R - 2 : mode == 2 ? 3 : LOG_R;  // DB for steps s < s_end
+  // the table holds w_R^(stride k), k < R / (2 stride)
+  static constexpr uint32_t stride = mode == 1 ? 4 : mode == 2 ? (1u << LOG_R) / 16 : 1;
   static constexpr uint32_t entries = on ? (1u << LOG_R) / (2 * stride) : 0;
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
   static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
-  static constexpr uint32_t shoup_fe = full ? 0 : (1u << LOG_R);  // staged Shoup pairs (R/2 roots)
-  static constexpr int occupancy = !on ? 4 : full ? 2 : 3;        // workgroups per CU the LDS allows
+  static constexpr bool shoup_global = on && mode == 2;  // later steps' Shoup pairs from global memory
+  static constexpr uint32_t shoup_fe = on && mode >= 2 ? 0 : (1u << LOG_R);  // staged Shoup pairs (R/2 roots)
+  static constexpr int occupancy = !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;  // workgroups per CU the LDS allows
 };
 
 template <int LOG_R, bool PERSIST, int COL>
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
   const uint32_t tile_mask = (1u << log_tiles) - 1;
 
-  if (!DB::full)
+  if (DB::shoup_fe)
     for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
   // The global table holds every w_R^k, k < R/2; the LDS copy every stride-th one.
   if (DB::on)
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass
     }
     if (DB::on) {
 #pragma unroll 1
-      for (; s < (int)LOG_R - (DB::full ? 0 : 2); s += 2) {
+      for (; s < DB::s_end; s += 2) {
         if (active) {
           const uint32_t m = 1u << s;
           const uint32_t jj = q & (m - 1);
@@ -317,15 +317,17 @@ __global__ __launch_bounds__(256, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass
         fe x2 = X[((base + 2 * m) << log_b) + b];
         fe x3 = X[((base + 3 * m) << log_b) + b];
         fe t1, t3;
+        // Shoup pairs staged in LDS, or (DbPlan mode 2) read from the global table through L1
+        const fe* shp = DB::shoup_global ? small : sm;
         const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
-        const fe ta = sm[ia], taq = sm[ia + 1];
+        const fe ta = shp[ia], taq = shp[ia + 1];
         shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
         fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
         fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
         const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
-        const fe tc = sm[ic], tcq = sm[ic + 1];
+        const fe tc = shp[ic], tcq = shp[ic + 1];
         const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
-        const fe t2 = shoup_a(x2, sm[ib], sm[ib + 1]);
+        const fe t2 = shoup_a(x2, shp[ib], shp[ib + 1]);
         t3 = shoup_b(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
