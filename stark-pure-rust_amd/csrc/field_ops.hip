@@ -44,19 +44,20 @@ __device__ __forceinline__ fe wg_others_product(fe t, const fe& one, fe* q, fe* 
   return fe_mul(before, after);
 }
 
-// Up pass: thread g owns elements [g*chunk, (g+1)*chunk): exclusive prefix
-// products of its non-zero elements into pref, then the workgroup scan gives
-// others[g] (the product of the other threads' chunks) and wg_tot[block].
+// Up pass: thread g owns elements g, g + T, g + 2T, .. (T = all threads of the launch, so a wave's
+// loads and stores are contiguous): exclusive prefix products of its non-zero elements into pref,
+// then the workgroup scan gives others[g] (the product of the other threads' elements) and
+// wg_tot[block].  Any partition gives the same inverses (each is exact; zeros map to zero).
 __global__ __launch_bounds__(kInvThreads) void inv_up_kernel(const fe* __restrict__ v, uint64_t n, uint32_t chunk,
                                                              fe* __restrict__ pref, fe* __restrict__ others,
                                                              fe* __restrict__ wg_tot, MontConsts mc) {
   __shared__ fe q[kInvThreads], sfx[kInvThreads];
+  (void)chunk;
   const uint64_t g = (uint64_t)blockIdx.x * kInvThreads + threadIdx.x;
-  const uint64_t lo = g * chunk;
-  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  const uint64_t T = (uint64_t)gridDim.x * kInvThreads;
   fe acc = mc.one;
-  for (uint64_t i = lo; i < hi; ++i) {
-    pref[i] = acc;
+  for (uint64_t i = g; i < n; i += T) {
+    fe_store(pref + i, acc);
     const fe x = fe_load(v + i);
     if (!fe_is_zero(x)) acc = fe_mul(acc, x);
   }
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(kInvThreads) void inv_up_kernel(const fe* __restric
 }
 
 // Down pass: wg_inv[block] = inverse of the workgroup total, so the inverse
-// of this thread's chunk product is wg_inv * others; then the chunk is walked
+// of this thread's product is wg_inv * others; then its elements are walked
 // backwards (poly_utils.rs:55-67 order).  OUT_CANON: level 0, canonical out.
 template <bool OUT_CANON>
 __global__ __launch_bounds__(kInvThreads) void inv_down_kernel(const fe* __restrict__ v, uint64_t n, uint32_t chunk,
@@ -74,12 +75,12 @@ __global__ __launch_bounds__(kInvThreads) void inv_down_kernel(const fe* __restr
                                                                const fe* __restrict__ others,
                                                                const fe* __restrict__ wg_inv, fe* __restrict__ out,
                                                                MontConsts mc) {
+  (void)chunk;
   const uint64_t g = (uint64_t)blockIdx.x * kInvThreads + threadIdx.x;
-  const uint64_t lo = g * chunk;
-  if (lo >= n) return;
-  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  if (g >= n) return;
+  const uint64_t T = (uint64_t)gridDim.x * kInvThreads;
   fe inv = fe_mul(wg_inv[blockIdx.x], others[g]);
-  for (uint64_t i = hi; i-- > lo;) {
+  for (uint64_t i = g + (n - 1 - g) / T * T;; i -= T) {  // this thread's elements, last first
     const fe x = fe_load(v + i);
     if (fe_is_zero(x)) {
       fe_store(out + i, fe_zero());
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(kInvThreads) void inv_down_kernel(const fe* __restr
       fe_store(out + i, OUT_CANON ? fe_mul(r, mc.rinv) : r);
       inv = fe_mul(inv, x);
     }
+    if (i < T) break;
   }
 }
 
