@@ -94,6 +94,24 @@ __device__ __forceinline__ fe fe_add(const fe& a, const fe& b) {
   return r;
 }
 
+// a + b without reduction (the caller bounds the sum below 2^256).
+__device__ __forceinline__ fe fe_add_raw(const fe& a, const fe& b) {
+  fe r = a;
+  asm("v_add_co_u32 %0, vcc, %0, %8\n\t"
+      "v_addc_co_u32 %1, vcc, %1, %9, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, %2, %10, vcc\n\t"
+      "v_addc_co_u32 %3, vcc, %3, %11, vcc\n\t"
+      "v_addc_co_u32 %4, vcc, %4, %12, vcc\n\t"
+      "v_addc_co_u32 %5, vcc, %5, %13, vcc\n\t"
+      "v_addc_co_u32 %6, vcc, %6, %14, vcc\n\t"
+      "v_addc_co_u32 %7, vcc, %7, %15, vcc"
+      : "+v"(r.w[0]), "+v"(r.w[1]), "+v"(r.w[2]), "+v"(r.w[3]), "+v"(r.w[4]), "+v"(r.w[5]), "+v"(r.w[6]),
+        "+v"(r.w[7])
+      : "v"(b.w[0]), "v"(b.w[1]), "v"(b.w[2]), "v"(b.w[3]), "v"(b.w[4]), "v"(b.w[5]), "v"(b.w[6]), "v"(b.w[7])
+      : "vcc");
+  return r;
+}
+
 __device__ __forceinline__ fe fe_sub(const fe& a, const fe& b) {
   fe r = a;
   uint64_t borrow;

@@ -27,6 +27,7 @@
 
 #include "internal.h"
 #include "blake2s.h"
+#include "fe_db.h"
 
 namespace stark {
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
@@ -79,6 +80,7 @@ __device__ __forceinline__ fe fe_from_u64(uint64_t v) {
 
 // Fiat-Shamir values derived on the device from the tree roots, so the proof
 // is enqueued end to end without waiting for the host.
+constexpr int kLincombConsts = 29;
 struct Transcript {
   fe r0;       // canonical r[0]
   fe r1_m;     // Montgomery r[1], r[2]
@@ -87,6 +89,8 @@ struct Transcript {
   fe kx_m[8][3];  // Montgomery k3 + k4 xs_t, k5 + k6 xs_t, k7 + k8 xs_t (t = i mod 8)
   uint32_t roots[3][8];  // a_root, m_root, l_root (LE words = the digest bytes)
   int err;
+  // Digit-basis tables (fe_db.h) of L's constants: k0, k1, k2, k9, k10, then kx[t][c] at 5 + 3 t + c.
+  uint32_t k_db[kLincombConsts][72];
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -101,6 +105,21 @@ __device__ __forceinline__ void b2s_short(const uint32_t* w, uint32_t extra_byte
   for (int i = 9; i < 16; ++i) m[i] = 0;
   b2s_init(out);
   b2s_compress(out, m, len, 0, true);
+}
+
+// The digit-basis table of a canonical constant c: limb j of c 2^(32 i) mod p at 9 i + j (two32_m = the
+// Montgomery image of 2^32, so fe_mul(c, two32_m) = c 2^32 mod p).
+__device__ void db_table_dev(fe c, const fe& two32_m, uint32_t* __restrict__ out) {
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int bit = 29 * j, w = bit >> 5, sh = bit & 31;
+      uint32_t v = c.w[w] >> sh;
+      if (sh > 3 && w < 7) v |= c.w[w + 1] << (32 - sh);
+      out[9 * i + j] = v & STARK_DB_M29;
+    }
+    c = fe_mul(c, two32_m);
+  }
 }
 
 // r = get_random_ff_values(a_root, precision, 3, 0) (utils.rs:272-290):
@@ -143,9 +162,10 @@ struct XsPowers {
 // Blake2s(m_root || i) mod p (prove.rs:274-283, utils.rs:25-27, 51-57); then the
 // three per-residue coefficients of L, kx[t] = (k3 + k4 xs_t, k5 + k6 xs_t,
 // k7 + k8 xs_t), so the L kernel needs 8 products per point instead of 14.
-__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, XsPowers xs,
+__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, XsPowers xs, fe two32_m,
                               Transcript* __restrict__ tr) {
   __shared__ fe ks[11];
+  __shared__ fe kx[8][3];
   const uint32_t i = threadIdx.x;
   if (i == 0) {
     ks[0] = one_m;
@@ -165,9 +185,20 @@ __global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one
   }
   __syncthreads();
   if (i < 8) {
-    tr->kx_m[i][0] = fe_add(ks[3], fe_mul(ks[4], xs.v[i]));
-    tr->kx_m[i][1] = fe_add(ks[5], fe_mul(ks[6], xs.v[i]));
-    tr->kx_m[i][2] = fe_add(ks[7], fe_mul(ks[8], xs.v[i]));
+    kx[i][0] = fe_add(ks[3], fe_mul(ks[4], xs.v[i]));
+    kx[i][1] = fe_add(ks[5], fe_mul(ks[6], xs.v[i]));
+    kx[i][2] = fe_add(ks[7], fe_mul(ks[8], xs.v[i]));
+    tr->kx_m[i][0] = kx[i][0];
+    tr->kx_m[i][1] = kx[i][1];
+    tr->kx_m[i][2] = kx[i][2];
+  }
+  __syncthreads();
+  if (i < kLincombConsts) {
+    static constexpr int kIdx[5] = {0, 1, 2, 9, 10};
+    const fe m = i < 5 ? ks[kIdx[i]] : kx[(i - 5) / 3][(i - 5) % 3];
+    fe unit = fe_zero();
+    unit.w[0] = 1;
+    db_table_dev(fe_mul(m, unit), two32_m, tr->k_db[i]);  // canonical constant (Montgomery image x R^-1)
   }
 }
 
@@ -433,6 +464,12 @@ struct LincombArgs {
 // L = k0 D1 + k1 D2 + k2 D3 + k3 P + k4 P x^steps + k5 B2 + k6 B2 x^steps +
 //     k7 B3 + k8 B3 x^steps + k9 A + k10 S (prove.rs:293-322).
 __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
+  // Every product is data x a constant of the proof: the digit-basis product (fe_db.h) from the
+  // transcript's tables, staged in LDS; the sum stays in [0, 2p) and is reduced once at the end.
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kLincombConsts * 72];
+  for (uint32_t k = threadIdx.x; k < kLincombConsts * 18; k += blockDim.x)
+    reinterpret_cast<uint4*>(tab)[k] = reinterpret_cast<const uint4*>(&a.tr->k_db[0][0])[k];
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.prec) return;
   const fe* row = a.rows + 8 * i;
@@ -440,16 +477,20 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
   const fe p = fe_load(row + 0), av = fe_load(row + 1), s = fe_load(row + 2), d1 = fe_load(row + 3),
            d2 = fe_load(row + 4), d3 = fe_load(row + 5), b2 = fe_load(row + 6), b3 = fe_load(row + 7);
   const uint32_t t = (uint32_t)(gi & 7);
-  const fe* k_m = a.tr->k_m;
-  const fe* kx = a.tr->kx_m[t];
-  fe acc = fe_mul(d1, k_m[0]);
-  acc = fe_add(acc, fe_mul(d2, k_m[1]));
-  acc = fe_add(acc, fe_mul(d3, k_m[2]));
-  acc = fe_add(acc, fe_mul(p, kx[0]));    // (k3 + k4 x^steps) P
-  acc = fe_add(acc, fe_mul(b2, kx[1]));   // (k5 + k6 x^steps) B2
-  acc = fe_add(acc, fe_mul(b3, kx[2]));   // (k7 + k8 x^steps) B3
-  acc = fe_add(acc, fe_mul(av, k_m[9]));
-  acc = fe_add(acc, fe_mul(s, k_m[10]));
+  auto T = [&](uint32_t c) { return static_cast<const uint32_t*>(__builtin_assume_aligned(tab + 72 * c, 16)); };
+  auto add = [](fe& acc, const fe& x) {  // acc, x in [0, 2p): acc + x < 4p < 2^256, back to [0, 2p)
+    acc = fe_add_raw(acc, x);
+    fe_csub2p(acc);
+  };
+  fe acc = fe_mul_db(d1, T(0));           // k0 D1
+  add(acc, fe_mul_db(d2, T(1)));          // k1 D2
+  add(acc, fe_mul_db(d3, T(2)));          // k2 D3
+  add(acc, fe_mul_db(p, T(5 + 3 * t)));   // (k3 + k4 x^steps) P
+  add(acc, fe_mul_db(b2, T(6 + 3 * t)));  // (k5 + k6 x^steps) B2
+  add(acc, fe_mul_db(b3, T(7 + 3 * t)));  // (k7 + k8 x^steps) B3
+  add(acc, fe_mul_db(av, T(3)));          // k9 A
+  add(acc, fe_mul_db(s, T(4)));           // k10 S
+  fe_reduce_once(acc);
   fe_store(a.out + i, acc);
 }
 
@@ -885,7 +926,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
       wt = F.mul(wt, w8);
     }
     hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(m_tree), mc.r2,
-                       mc.one, xs, d_tr);
+                       mc.one, xs, to_dev(F.from_u64((uint64_t)1 << 32)), d_tr);
     STARK_HIP(ctx, hipGetLastError());
   }
   LincombArgs la;
@@ -1442,7 +1483,8 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
   STARK_HIP(d.ctx, hipMemcpyAsync(d_root, m_root, 32, hipMemcpyHostToDevice, d.s));
   XsPowers xs;
   for (int t = 0; t < 8; ++t) xs.v[t] = d.xs_m[t];
-  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs, d.d_tr);
+  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs,
+                     to_dev(FieldHost::get().from_u64((uint64_t)1 << 32)), d.d_tr);
   STARK_HIP(d.ctx, hipGetLastError());
   LincombArgs la;
   la.rows = d.rows;
