@@ -89,7 +89,7 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 template <int LOG_R, int COL>
 struct DbPlan {
   static constexpr int mode = STARK_NTT_DB_MODE;
-  static constexpr bool on = mode != 0 && LOG_R >= 4 && (COL != 0 || STARK_NTT_DB_FIRST || mode == 2);
+  static constexpr bool on = mode != 0 && LOG_R >= 4 && LOG_R <= 8 && (COL != 0 || STARK_NTT_DB_FIRST || mode == 2);
   static constexpr int s_end = !on ? 0 : mode == 1 ? LOG_R - 2 : mode == 2 ? 3 : LOG_R;  // DB for steps s < s_end
   // the table holds w_R^(stride k), k < R / (2 stride)
   static constexpr uint32_t stride = mode == 1 ? 4 : mode == 2 ? (1u << LOG_R) / 16 : 1;

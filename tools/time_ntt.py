@@ -44,17 +44,17 @@ def main():
             step = lambda: lib.stark_merkle_update_dev(tree, d, n, 32, None)  # noqa: E731
         else:
             step = lambda: lib.stark_ntt_dev(ctx, d, log_n, 1, wp, 0, None)  # noqa: E731
-        for _ in range(3):
+        for _ in range(int(os.environ.get("WARM", "3"))):
             step()
         lib.stark_ctx_synchronize(ctx)
-        reps = 20
+        reps = int(os.environ.get("REPS", "20"))
         t0 = time.perf_counter()
         for _ in range(reps):
             step()
         lib.stark_ctx_synchronize(ctx)
         ms = (time.perf_counter() - t0) * 1000 / reps
         results[path] = ms
-        # Every build ran the same 23 in-place transforms of the same input: equal digests = equal outputs.
+        # Every build ran the same WARM + REPS in-place transforms of the same input: equal digests = equal outputs.
         lib.stark_memcpy_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         back = np.empty_like(host)
         lib.stark_memcpy_d2h(ctx, back.ctypes.data, d, n * 32)
