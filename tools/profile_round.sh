@@ -15,7 +15,7 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 B="$ROOT/bench.py --no-extras --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $B --steps 20 --warmup 3 > "$OUT/bench_stats.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 $B --steps 200 --warmup 10 > "$OUT/bench_stats.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B --steps 5 --warmup 1 > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B --steps 5 --warmup 1 > "$OUT/bench_write.log" 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/full" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/bench_full.log" 2>&1
