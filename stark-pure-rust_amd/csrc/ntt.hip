@@ -86,10 +86,20 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #ifndef STARK_NTT_DB_FIRST
 #define STARK_NTT_DB_FIRST 0
 #endif
+// Elements per workgroup tile (log2): 2^10 (B = 4 columns of 256, 256 threads, up to 4 workgroups per
+// CU) or, with STARK_NTT_TILE_LOG=12, 2^12 (B = 16, 1024 threads, one workgroup per CU whose 16 waves
+// share one copy of the constant tables).
+#ifndef STARK_NTT_TILE_LOG
+#define STARK_NTT_TILE_LOG 10
+#endif
+constexpr uint32_t kTileLog = STARK_NTT_TILE_LOG;
+constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
+
 template <int LOG_R, int COL>
 struct DbPlan {
   static constexpr int mode = STARK_NTT_DB_MODE;
-  static constexpr bool on = mode != 0 && LOG_R >= 4 && LOG_R <= 8 && (COL != 0 || STARK_NTT_DB_FIRST || mode == 2);
+  static constexpr bool on = mode != 0 && LOG_R >= 4 && LOG_R <= 8 &&
+                             (COL != 0 || STARK_NTT_DB_FIRST || mode == 2 || kTileLog > 10);
   static constexpr int s_end = !on ? 0 : mode == 1 ? LOG_R - 2 : mode == 2 ? 3 : LOG_R;  // DB for steps s < s_end
   // the table holds w_R^(stride k), k < R / (2 stride)
   static constexpr uint32_t stride = mode == 1 ? 4 : mode == 2 ? (1u << LOG_R) / 16 : 1;
@@ -98,11 +108,12 @@ struct DbPlan {
   static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
   static constexpr bool shoup_global = on && mode == 2;  // later steps' Shoup pairs from global memory
   static constexpr uint32_t shoup_fe = on && mode >= 2 ? 0 : (1u << LOG_R);  // staged Shoup pairs (R/2 roots)
-  static constexpr int occupancy = !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;  // workgroups per CU the LDS allows
+  // workgroups per CU the LDS allows
+  static constexpr int occupancy = kTileLog > 10 ? 1 : !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;
 };
 
 template <int LOG_R, bool PERSIST, int COL>
-__global__ __launch_bounds__(256, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
+__global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
                                                           const fe* __restrict__ small, const uint32_t* __restrict__ db,
                                                           fe scale, int do_scale,
@@ -431,8 +442,8 @@ PassPlan plan_passes(uint32_t log_n) {
 // Columns per workgroup (log2): 1024 elements (256 threads x 4) when the
 // transform has that many columns, so every global access is a run of
 // B*32 >= 128 contiguous bytes for R <= 256.
-uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r) {
-  uint32_t lb = log_r >= 10 ? 0 : 10 - log_r;
+uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r, uint32_t tile_log) {
+  uint32_t lb = log_r >= tile_log ? 0 : tile_log - log_r;
   if (lb > log_n - log_r) lb = log_n - log_r;
   return lb;
 }
@@ -693,7 +704,8 @@ extern "C" uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap
 
 namespace stark {
 
-uint32_t ntt_choose_log_b(uint32_t log_n, uint32_t log_r) { return choose_log_b_impl(log_n, log_r); }
+// (the radix-2^29 pass kernels keep 2^10-element tiles)
+uint32_t ntt_choose_log_b(uint32_t log_n, uint32_t log_r) { return choose_log_b_impl(log_n, log_r, 10); }
 
 uint32_t ntt_first_log_r(uint32_t log_n) { return log_n < 2 ? log_n : plan_passes(log_n).log_r[0]; }
 
@@ -749,7 +761,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
       if ((k & 1) != (lr & 1)) --k;
       sp = Sparse{k, zero_log, log_n - zero_log};
     }
-    const uint32_t lb = ntt_choose_log_b(log_n, lr);
+    const uint32_t lb = choose_log_b_impl(log_n, lr, kTileLog);
     const uint32_t elems = 1u << (lr + lb);
     const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
     const uint32_t log_tiles = log_n - lr - lb;
