@@ -112,6 +112,56 @@ struct DbPlan {
   static constexpr int occupancy = kTileLog > 10 ? 1 : !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;
 };
 
+// LDS data image of a pass, element index i = (row << log_b) + column.  STARK_NTT_XSPLIT=1 keeps the
+// two 16-B halves of each element in separate planes (lo at v[i], hi at v[n + i]), so the 16 lanes of a
+// ds_read_b128 group read 16 adjacent 16-B slots instead of every other one; STARK_NTT_XSWZ=1 also
+// XORs index bit 4 into bits 2 and 3 (a bijection), which spreads the radix-4 step s = 0's rows
+// (4q + k) over both halves of the 256-B bank window.
+#ifndef STARK_NTT_XSPLIT
+#define STARK_NTT_XSPLIT 1
+#endif
+#ifndef STARK_NTT_XSWZ
+#define STARK_NTT_XSWZ 0
+#endif
+// STARK_NTT_JJ_MAJOR=1: the radix-4 step s = 2 runs jj-major (see the pass kernel).
+#ifndef STARK_NTT_JJ_MAJOR
+#define STARK_NTT_JJ_MAJOR 1
+#endif
+struct XImage {
+  fe* base;
+  uint32_t n;  // elements
+  __device__ __forceinline__ static uint32_t swz(uint32_t i) {
+#if STARK_NTT_XSWZ
+    return i ^ (((i >> 4) & 1u) * 12u);
+#else
+    return i;
+#endif
+  }
+  __device__ __forceinline__ fe ld(uint32_t i) const {
+#if STARK_NTT_XSPLIT
+    const uint4* v = reinterpret_cast<const uint4*>(base);
+    i = swz(i);
+    const uint4 lo = v[i], hi = v[n + i];
+    fe r;
+    r.w[0] = lo.x; r.w[1] = lo.y; r.w[2] = lo.z; r.w[3] = lo.w;
+    r.w[4] = hi.x; r.w[5] = hi.y; r.w[6] = hi.z; r.w[7] = hi.w;
+    return r;
+#else
+    return base[swz(i)];
+#endif
+  }
+  __device__ __forceinline__ void st(uint32_t i, const fe& x) const {
+#if STARK_NTT_XSPLIT
+    uint4* v = reinterpret_cast<uint4*>(base);
+    i = swz(i);
+    v[i] = make_uint4(x.w[0], x.w[1], x.w[2], x.w[3]);
+    v[n + i] = make_uint4(x.w[4], x.w[5], x.w[6], x.w[7]);
+#else
+    base[swz(i)] = x;
+#endif
+  }
+};
+
 template <int LOG_R, bool PERSIST, int COL>
 __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
                                                           uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
@@ -125,6 +175,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   uint32_t* sdb = reinterpret_cast<uint32_t*>(lds + DB::shoup_fe);  // digit-basis tables (DbPlan)
   fe* X = lds + DB::shoup_fe + DB::lds_fe;  // [R][B] data image
   const uint32_t B = 1u << log_b;
+  const XImage XI{X, B << LOG_R};
   const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
   const uint32_t tid = threadIdx.x;
   const bool active = tid < nthr;
@@ -209,7 +260,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
-          X[(rr << log_b) + eb[t]] = v[t];
+          XI.st((rr << log_b) + eb[t], v[t]);
         }
       } else {
         // Rows >= live_rows are zero, so after sp.skip DIT stages every
@@ -218,7 +269,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         for (int t = 0; t < 4; ++t) {
           if (er[t] >= live_rows) continue;
           const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
-          for (uint32_t k = 0; k < (1u << sp.skip); ++k) X[((rr + k) << log_b) + eb[t]] = v[t];
+          for (uint32_t k = 0; k < (1u << sp.skip); ++k) XI.st(((rr + k) << log_b) + eb[t], v[t]);
         }
       }
     }
@@ -244,13 +295,12 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t g = q * 2 + h;
-          fe* xa = &X[((2 * g) << log_b) + b];
-          fe* xb = &X[((2 * g + 1) << log_b) + b];
-          fe a = *xa, c = *xb;
+          const uint32_t ia = ((2 * g) << log_b) + b, ib = ((2 * g + 1) << log_b) + b;
+          fe a = XI.ld(ia), c = XI.ld(ib);
           fe_csub2p(c);
           fe_bfly_lazy(a, c, c);
-          *xa = a;
-          *xb = c;
+          XI.st(ia, a);
+          XI.st(ib, c);
         }
       }
       __syncthreads();
@@ -261,10 +311,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       // branch-free, so no register shuffles at merge points).
       if (active) {
         const uint32_t base = q << 2;
-        fe x0 = X[(base << log_b) + b];
-        fe x1 = X[((base + 1) << log_b) + b];
-        fe x2 = X[((base + 2) << log_b) + b];
-        fe x3 = X[((base + 3) << log_b) + b];
+        fe x0 = XI.ld((base << log_b) + b);
+        fe x1 = XI.ld(((base + 1) << log_b) + b);
+        fe x2 = XI.ld(((base + 2) << log_b) + b);
+        fe x3 = XI.ld(((base + 3) << log_b) + b);
         fe_csub2p(x1);
         fe_csub2p(x3);
         fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
@@ -279,13 +329,75 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         fe_csub2p(x2);
         fe_bfly_lazy(x0, x2, x2);
         fe_bfly_lazy(x1, x3, t3);
-        X[(base << log_b) + b] = x0;
-        X[((base + 2) << log_b) + b] = x2;
-        X[((base + 1) << log_b) + b] = x1;
-        X[((base + 3) << log_b) + b] = x3;
+        XI.st((base << log_b) + b, x0);
+        XI.st(((base + 2) << log_b) + b, x2);
+        XI.st(((base + 1) << log_b) + b, x1);
+        XI.st(((base + 3) << log_b) + b, x3);
       }
       __syncthreads();
       s = 2;
+    }
+    if (STARK_NTT_JJ_MAJOR && !(LOG_R & 1) && LOG_R >= 6 && s == 2) {
+      // Radix-4 step s = 2 (m = 4) with a jj-major thread mapping: each quarter of the threads takes
+      // one jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products
+      // by w_8^0 = w_16^0 = 1 (branch uniform per wave; lane masking was measured slower).
+      if (active) {
+        const uint32_t lq = LOG_R + log_b - 4;  // log2(threads per jj)
+        const uint32_t jj = tid >> lq;
+        const uint32_t rest = tid & ((1u << lq) - 1);
+        const uint32_t i0 = ((((rest >> log_b) << 4) + jj) << log_b) + (rest & (B - 1));
+        const uint32_t st = 4u << log_b;  // m rows
+        fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
+        if (jj == 0) {
+          fe_csub2p(x1);
+          fe_csub2p(x3);
+          fe_bfly_lazy(x0, x1, x1);
+          fe_bfly_lazy(x2, x3, x3);
+          fe t3;
+          if (DB::on) {
+            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_16^4 = w_4^1
+          } else {
+            const fe* shp = DB::shoup_global ? small : sm;
+            const uint32_t ic = 2 * (1u << (LOG_R - 2));
+            t3 = shoup_b(x3, shp[ic], shp[ic + 1]);
+          }
+          fe_csub2p(x2);
+          fe_bfly_lazy(x0, x2, x2);
+          fe_bfly_lazy(x1, x3, t3);
+        } else if (DB::on && DB::s_end > 2) {
+          constexpr uint32_t S = DB::stride;
+          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 3)) / S);  // w_8^jj
+          const fe t1 = fe_mul_db(x1, wa);
+          fe t3 = fe_mul_db(x3, wa);
+          fe_bfly_lazy(x0, x1, t1);
+          fe_bfly_lazy(x2, x3, t3);
+          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 4)) / S));  // w_16^jj
+          t3 = fe_mul_db(x3, dbt(sdb, ((jj + 4) << (LOG_R - 4)) / S));   // w_16^(jj+4)
+          fe_bfly_lazy(x0, x2, t2);
+          fe_bfly_lazy(x1, x3, t3);
+        } else {
+          const fe* shp = DB::shoup_global ? small : sm;
+          fe t1, t3;
+          const uint32_t ia = 2 * (jj << (LOG_R - 3));
+          const fe ta = shp[ia], taq = shp[ia + 1];
+          shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
+          fe_bfly_lazy(x0, x1, t1);
+          fe_bfly_lazy(x2, x3, t3);
+          const uint32_t ic = 2 * ((jj + 4) << (LOG_R - 4));
+          const fe tc = shp[ic], tcq = shp[ic + 1];
+          const uint32_t ib = 2 * (jj << (LOG_R - 4));
+          const fe t2 = shoup_a(x2, shp[ib], shp[ib + 1]);
+          t3 = shoup_b(x3, tc, tcq);
+          fe_bfly_lazy(x0, x2, t2);
+          fe_bfly_lazy(x1, x3, t3);
+        }
+        XI.st(i0, x0);
+        XI.st(i0 + 2 * st, x2);
+        XI.st(i0 + st, x1);
+        XI.st(i0 + 3 * st, x3);
+      }
+      __syncthreads();
+      s = 4;
     }
     if (DB::on) {
 #pragma unroll 1
@@ -294,10 +406,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           const uint32_t m = 1u << s;
           const uint32_t jj = q & (m - 1);
           const uint32_t base = ((q >> s) << (s + 2)) + jj;
-          fe x0 = X[(base << log_b) + b];
-          fe x1 = X[((base + m) << log_b) + b];
-          fe x2 = X[((base + 2 * m) << log_b) + b];
-          fe x3 = X[((base + 3 * m) << log_b) + b];
+          fe x0 = XI.ld((base << log_b) + b);
+          fe x1 = XI.ld(((base + m) << log_b) + b);
+          fe x2 = XI.ld(((base + 2 * m) << log_b) + b);
+          fe x3 = XI.ld(((base + 3 * m) << log_b) + b);
           // exponents (in w_R units) jj R/2m, jj R/4m, (jj + m) R/4m: multiples of 4 before the last step
           constexpr uint32_t S = DB::stride;
           const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) / S);  // w_{2m}^jj
@@ -309,10 +421,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) / S));   // w_{4m}^(jj+m)
           fe_bfly_lazy(x0, x2, t2);
           fe_bfly_lazy(x1, x3, t3);
-          X[(base << log_b) + b] = x0;
-          X[((base + 2 * m) << log_b) + b] = x2;
-          X[((base + m) << log_b) + b] = x1;
-          X[((base + 3 * m) << log_b) + b] = x3;
+          XI.st((base << log_b) + b, x0);
+          XI.st(((base + 2 * m) << log_b) + b, x2);
+          XI.st(((base + m) << log_b) + b, x1);
+          XI.st(((base + 3 * m) << log_b) + b, x3);
         }
         __syncthreads();
       }
@@ -323,10 +435,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         const uint32_t m = 1u << s;
         const uint32_t jj = q & (m - 1);
         const uint32_t base = ((q >> s) << (s + 2)) + jj;
-        fe x0 = X[(base << log_b) + b];
-        fe x1 = X[((base + m) << log_b) + b];
-        fe x2 = X[((base + 2 * m) << log_b) + b];
-        fe x3 = X[((base + 3 * m) << log_b) + b];
+        fe x0 = XI.ld((base << log_b) + b);
+        fe x1 = XI.ld(((base + m) << log_b) + b);
+        fe x2 = XI.ld(((base + 2 * m) << log_b) + b);
+        fe x3 = XI.ld(((base + 3 * m) << log_b) + b);
         fe t1, t3;
         // Shoup pairs staged in LDS, or (DbPlan mode 2) read from the global table through L1
         const fe* shp = DB::shoup_global ? small : sm;
@@ -342,10 +454,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         t3 = shoup_b(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
-        X[(base << log_b) + b] = x0;
-        X[((base + 2 * m) << log_b) + b] = x2;
-        X[((base + m) << log_b) + b] = x1;
-        X[((base + 3 * m) << log_b) + b] = x3;
+        XI.st((base << log_b) + b, x0);
+        XI.st(((base + 2 * m) << log_b) + b, x2);
+        XI.st(((base + m) << log_b) + b, x1);
+        XI.st(((base + 3 * m) << log_b) + b, x3);
       }
       __syncthreads();
     }
@@ -359,7 +471,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         for (int t = 0; t < 4; ++t) {
           const size_t j = j0 + eb[t];
           const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
-          fe val = X[(er[t] << log_b) + eb[t]];
+          fe val = XI.ld((er[t] << log_b) + eb[t]);
           if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
           fe_store(dst + o, val);
@@ -373,7 +485,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           const uint32_t rem = o & ((1u << (log_ns + LOG_R)) - 1);
           const uint32_t r = rem >> log_ns;
           const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
-          fe val = X[(r << log_b) + bb];
+          fe val = XI.ld((r << log_b) + bb);
           if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
           fe_store(dst + (j0 << LOG_R) + o, val);
