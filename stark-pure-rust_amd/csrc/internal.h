@@ -170,7 +170,7 @@ void tw29_free(Tw29* t);
 
 // Merkle internals (merkle.hip).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream);
+                          hipStream_t stream, size_t plane_stride = 0);
 stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t);
 stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,

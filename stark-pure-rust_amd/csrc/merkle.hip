@@ -26,6 +26,7 @@ struct stark_merkle_tree {
   stark::DevBuf nodes;               // (2n - 1) * 32 B
   stark::DevBuf own_leaves;          // leaves copied from the host
   const uint8_t* d_leaves = nullptr; // leaves the proofs are read from
+  uint64_t plane_stride = 0;         // 0: contiguous leaves; else 32-B planes (merkle_build)
   bool built = false;
   bool has_root = false;             // set by gen_proofs (reference: root = H::default() before)
   uint8_t root[32];
@@ -90,6 +91,33 @@ __device__ __forceinline__ Digest hash_leaf(const uint8_t* __restrict__ p, uint3
   return d;
 }
 
+// Digest of a leaf stored as len / 32 planes: its bytes [32 c, 32 c + 32) sit at
+// base + c * stride + 32 * node (a column-major table whose rows are the leaves).  Every
+// lane of a wave reads 32 adjacent bytes of each plane, so the loads coalesce.
+__device__ __forceinline__ Digest hash_leaf_planes(const uint8_t* __restrict__ base, uint64_t node,
+                                                   uint64_t stride, uint32_t len) {
+  Digest d;
+  b2s_init(d.h);
+  const uint32_t planes = len / 32;
+  uint32_t m[16];
+  for (uint32_t c = 0; c < planes; c += 2) {
+    const uint4* q0 = reinterpret_cast<const uint4*>(base + c * stride + 32 * node);
+    uint4 x[4] = {q0[0], q0[1], make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (c + 1 < planes) {
+      const uint4* q1 = reinterpret_cast<const uint4*>(base + (c + 1) * stride + 32 * node);
+      x[2] = q1[0];
+      x[3] = q1[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      m[4 * i] = x[i].x; m[4 * i + 1] = x[i].y; m[4 * i + 2] = x[i].z; m[4 * i + 3] = x[i].w;
+    }
+    const bool last = c + 2 >= planes;
+    b2s_compress(d.h, m, last ? len : 32 * (c + 2), 0, last);
+  }
+  return d;
+}
+
 // A 32-byte leaf (one canonical field element): one final block whose words
 // 8..15 are compile-time zeros, so their message additions fold away.
 __device__ __forceinline__ Digest hash_leaf32(const uint8_t* __restrict__ p) {
@@ -146,14 +174,16 @@ __global__ __launch_bounds__(kMerkleThreads) void merkle_build_kernel(const uint
                                                                       uint32_t leaf_len,
                                                                       const Digest* __restrict__ below,
                                                                       uint64_t count, uint32_t block,
-                                                                      uint32_t extra, LevelPtrs out) {
+                                                                      uint32_t extra, LevelPtrs out,
+                                                                      uint64_t plane_stride) {
   __shared__ __attribute__((aligned(16))) Digest lds[kMerkleBlock];
   const uint64_t base = (uint64_t)blockIdx.x * block;
   const uint32_t here = (uint32_t)((count - base) < block ? (count - base) : block);
   if (leaves && !LEAF32) {
     for (uint32_t i = threadIdx.x; i < here; i += blockDim.x) {
       const uint64_t node = base + i;
-      const Digest d = hash_leaf(leaves + node * leaf_len, leaf_len);
+      const Digest d = plane_stride ? hash_leaf_planes(leaves, node, plane_stride, leaf_len)
+                                    : hash_leaf(leaves + node * leaf_len, leaf_len);
       store_digest(out.lv[0] + node, d);
       lds[i] = d;
     }
@@ -319,14 +349,21 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
 
 // Proof gather: for proof i (index idx[i]): the leaf bytes and the depth
 // siblings ((idx >> d) ^ 1 at level d), leaf -> root.
-__global__ void merkle_gather_kernel(const uint8_t* __restrict__ leaves, uint32_t leaf_len,
+// Byte b of leaf id: contiguous leaves, or 32-B planes plane_stride apart (merkle_build).
+__device__ __forceinline__ const uint8_t* leaf_byte(const uint8_t* leaves, uint64_t id, uint32_t leaf_len,
+                                                    uint64_t plane_stride, uint32_t b) {
+  return plane_stride ? leaves + (b >> 5) * plane_stride + 32 * id + (b & 31) : leaves + id * leaf_len + b;
+}
+
+__global__ void merkle_gather_kernel(const uint8_t* __restrict__ leaves, uint32_t leaf_len, uint64_t plane_stride,
                                      const Digest* __restrict__ nodes, uint64_t n, uint32_t depth,
                                      const uint64_t* __restrict__ idx, uint32_t k, uint8_t* __restrict__ leaf_out,
                                      Digest* __restrict__ node_out) {
   const uint32_t i = blockIdx.x;
   if (i >= k) return;
   const uint64_t id = idx[i];
-  for (uint32_t b = threadIdx.x; b < leaf_len; b += blockDim.x) leaf_out[(uint64_t)i * leaf_len + b] = leaves[id * leaf_len + b];
+  for (uint32_t b = threadIdx.x; b < leaf_len; b += blockDim.x)
+    leaf_out[(uint64_t)i * leaf_len + b] = *leaf_byte(leaves, id, leaf_len, plane_stride, b);
   uint64_t off = 0, width = n;
   for (uint32_t d = 0; d < depth; ++d) {
     if (threadIdx.x == d % blockDim.x) node_out[(uint64_t)i * depth + d] = nodes[off + ((id >> d) ^ 1)];
@@ -366,10 +403,15 @@ __global__ void merkle_interleave_kernel(const Digest* __restrict__ chunks, uint
 
 // Builds every level of the tree over d_leaves (n leaves of leaf_len bytes);
 // with d_leaves == nullptr level 0 (the leaf digests) is already in place.
+// plane_stride != 0: leaf i's bytes [32 c, 32 c + 32) are at d_leaves + c * plane_stride + 32 i
+// (leaf_len a multiple of 32, 16-B aligned planes).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream) {
+                          hipStream_t stream, size_t plane_stride) {
   if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
   if (leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
+  if (plane_stride && (!d_leaves || leaf_len == 0 || leaf_len % 32 || plane_stride % 16 || plane_stride < 32 * n ||
+                       (((uintptr_t)d_leaves) & 15)))
+    return STARK_ERR_BAD_ARG;
   uint32_t depth = 0;
   while (((size_t)1 << depth) < n) ++depth;
   stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
@@ -410,7 +452,7 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
       const bool leaf32 = leaf_mode && leaf_len == 32 && (((uintptr_t)d_leaves) & 15) == 0;
       hipLaunchKernelGGL(leaf32 ? merkle_build_kernel<true> : merkle_build_kernel<false>, dim3(grid),
                          dim3(kMerkleThreads), 0, stream, leaf_mode ? d_leaves : nullptr, (uint32_t)leaf_len, below,
-                         count, block, extra, lp);
+                         count, block, extra, lp, (uint64_t)plane_stride);
       STARK_HIP(ctx, hipGetLastError());
       level += extra;
       count >>= extra;
@@ -425,6 +467,7 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   t->leaf_len = leaf_len;
   t->depth = depth;
   t->d_leaves = have_level0 ? (const uint8_t*)nodes : d_leaves;
+  t->plane_stride = have_level0 ? 0 : plane_stride;
   t->built = true;
   return STARK_OK;
 }
@@ -462,7 +505,7 @@ stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* i
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t indices are uploaded as u64");
   STARK_HIP(ctx, hipMemcpyAsync(d_idx, indices, idx_bytes, hipMemcpyHostToDevice, stream));
   hipLaunchKernelGGL(merkle_gather_kernel, dim3((unsigned)k), dim3(64), 0, stream, t->d_leaves,
-                     (uint32_t)t->leaf_len, (const Digest*)t->nodes.ptr, (uint64_t)t->n, t->depth, d_idx,
+                     (uint32_t)t->leaf_len, (uint64_t)t->plane_stride, (const Digest*)t->nodes.ptr, (uint64_t)t->n, t->depth, d_idx,
                      (uint32_t)k, d_leaf, d_node);
   STARK_HIP(ctx, hipGetLastError());
   if (leaves_out) STARK_HIP(ctx, hipMemcpyAsync(leaves_out, d_leaf, leaf_bytes, hipMemcpyDeviceToHost, stream));
@@ -484,6 +527,7 @@ struct GatherDesc {
   const Digest* nodes;
   uint64_t n;        // leaves
   uint64_t out_off;  // byte offset of this request's region in the output
+  uint64_t plane_stride;
   uint32_t first;    // first proof (block) of this request
   uint32_t k, leaf_len, depth;
 };
@@ -506,7 +550,11 @@ __global__ __launch_bounds__(64) void merkle_gather_multi_kernel(GatherDescs g, 
   uint8_t* region = out + q.out_off;
   uint8_t* leaf_out = region + (uint64_t)i * q.leaf_len;
   const uint8_t* leaf_in = q.leaves + id * q.leaf_len;
-  if ((q.leaf_len & 3) == 0 && (((uintptr_t)leaf_in | (uintptr_t)leaf_out) & 3) == 0) {
+  if (q.plane_stride) {  // 32-B planes (4-B aligned: leaf_len and the planes are multiples of 16)
+    for (uint32_t w = threadIdx.x; w < q.leaf_len / 4; w += blockDim.x)
+      reinterpret_cast<uint32_t*>(leaf_out)[w] =
+          *reinterpret_cast<const uint32_t*>(leaf_byte(q.leaves, id, q.leaf_len, q.plane_stride, 4 * w));
+  } else if ((q.leaf_len & 3) == 0 && (((uintptr_t)leaf_in | (uintptr_t)leaf_out) & 3) == 0) {
     for (uint32_t w = threadIdx.x; w < q.leaf_len / 4; w += blockDim.x)
       reinterpret_cast<uint32_t*>(leaf_out)[w] = reinterpret_cast<const uint32_t*>(leaf_in)[w];
   } else {
@@ -561,6 +609,7 @@ stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& r
       d.nodes = (const Digest*)q.t->nodes.ptr;
       d.n = q.t->n;
       d.out_off = off[r];
+      d.plane_stride = q.t->plane_stride;
       d.first = proofs;
       d.k = (uint32_t)q.k;
       d.leaf_len = (uint32_t)q.t->leaf_len;

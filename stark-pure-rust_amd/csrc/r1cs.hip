@@ -366,7 +366,8 @@ struct ConstraintArgs {
   const fe* interp3;
   const fe* lo;          // g2 tables
   const fe* hi;
-  fe* rows;              // precision x 8 elements
+  fe* rows;              // precision x 8 elements: rows (plane = 0) or 8 columns of `plane` elements
+  uint64_t plane;
   int* err;
   uint64_t prec;            // points on this GPU (a power of two)
   uint64_t shift1, shift2;  // original_steps/3*skips, original_steps/3*2*skips (mod precision), in local points
@@ -441,19 +442,22 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
   const fe b2 = mc ? fe_mul(e2, izb2) : fe_mul(fe_mul(e2, a.mr2), izb2);
   const fe b3 = mc ? fe_mul(e3, izb3) : fe_mul(fe_mul(e3, a.mr2), izb3);
-  fe* row = a.rows + 8 * i;
-  fe_store(row + 0, p);
-  fe_store(row + 1, av);
-  fe_store(row + 2, s);
-  fe_store(row + 3, d1);
-  fe_store(row + 4, d2);
-  fe_store(row + 5, d3);
-  fe_store(row + 6, b2);
-  fe_store(row + 7, b3);
+  // Row i = P|A|S|D1|D2|D3|B2|B3: contiguous (256 B), or column c at rows + c * plane + i
+  const uint64_t cs = a.plane ? a.plane : 1;
+  fe* row = a.plane ? a.rows + i : a.rows + 8 * i;
+  fe_store(row + 0 * cs, p);
+  fe_store(row + 1 * cs, av);
+  fe_store(row + 2 * cs, s);
+  fe_store(row + 3 * cs, d1);
+  fe_store(row + 4 * cs, d2);
+  fe_store(row + 5 * cs, d3);
+  fe_store(row + 6 * cs, b2);
+  fe_store(row + 7 * cs, b3);
 }
 
 struct LincombArgs {
-  const fe* rows;
+  const fe* rows;        // the constraint kernel's rows (plane = 0) or columns (plane elements apart)
+  uint64_t plane;
   fe* out;
   uint64_t prec;
   uint64_t g_add;        // local point i is global point g_add + (i << log_g)
@@ -472,10 +476,12 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.prec) return;
-  const fe* row = a.rows + 8 * i;
+  const uint64_t cs = a.plane ? a.plane : 1;
+  const fe* row = a.plane ? a.rows + i : a.rows + 8 * i;
   const uint64_t gi = a.g_add + (i << a.log_g);
-  const fe p = fe_load(row + 0), av = fe_load(row + 1), s = fe_load(row + 2), d1 = fe_load(row + 3),
-           d2 = fe_load(row + 4), d3 = fe_load(row + 5), b2 = fe_load(row + 6), b3 = fe_load(row + 7);
+  const fe p = fe_load(row + 0 * cs), av = fe_load(row + 1 * cs), s = fe_load(row + 2 * cs),
+           d1 = fe_load(row + 3 * cs), d2 = fe_load(row + 4 * cs), d3 = fe_load(row + 5 * cs),
+           b2 = fe_load(row + 6 * cs), b3 = fe_load(row + 7 * cs);
   const uint32_t t = (uint32_t)(gi & 7);
   auto T = [&](uint32_t c) { return static_cast<const uint32_t*>(__builtin_assume_aligned(tab + 72 * c, 16)); };
   auto add = [](fe& acc, const fe& x) {  // acc, x in [0, 2p): acc + x < 4p < 2^256, back to [0, 2p)
@@ -898,6 +904,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.lo = tw2->d_lo;
   ca.hi = tw2->d_hi;
   ca.rows = rows;
+  ca.plane = prec;  // column-major: coalesced stores here and loads in the L kernel and the main tree
   ca.err = &d_tr->err;
   ca.prec = prec;
   ca.shift1 = (os / 3 * skips) % prec;
@@ -915,8 +922,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.mont_cols = pre ? 1 : 0;
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
-  // Main tree over the 256-B rows (prove.rs:261-264).
-  STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s));
+  // Main tree over the 256-B rows (prove.rs:261-264), read as 8 column planes.
+  STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s, prec * sizeof(fe)));
   {
     XsPowers xs;
     const HostFp w8 = F.pow_u64(g2, steps);
@@ -931,6 +938,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   LincombArgs la;
   la.rows = rows;
+  la.plane = prec;
   la.out = lvals;
   la.prec = prec;
   la.g_add = 0;
@@ -1292,6 +1300,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   ca.lo = tw2->d_lo;
   ca.hi = tw2->d_hi;
   ca.rows = d.rows;
+  ca.plane = 0;  // the distributed prover exports its rows (stark_dprove_rows)
   ca.err = &d.d_tr->err;
   ca.prec = P;
   ca.shift1 = ((os / 3 * skips) % prec) >> d.log_g;  // multiples of 8, hence of G
@@ -1488,6 +1497,7 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
   STARK_HIP(d.ctx, hipGetLastError());
   LincombArgs la;
   la.rows = d.rows;
+  la.plane = 0;
   la.out = d.lvals;
   la.prec = d.P;
   la.g_add = d.r;
