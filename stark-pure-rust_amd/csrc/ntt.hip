@@ -123,7 +123,8 @@ struct DbPlan {
 #ifndef STARK_NTT_XSWZ
 #define STARK_NTT_XSWZ 0
 #endif
-// STARK_NTT_JJ_MAJOR=1: the radix-4 step s = 2 runs jj-major (see the pass kernel).
+// STARK_NTT_JJ_MAJOR=1: the first radix-4 step with twiddles (s = 2, or s = 1 for an odd radix) runs
+// jj-major (see the pass kernel).
 #ifndef STARK_NTT_JJ_MAJOR
 #define STARK_NTT_JJ_MAJOR 1
 #endif
@@ -337,16 +338,19 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       __syncthreads();
       s = 2;
     }
-    if (STARK_NTT_JJ_MAJOR && !(LOG_R & 1) && LOG_R >= 6 && s == 2) {
-      // Radix-4 step s = 2 (m = 4) with a jj-major thread mapping: each quarter of the threads takes
-      // one jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products
-      // by w_8^0 = w_16^0 = 1 (branch uniform per wave; lane masking was measured slower).
+    // The first radix-4 step with twiddles (s0 = 2, m = 4 for an even radix; s0 = 1, m = 2 after the
+    // radix-2 stage of an odd one) with a jj-major thread mapping: each 1/m of the threads takes one
+    // jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products by
+    // w_{2m}^0 = w_{4m}^0 = 1 (3 of 4; branch uniform per wave; lane masking was measured slower,
+    // DESIGN §5): 3n/16 products per even pass, 3n/8 per odd one.
+    constexpr int kS0 = (LOG_R & 1) ? 1 : 2;
+    if (STARK_NTT_JJ_MAJOR && LOG_R >= 5 && s == kS0) {
       if (active) {
-        const uint32_t lq = LOG_R + log_b - 4;  // log2(threads per jj)
+        const uint32_t lq = LOG_R + log_b - 2 - kS0;  // log2(threads per jj)
         const uint32_t jj = tid >> lq;
         const uint32_t rest = tid & ((1u << lq) - 1);
-        const uint32_t i0 = ((((rest >> log_b) << 4) + jj) << log_b) + (rest & (B - 1));
-        const uint32_t st = 4u << log_b;  // m rows
+        const uint32_t i0 = ((((rest >> log_b) << (kS0 + 2)) + jj) << log_b) + (rest & (B - 1));
+        const uint32_t st = (1u << kS0) << log_b;  // m rows
         fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
         if (jj == 0) {
           fe_csub2p(x1);
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           fe_bfly_lazy(x2, x3, x3);
           fe t3;
           if (DB::on) {
-            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_16^4 = w_4^1
+            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_{4m}^m = w_4^1
           } else {
             const fe* shp = DB::shoup_global ? small : sm;
             const uint32_t ic = 2 * (1u << (LOG_R - 2));
@@ -364,28 +368,28 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           fe_csub2p(x2);
           fe_bfly_lazy(x0, x2, x2);
           fe_bfly_lazy(x1, x3, t3);
-        } else if (DB::on && DB::s_end > 2) {
+        } else if (DB::on && DB::s_end > kS0) {
           constexpr uint32_t S = DB::stride;
-          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 3)) / S);  // w_8^jj
+          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - kS0)) / S);  // w_{2m}^jj
           const fe t1 = fe_mul_db(x1, wa);
           fe t3 = fe_mul_db(x3, wa);
           fe_bfly_lazy(x0, x1, t1);
           fe_bfly_lazy(x2, x3, t3);
-          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 4)) / S));  // w_16^jj
-          t3 = fe_mul_db(x3, dbt(sdb, ((jj + 4) << (LOG_R - 4)) / S));   // w_16^(jj+4)
+          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - kS0)) / S));                // w_{4m}^jj
+          t3 = fe_mul_db(x3, dbt(sdb, ((jj + (1u << kS0)) << (LOG_R - 2 - kS0)) / S));  // w_{4m}^(jj+m)
           fe_bfly_lazy(x0, x2, t2);
           fe_bfly_lazy(x1, x3, t3);
         } else {
           const fe* shp = DB::shoup_global ? small : sm;
           fe t1, t3;
-          const uint32_t ia = 2 * (jj << (LOG_R - 3));
+          const uint32_t ia = 2 * (jj << (LOG_R - 1 - kS0));
           const fe ta = shp[ia], taq = shp[ia + 1];
           shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
           fe_bfly_lazy(x0, x1, t1);
           fe_bfly_lazy(x2, x3, t3);
-          const uint32_t ic = 2 * ((jj + 4) << (LOG_R - 4));
+          const uint32_t ic = 2 * ((jj + (1u << kS0)) << (LOG_R - 2 - kS0));
           const fe tc = shp[ic], tcq = shp[ic + 1];
-          const uint32_t ib = 2 * (jj << (LOG_R - 4));
+          const uint32_t ib = 2 * (jj << (LOG_R - 2 - kS0));
           const fe t2 = shoup_a(x2, shp[ib], shp[ib + 1]);
           t3 = shoup_b(x3, tc, tcq);
           fe_bfly_lazy(x0, x2, t2);
@@ -397,7 +401,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         XI.st(i0 + 3 * st, x3);
       }
       __syncthreads();
-      s = 4;
+      s = kS0 + 2;
     }
     if (DB::on) {
 #pragma unroll 1
