@@ -372,7 +372,7 @@ def ntt_products(log_n: int, plan: list) -> tuple:
     radix-2 stage 0 first; every pass after the first multiplies each element by its column twiddle,
     one product from a table (t16 when Ns R <= 2^l16, or the last pass's full table for 2^17..2^26)
     or two in the lo * hi form.  Returns (all products, digit-basis products): the radix-4 steps
-    before the last one of every pass after the first use the digit-basis product (ntt.hip DbPlan,
+    before the last one of every pass use the digit-basis product (ntt.hip DbPlan,
     radices 2^4..2^8).  Radices >= 2^5 run their first step with twiddles (s = 2 even, s = 1 odd)
     jj-major, and its jj = 0 butterflies (n/16 even, n/8 odd) skip the products by w^0 = 1 (three of
     their four; ntt.hip STARK_NTT_JJ_MAJOR)."""
@@ -386,9 +386,9 @@ def ntt_products(log_n: int, plan: list) -> tuple:
             steps = n * (r // 2 - 1) + n // 4
         skip = 0 if r < 5 else 3 * n // 8 if r % 2 else 3 * n // 16
         total += steps - skip
+        if 4 <= r <= 8:
+            db += steps - n - skip  # all but the last radix-4 step (every pass: ntt.hip STARK_NTT_DB_FIRST)
         if ns:
-            if 4 <= r <= 8:
-                db += steps - n - skip  # all but the last radix-4 step
             last = i == len(plan) - 1
             table = ns + r <= l16 or (last and log_n > l16 and 17 <= log_n <= 26)
             total += n * (1 if table else 2)

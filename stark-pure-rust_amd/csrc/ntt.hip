@@ -76,7 +76,7 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 //   0  none: Shoup pairs of all R/2 roots staged in LDS (40 KB with the data image, 4 workgroups/CU);
 //   1  (default) the steps before a pass's last one, in passes with a column twiddle: their constants
 //      are w_R^(4k), k < R/8 (32 for R = 256, 9 KB); the last step keeps the staged Shoup pairs
-//      (49 KB, 3 workgroups/CU).  The first pass stays Shoup-only unless STARK_NTT_DB_FIRST=1;
+//      (49 KB, 3 workgroups/CU).  STARK_NTT_DB_FIRST=1 (default) does the same in the first pass;
 //   2  the steps with m <= 4 in every pass (8 constants w_R^(16k), 2.3 KB); the later steps read
 //      their Shoup pairs from global memory (L1/L2), so nothing else is staged (34 KB, 4/CU);
 //   3  every step, a table of all R/2 constants (36 KB, 2/CU).
@@ -84,7 +84,7 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #define STARK_NTT_DB_MODE 1
 #endif
 #ifndef STARK_NTT_DB_FIRST
-#define STARK_NTT_DB_FIRST 0
+#define STARK_NTT_DB_FIRST 1
 #endif
 // Elements per workgroup tile (log2): 2^10 (B = 4 columns of 256, 256 threads, up to 4 workgroups per
 // CU) or, with STARK_NTT_TILE_LOG=12, 2^12 (B = 16, 1024 threads, one workgroup per CU whose 16 waves
