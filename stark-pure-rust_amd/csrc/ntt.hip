@@ -123,6 +123,10 @@ struct DbPlan {
 #ifndef STARK_NTT_XSWZ
 #define STARK_NTT_XSWZ 0
 #endif
+// STARK_NTT_FUSE_STORE=1: the last radix-4 step stores from registers (see the pass kernel).
+#ifndef STARK_NTT_FUSE_STORE
+#define STARK_NTT_FUSE_STORE 1
+#endif
 // STARK_NTT_JJ_MAJOR=1: the first radix-4 step with twiddles (s = 2, or s = 1 for an odd radix) runs
 // jj-major (see the pass kernel).
 #ifndef STARK_NTT_JJ_MAJOR
@@ -433,8 +437,15 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         __syncthreads();
       }
     }
+    // The last radix-4 step (m = R/4) leaves thread tid the rows q + k R/4 of column b: exactly the
+    // elements (er[k], eb[k]) it stores.  With the standard store it keeps them in registers (no LDS
+    // round trip and one barrier less per tile).
+    const bool fuse = STARK_NTT_FUSE_STORE && ((size_t)1 << log_ns) >= B;
+    bool kept = false;
+    fe yl[4];
 #pragma unroll 1
     for (; s < LOG_R; s += 2) {
+      const bool keep = fuse && s == LOG_R - 2;  // uniform
       if (active) {
         const uint32_t m = 1u << s;
         const uint32_t jj = q & (m - 1);
@@ -458,12 +469,20 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         t3 = shoup_b(x3, tc, tcq);
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
-        XI.st((base << log_b) + b, x0);
-        XI.st(((base + 2 * m) << log_b) + b, x2);
-        XI.st(((base + m) << log_b) + b, x1);
-        XI.st(((base + 3 * m) << log_b) + b, x3);
+        if (keep) {
+          yl[0] = x0;
+          yl[1] = x1;
+          yl[2] = x2;
+          yl[3] = x3;
+        } else {
+          XI.st((base << log_b) + b, x0);
+          XI.st(((base + 2 * m) << log_b) + b, x2);
+          XI.st(((base + m) << log_b) + b, x1);
+          XI.st(((base + 3 * m) << log_b) + b, x3);
+        }
       }
-      __syncthreads();
+      kept = keep;
+      if (!keep) __syncthreads();
     }
 
     // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
@@ -475,7 +494,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         for (int t = 0; t < 4; ++t) {
           const size_t j = j0 + eb[t];
           const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
-          fe val = XI.ld((er[t] << log_b) + eb[t]);
+          fe val = kept ? yl[t] : XI.ld((er[t] << log_b) + eb[t]);
           if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
           fe_store(dst + o, val);
