@@ -123,6 +123,12 @@ struct DbPlan {
 #ifndef STARK_NTT_XSWZ
 #define STARK_NTT_XSWZ 0
 #endif
+// STARK_NTT_FUSE_FIRST=1: the first butterfly step runs in registers on the loaded elements (each
+// thread loads the rows of its own first butterflies).  Measured slower at 2^23/2^24 (1.663-1.670 vs
+// 1.623-1.624 ms), faster only at 2^20: off.
+#ifndef STARK_NTT_FUSE_FIRST
+#define STARK_NTT_FUSE_FIRST 0
+#endif
 // STARK_NTT_FUSE_STORE=1: the last radix-4 step stores from registers (see the pass kernel).
 #ifndef STARK_NTT_FUSE_STORE
 #define STARK_NTT_FUSE_STORE 1
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           reinterpret_cast<const uint4*>(db)[(e * DB::stride) * 18 + (k - e * 18)];
     }
 
-  // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row).
+  // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row) as stored.
   uint32_t eb[4], er[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -208,6 +214,17 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   }
   const uint32_t b = tid & (B - 1);
   const uint32_t q = tid >> log_b;  // radix-4 group within the column
+  // Rows as loaded (el[t]).  With STARK_NTT_FUSE_FIRST the thread loads rows rev(q) + t R/4 (rev over
+  // LOG_R - 2 bits), whose bit-reversed positions are 4q + rev2(t): the inputs of its own first
+  // butterfly step, which it then computes in registers before the first LDS write.
+  const bool fuse_first = STARK_NTT_FUSE_FIRST && LOG_R >= 4 && LOG_R <= 8 && sp.skip == 0;  // 2^9: spills
+  uint32_t el[4];
+  {
+    const uint32_t rq = fuse_first ? (__builtin_bitreverse32(q) >> (34 - LOG_R)) : q;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) el[t] = rq + (uint32_t)t * (nthr >> log_b);
+  }
+  __syncthreads();  // the staged tables are read before the first barrier of the tile loop
 
   // Sparse first pass (sp.skip > 0): only rows < R >> sp.zero_log are
   // non-zero (read from a compact input of batch stride 2^sp.log_in), and the
@@ -220,7 +237,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     const fe* src = in + ((size_t)(tile >> log_tiles) << log_in) + ((size_t)(tile & tile_mask) << log_b);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
+      v[t] = el[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)el[t] << log_cols)) : fe_zero();
   }
 
   for (; tile < total_tiles; tile += gridDim.x) {
@@ -235,7 +252,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
+            tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + el[t]];
           // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
           // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
           mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
@@ -245,7 +262,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           const fe* e[4];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
+            const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * el[t]) & (((uint64_t)1 << lnr) - 1);
             e[t] = ct.t16 + 2 * (k << (ct.l16 - lnr));
           }
           shoup2(v[0], v[1], v[0], e[0][0], e[0][1], v[1], e[1][0], e[1][1]);
@@ -254,17 +271,47 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           const uint32_t unit = log_n - lnr;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) << unit;
+            const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * el[t]) << unit;
             tw[t] = fe_mul(ct.lo[ex & (((uint64_t)1 << ct.kb) - 1)], ct.hi[ex >> ct.kb]);
           }
           mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
           mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
         }
       }
-      if (sp.skip == 0) {
+      if (fuse_first) {
+        // v[t] sits at bit-reversed position 4q + rev2(t): the first step's inputs x0..x3
+        fe x0 = v[0], x1 = v[2], x2 = v[1], x3 = v[3];
+        if (LOG_R & 1) {  // radix-2 stage 0 (twiddles 1)
+          fe_csub2p(x1);
+          fe_bfly_lazy(x0, x1, x1);
+          fe_csub2p(x3);
+          fe_bfly_lazy(x2, x3, x3);
+        } else {  // radix-4 step s = 0 (as the peeled step below)
+          fe_csub2p(x1);
+          fe_csub2p(x3);
+          fe_bfly_lazy(x0, x1, x1);
+          fe_bfly_lazy(x2, x3, x3);
+          fe t3;
+          if (DB::on) {
+            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
+          } else {
+            const fe* shp = DB::shoup_global ? small : sm;
+            const uint32_t ic = 2 * (1u << (LOG_R - 2));
+            t3 = shoup_b(x3, shp[ic], shp[ic + 1]);
+          }
+          fe_csub2p(x2);
+          fe_bfly_lazy(x0, x2, x2);
+          fe_bfly_lazy(x1, x3, t3);
+        }
+        const uint32_t p0 = ((q << 2) << log_b) + b, st1 = 1u << log_b;
+        XI.st(p0, x0);
+        XI.st(p0 + st1, x1);
+        XI.st(p0 + 2 * st1, x2);
+        XI.st(p0 + 3 * st1, x3);
+      } else if (sp.skip == 0) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+          const uint32_t rr = __builtin_bitreverse32(el[t]) >> (32 - LOG_R);
           XI.st((rr << log_b) + eb[t], v[t]);
         }
       } else {
@@ -272,8 +319,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         // position of a group of 2^skip holds the group's one live input.
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          if (er[t] >= live_rows) continue;
-          const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+          if (el[t] >= live_rows) continue;
+          const uint32_t rr = __builtin_bitreverse32(el[t]) >> (32 - LOG_R);
           for (uint32_t k = 0; k < (1u << sp.skip); ++k) XI.st(((rr + k) << log_b) + eb[t], v[t]);
         }
       }
@@ -286,7 +333,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       const fe* src = in + ((size_t)(nt >> log_tiles) << log_in) + ((size_t)(nt & tile_mask) << log_b);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
+        v[t] = el[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)el[t] << log_cols)) : fe_zero();
     }
 
     // ---- R-point DIT over the bit-reversed image ----
@@ -294,8 +341,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     // left in [0, 2p) and each radix-2 butterfly reduces only its X input
     // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
     // it is the transform's last pass.
-    int s = (int)sp.skip;
-    if ((LOG_R & 1) && sp.skip == 0) {
+    int s = fuse_first ? ((LOG_R & 1) ? 1 : 2) : (int)sp.skip;
+    if ((LOG_R & 1) && sp.skip == 0 && !fuse_first) {
       if (active) {  // radix-2 stage 0: twiddles are all 1
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -440,7 +487,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     // The last radix-4 step (m = R/4) leaves thread tid the rows q + k R/4 of column b: exactly the
     // elements (er[k], eb[k]) it stores.  With the standard store it keeps them in registers (no LDS
     // round trip and one barrier less per tile).
-    const bool fuse = STARK_NTT_FUSE_STORE && ((size_t)1 << log_ns) >= B;
+    const bool fuse = STARK_NTT_FUSE_STORE && LOG_R <= 8 && ((size_t)1 << log_ns) >= B;  // 2^9: spills at 128 VGPRs
     bool kept = false;
     fe yl[4];
 #pragma unroll 1
