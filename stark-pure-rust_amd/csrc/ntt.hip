@@ -86,6 +86,10 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #ifndef STARK_NTT_DB_FIRST
 #define STARK_NTT_DB_FIRST 1
 #endif
+// STARK_NTT_DB_LAST: the last radix-4 step digit-basis too, for radices up to 2^STARK_NTT_DB_LAST (0 = off).
+#ifndef STARK_NTT_DB_LAST
+#define STARK_NTT_DB_LAST 7
+#endif
 // Elements per workgroup tile (log2): 2^10 (B = 4 columns of 256, 256 threads, up to 4 workgroups per
 // CU) or, with STARK_NTT_TILE_LOG=12, 2^12 (B = 16, 1024 threads, one workgroup per CU whose 16 waves
 // share one copy of the constant tables).
@@ -107,7 +111,12 @@ struct DbPlan {
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
   static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
   static constexpr bool shoup_global = on && mode == 2;  // later steps' Shoup pairs from global memory
-  static constexpr uint32_t shoup_fe = on && mode >= 2 ? 0 : (1u << LOG_R);  // staged Shoup pairs (R/2 roots)
+  // STARK_NTT_DB_LAST: in passes with a column twiddle the last step too is digit-basis, from a table of
+  // all R/2 constants staged per tile over the data image once the step has read its inputs
+  static constexpr bool last = LOG_R <= STARK_NTT_DB_LAST && on && mode == 1 && COL != 0;
+  static constexpr uint32_t full_entries = last ? (1u << LOG_R) / 2 : 0;
+  static constexpr uint32_t full_fe = full_entries * 9 + full_entries / 16;
+  static constexpr uint32_t shoup_fe = (on && mode >= 2) || last ? 0 : (1u << LOG_R);  // staged Shoup pairs
   // workgroups per CU the LDS allows
   static constexpr int occupancy = kTileLog > 10 ? 1 : !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;
 };
@@ -491,7 +500,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     bool kept = false;
     fe yl[4];
 #pragma unroll 1
-    for (; s < LOG_R; s += 2) {
+    for (; s < (DB::last ? LOG_R - 2 : LOG_R); s += 2) {
       const bool keep = fuse && s == LOG_R - 2;  // uniform
       if (active) {
         const uint32_t m = 1u << s;
@@ -530,6 +539,53 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       }
       kept = keep;
       if (!keep) __syncthreads();
+    }
+    if (DB::last) {
+      // Last step (s = LOG_R - 2, m = R/4: thread q owns rows q + k m of column b) by the digit basis:
+      // read the inputs, then stage the R/2 constants over the data image (L2-resident table).
+      const uint32_t m = 1u << (LOG_R - 2);
+      const uint32_t i0 = (q << log_b) + b, st = m << log_b;
+      fe x0, x1, x2, x3;
+      if (active) {
+        x0 = XI.ld(i0);
+        x1 = XI.ld(i0 + st);
+        x2 = XI.ld(i0 + 2 * st);
+        x3 = XI.ld(i0 + 3 * st);
+      }
+      __syncthreads();
+      uint32_t* ft = reinterpret_cast<uint32_t*>(X);
+      for (uint32_t k = tid; k < DB::full_entries * 18; k += blockDim.x) {
+        const uint32_t e = k / 18;
+        reinterpret_cast<uint4*>(ft)[k + (e >> 3)] = reinterpret_cast<const uint4*>(db)[k];
+      }
+      __syncthreads();
+      if (active) {
+        const uint32_t jj = q;
+        const uint32_t* wa = dbt(ft, 2 * jj);  // w_{2m}^jj = w_R^(2 jj)
+        const fe t1 = fe_mul_db(x1, wa);
+        fe t3 = fe_mul_db(x3, wa);
+        fe_bfly_lazy(x0, x1, t1);
+        fe_bfly_lazy(x2, x3, t3);
+        const fe t2 = fe_mul_db(x2, dbt(ft, jj));  // w_{4m}^jj
+        t3 = fe_mul_db(x3, dbt(ft, jj + m));       // w_{4m}^(jj+m)
+        fe_bfly_lazy(x0, x2, t2);
+        fe_bfly_lazy(x1, x3, t3);
+        yl[0] = x0;
+        yl[1] = x1;
+        yl[2] = x2;
+        yl[3] = x3;
+      }
+      kept = fuse;
+      if (!fuse) {  // the store reads the image: write it back once the table is no longer read
+        __syncthreads();
+        if (active) {
+          XI.st(i0, yl[0]);
+          XI.st(i0 + st, yl[1]);
+          XI.st(i0 + 2 * st, yl[2]);
+          XI.st(i0 + 3 * st, yl[3]);
+        }
+        __syncthreads();
+      }
     }
 
     // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
@@ -632,6 +688,27 @@ uint32_t choose_log_b_impl(uint32_t log_n, uint32_t log_r, uint32_t tile_log) {
 
 typedef void (*pass_fn)(const fe*, fe*, uint32_t, uint32_t, uint32_t, ColTw, const fe*, const uint32_t*, fe, int,
                         uint32_t, uint32_t, Sparse);
+
+// Minimum data-image size of a pass instance (in fe): the last-step table is staged over it.
+template <int COL>
+size_t db_full_fe_c(uint32_t log_r) {
+  switch (log_r) {
+    case 4: return DbPlan<4, COL>::full_fe;
+    case 5: return DbPlan<5, COL>::full_fe;
+    case 6: return DbPlan<6, COL>::full_fe;
+    case 7: return DbPlan<7, COL>::full_fe;
+    case 8: return DbPlan<8, COL>::full_fe;
+    default: return 0;
+  }
+}
+size_t db_full_fe(uint32_t log_r, int col) {
+  switch (col) {
+    case kColNone: return db_full_fe_c<kColNone>(log_r);
+    case kColFull: return db_full_fe_c<kColFull>(log_r);
+    case kColT16: return db_full_fe_c<kColT16>(log_r);
+    default: return db_full_fe_c<kColTwoLevel>(log_r);
+  }
+}
 
 // LDS of a pass instance beyond its data image: staged Shoup pairs + digit-basis tables (in fe).
 template <int COL>
@@ -959,7 +1036,8 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
     const int col = log_ns == 0 ? kColNone : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
     // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
-    const size_t lds = ((size_t)elems + db_lds_fe(lr, col)) * sizeof(fe);
+    const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
+    const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
     const uint64_t persistent_grid = 256 * (uint64_t)pass_occupancy(lr, col);
     const bool persist = kPersistent && total > persistent_grid;
     const unsigned grid = (unsigned)(persist ? persistent_grid : total);
