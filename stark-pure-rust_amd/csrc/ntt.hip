@@ -86,6 +86,10 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #ifndef STARK_NTT_DB_FIRST
 #define STARK_NTT_DB_FIRST 1
 #endif
+// STARK_NTT_SMALL_LAST=1: a plan's smaller radices go last instead of first.
+#ifndef STARK_NTT_SMALL_LAST
+#define STARK_NTT_SMALL_LAST 0
+#endif
 // STARK_NTT_DB_LAST: the last radix-4 step digit-basis too, for radices up to 2^STARK_NTT_DB_LAST (0 = off).
 #ifndef STARK_NTT_DB_LAST
 #define STARK_NTT_DB_LAST 7
@@ -673,7 +677,8 @@ PassPlan plan_passes(uint32_t log_n) {
   const uint32_t cap = max_log_r(log_n);
   p.n_pass = (int)((log_n + cap - 1) / cap);
   const uint32_t base = log_n / p.n_pass, extra = log_n % p.n_pass;
-  for (int i = 0; i < p.n_pass; ++i) p.log_r[i] = base + ((uint32_t)(p.n_pass - 1 - i) < extra ? 1 : 0);
+  for (int i = 0; i < p.n_pass; ++i)
+    p.log_r[i] = base + ((uint32_t)(STARK_NTT_SMALL_LAST ? i : p.n_pass - 1 - i) < extra ? 1 : 0);
   return p;
 }
 
