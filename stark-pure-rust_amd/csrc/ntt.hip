@@ -662,7 +662,10 @@ constexpr uint32_t kMaxLogR = 9;  // largest radix with a kernel instance and sm
 // Radix cap of a size: 2^8 up to 2^24 (three passes of 256 at the headline size); 2^9 from 2^25 on,
 // so 2^25 and 2^26 take three passes, not four (2^26: 13.25 n products instead of 14.5 n, with the
 // column-twiddle table of 2^18 entries below).
-inline uint32_t max_log_r(uint32_t log_n) { return log_n >= 25 ? 9 : 8; }
+// Radix 2^9 passes (three passes instead of four) at 2^25 and from 2^27 on.  At 2^26 the four
+// digit-basis passes (6, 6, 7, 7) beat (8, 9, 9): 7.56 vs 7.73 ms; at 2^25 (8, 8, 9) beats
+// (6, 6, 6, 7): 3.49-3.51 vs 3.55-3.56 ms.
+inline uint32_t max_log_r(uint32_t log_n) { return (log_n == 25 || log_n >= 27) ? 9 : 8; }
 // Workgroups of a persistent pass: 256 CUs x the resident 256-thread groups its LDS allows.
 #ifndef STARK_NTT_PERSISTENT
 #define STARK_NTT_PERSISTENT 0
