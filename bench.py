@@ -388,8 +388,8 @@ def ntt_products(log_n: int, plan: list) -> tuple:
         total += steps - skip
         if 4 <= r <= 8:
             db += steps - n - skip  # all but the last radix-4 step (every pass: ntt.hip STARK_NTT_DB_FIRST)
-            if ns and r <= 7:
-                db += n  # the last step too, from the table staged per tile (ntt.hip STARK_NTT_DB_LAST)
+            if r <= 7:
+                db += n  # the last step too, from the table staged per tile (ntt.hip STARK_NTT_DB_LAST[_FIRST])
         if ns:
             last = i == len(plan) - 1
             table = ns + r <= l16 or (last and log_n > l16 and 17 <= log_n <= 26)

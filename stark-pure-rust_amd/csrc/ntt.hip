@@ -94,6 +94,10 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 #ifndef STARK_NTT_DB_LAST
 #define STARK_NTT_DB_LAST 7
 #endif
+// STARK_NTT_DB_LAST_FIRST=1: the same in the first pass (its store reads the image back: two more barriers).
+#ifndef STARK_NTT_DB_LAST_FIRST
+#define STARK_NTT_DB_LAST_FIRST 1
+#endif
 // Elements per workgroup tile (log2): 2^10 (B = 4 columns of 256, 256 threads, up to 4 workgroups per
 // CU) or, with STARK_NTT_TILE_LOG=12, 2^12 (B = 16, 1024 threads, one workgroup per CU whose 16 waves
 // share one copy of the constant tables).
@@ -117,7 +121,7 @@ struct DbPlan {
   static constexpr bool shoup_global = on && mode == 2;  // later steps' Shoup pairs from global memory
   // STARK_NTT_DB_LAST: in passes with a column twiddle the last step too is digit-basis, from a table of
   // all R/2 constants staged per tile over the data image once the step has read its inputs
-  static constexpr bool last = LOG_R <= STARK_NTT_DB_LAST && on && mode == 1 && COL != 0;
+  static constexpr bool last = LOG_R <= STARK_NTT_DB_LAST && on && mode == 1 && (COL != 0 || STARK_NTT_DB_LAST_FIRST);
   static constexpr uint32_t full_entries = last ? (1u << LOG_R) / 2 : 0;
   static constexpr uint32_t full_fe = full_entries * 9 + full_entries / 16;
   static constexpr uint32_t shoup_fe = (on && mode >= 2) || last ? 0 : (1u << LOG_R);  // staged Shoup pairs
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       kept = keep;
       if (!keep) __syncthreads();
     }
-    if (DB::last) {
+    if (DB::last && s == LOG_R - 2) {  // (a sparse first pass whose copy stages cover all of R has none)
       // Last step (s = LOG_R - 2, m = R/4: thread q owns rows q + k m of column b) by the digit basis:
       // read the inputs, then stage the R/2 constants over the data image (L2-resident table).
       const uint32_t m = 1u << (LOG_R - 2);
