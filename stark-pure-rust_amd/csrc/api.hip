@@ -236,7 +236,6 @@ void stark_ctx_destroy(stark_ctx* ctx) {
     if (kv.second->d_lo) hipFree(kv.second->d_lo);
     if (kv.second->d_full) hipFree(kv.second->d_full);
     if (kv.second->d_full_s) hipFree(kv.second->d_full_s);
-    tw29_free(kv.second->t29);
   }
   for (stark_merkle_tree*& t : ctx->trees) {
     stark_merkle_free(t);
@@ -246,7 +245,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (void* p : ctx->pinned)
     if (p) hipHostFree(p);
   ctx->fri_trees.clear();
-  for (DevBuf* b : {&ctx->scratch, &ctx->scratch2, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);

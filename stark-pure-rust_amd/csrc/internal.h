@@ -59,8 +59,6 @@ struct DevBuf {
 //   lo[i] = w^i                   i < 2^kb
 //   hi[i] = w^(i * 2^kb)          i < 2^(log_n - kb)
 //   small_off[l] = offset (in fe) into `small` of the Shoup pairs of w_R^k = w^(k * n / R), k < R/2, R = 2^l
-struct Tw29;
-
 struct Twiddles {
   uint32_t log_n = 0, kb = 0;
   fe* d_lo = nullptr;
@@ -82,7 +80,6 @@ struct Twiddles {
   // radix-4 steps (ntt.hip DbPlan).  db_off[l] = offset in u32 into d_db (72 u32 per root).
   uint32_t* d_db = nullptr;
   uint32_t db_off[16] = {0};
-  Tw29* t29 = nullptr;    // radix-2^29 images of these tables (ntt29.hip), built on first use
   HostFp root;      // the root these tables were built for (Montgomery)
   HostFp inv_n;     // n^-1 (Montgomery)
 };
@@ -94,7 +91,6 @@ struct stark_ctx {
   hipStream_t stream = nullptr;
   std::string last_error;
   stark::DevBuf scratch;   // NTT ping-pong partner
-  stark::DevBuf scratch2;  // second plane-format NTT buffer (ntt29.hip)
   stark::DevBuf io;        // staging for host-buffer entry points
   stark::DevBuf io2;
   stark::DevBuf fri_cols;    // folded FRI columns (prove_low_degree)
@@ -159,14 +155,6 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
 struct Sparse {
   uint32_t skip, zero_log, log_in;
 };
-uint32_t ntt_choose_log_b(uint32_t log_n, uint32_t log_r);  // columns per workgroup (log2)
-bool ntt_full_table_enabled();                               // STARK_NTT_FULL_TW != 0
-// The radix-2^29 pass kernels (ntt29.hip), selected by STARK_NTT29=1 (default: ntt.hip's radix-2^32).
-bool ntt29_enabled();
-stark_status ntt29_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
-                               uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream,
-                               const uint32_t* plan_log_r, int n_pass);
-void tw29_free(Tw29* t);
 
 // Merkle internals (merkle.hip).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,

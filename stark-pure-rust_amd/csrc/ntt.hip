@@ -31,33 +31,19 @@ struct ColTw {
   uint32_t l16, kb;
 };
 
-// One Stockham pass (see the file comment), persistent: each workgroup walks
-// tiles (B adjacent columns x R points) with stride gridDim.x and prefetches
-// the next tile's 4 elements per thread into registers while it computes the
-// current one, so HBM traffic overlaps the modular arithmetic.
-// T = B*R/4 threads, each owning exactly 4 elements in every phase.
+// One Stockham pass (see the file comment): each workgroup transforms one tile of B adjacent
+// columns x R points.  T = B*R/4 threads, each owning exactly 4 elements in every phase.
 
-// Two independent lazy products: interleaved in one asm block (fe_mul_lazy2) unless
-// STARK_NTT_DUAL=0 (A/B switch, tools/build_variant.sh).
-#ifndef STARK_NTT_DUAL
-#define STARK_NTT_DUAL 1
-#endif
-// Shoup products stay one chain per block: the interleaved pair (fe_mul_shoup2 in the r02
-// experiment) measured 1.867 vs 1.843 ms per 2^24 transform.
-__device__ __forceinline__ fe shoup_a(const fe& a, const fe& w, const fe& wq) { return fe_mul_shoup(a, w, wq); }
-__device__ __forceinline__ fe shoup_b(const fe& a, const fe& w, const fe& wq) { return fe_mul_shoup(a, w, wq); }
+// Two independent Montgomery products interleaved in one asm block (the full-table and two-level
+// column twiddles).  Shoup products stay one chain per block: the interleaved pair measured 1.867 vs
+// 1.843 ms per 2^24 transform.
 __device__ __forceinline__ void shoup2(fe& r, fe& s, const fe& a, const fe& w, const fe& wq, const fe& c,
                                        const fe& x, const fe& xq) {
-  r = shoup_a(a, w, wq);
-  s = shoup_b(c, x, xq);
+  r = fe_mul_shoup(a, w, wq);
+  s = fe_mul_shoup(c, x, xq);
 }
 __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, const fe& c, const fe& d) {
-#if STARK_NTT_DUAL
   fe_mul_lazy2(r, s, a, b, c, d);
-#else
-  r = fe_mul_lazy(a, b);
-  s = fe_mul_lazy(c, d);
-#endif
 }
 
 // The digit-basis table of constant k in LDS: 72 u32 per constant, 16-B aligned.  Constants 8 apart
@@ -72,130 +58,60 @@ __device__ __forceinline__ const uint32_t* dbt(const uint32_t* sdb, uint32_t k) 
 // kColTwoLevel: lo * hi, Montgomery).
 enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
 
-// Which radix-4 steps multiply by the digit-basis product (fe_db.h), STARK_NTT_DB_MODE:
-//   0  none: Shoup pairs of all R/2 roots staged in LDS (40 KB with the data image, 4 workgroups/CU);
-//   1  (default) the steps before a pass's last one, in passes with a column twiddle: their constants
-//      are w_R^(4k), k < R/8 (32 for R = 256, 9 KB); the last step keeps the staged Shoup pairs
-//      (49 KB, 3 workgroups/CU).  STARK_NTT_DB_FIRST=1 (default) does the same in the first pass;
-//   2  the steps with m <= 4 in every pass (8 constants w_R^(16k), 2.3 KB); the later steps read
-//      their Shoup pairs from global memory (L1/L2), so nothing else is staged (34 KB, 4/CU);
-//   3  every step, a table of all R/2 constants (36 KB, 2/CU).
-#ifndef STARK_NTT_DB_MODE
-#define STARK_NTT_DB_MODE 1
-#endif
-#ifndef STARK_NTT_DB_FIRST
-#define STARK_NTT_DB_FIRST 1
-#endif
-// STARK_NTT_SMALL_LAST=1: a plan's smaller radices go last instead of first.
-#ifndef STARK_NTT_SMALL_LAST
-#define STARK_NTT_SMALL_LAST 0
-#endif
-// STARK_NTT_DB_LAST: the last radix-4 step digit-basis too, for radices up to 2^STARK_NTT_DB_LAST (0 = off).
-#ifndef STARK_NTT_DB_LAST
-#define STARK_NTT_DB_LAST 7
-#endif
-// STARK_NTT_DB_LAST_FIRST=1: the same in the first pass (its store reads the image back: two more barriers).
-#ifndef STARK_NTT_DB_LAST_FIRST
-#define STARK_NTT_DB_LAST_FIRST 1
-#endif
-// Elements per workgroup tile (log2): 2^10 (B = 4 columns of 256, 256 threads, up to 4 workgroups per
-// CU) or, with STARK_NTT_TILE_LOG=12, 2^12 (B = 16, 1024 threads, one workgroup per CU whose 16 waves
-// share one copy of the constant tables).
-#ifndef STARK_NTT_TILE_LOG
-#define STARK_NTT_TILE_LOG 10
-#endif
-constexpr uint32_t kTileLog = STARK_NTT_TILE_LOG;
+// Elements per workgroup tile: 2^10 (B = 1024 / R columns, 256 threads).  4096- and 2048-element
+// tiles measured slower (one or two workgroups per CU leave the barriers uncovered).
+constexpr uint32_t kTileLog = 10;
 constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
 
+// Which radix-4 steps multiply by the digit-basis product (fe_db.h), radices 2^4..2^8:
+//   * every step before the pass's last one: constants w_R^(4k), k < R/8 (32 for R = 256, 9 KB of
+//     LDS, staged once per workgroup);
+//   * the last step too for radices <= 2^7: once the step has read its inputs, all R/2 constants
+//     (L2-resident, <= 18 KB) are staged over the data image (two more barriers per tile).  For R = 2^8
+//     (36 KB) that measured slower, so its last step multiplies by Shoup pairs staged in LDS (8 KB).
+// (Measured and dropped, DESIGN.md section 5: no digit basis, the R/2-constant table resident (2
+// workgroups per CU), the m <= 4 steps only with global Shoup pairs, the tables read through L1.)
 template <int LOG_R, int COL>
 struct DbPlan {
-  static constexpr int mode = STARK_NTT_DB_MODE;
-  static constexpr bool on = mode != 0 && LOG_R >= 4 && LOG_R <= 8 &&
-                             (COL != 0 || STARK_NTT_DB_FIRST || mode == 2 || kTileLog > 10);
-  static constexpr int s_end = !on ? 0 : mode == 1 ? LOG_R - 2 : mode == 2 ? 3 : LOG_R;  // DB for steps s < s_end
-  // the table holds w_R^(stride k), k < R / (2 stride)
-  static constexpr uint32_t stride = mode == 1 ? 4 : mode == 2 ? (1u << LOG_R) / 16 : 1;
+  static constexpr bool on = LOG_R >= 4 && LOG_R <= 8;
+  static constexpr int s_end = on ? LOG_R - 2 : 0;  // DB for steps s < s_end
+  static constexpr uint32_t stride = 4;             // the table holds w_R^(4 k), k < R / 8
   static constexpr uint32_t entries = on ? (1u << LOG_R) / (2 * stride) : 0;
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
   static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
-  static constexpr bool shoup_global = on && mode == 2;  // later steps' Shoup pairs from global memory
-  // STARK_NTT_DB_LAST: in passes with a column twiddle the last step too is digit-basis, from a table of
-  // all R/2 constants staged per tile over the data image once the step has read its inputs
-  static constexpr bool last = LOG_R <= STARK_NTT_DB_LAST && on && mode == 1 && (COL != 0 || STARK_NTT_DB_LAST_FIRST);
+  static constexpr bool last = on && LOG_R <= 7;
   static constexpr uint32_t full_entries = last ? (1u << LOG_R) / 2 : 0;
   static constexpr uint32_t full_fe = full_entries * 9 + full_entries / 16;
-  static constexpr uint32_t shoup_fe = (on && mode >= 2) || last ? 0 : (1u << LOG_R);  // staged Shoup pairs
-  // workgroups per CU the LDS allows
-  static constexpr int occupancy = kTileLog > 10 ? 1 : !on ? 4 : mode == 1 ? 3 : mode == 2 ? 4 : 2;
+  static constexpr uint32_t shoup_fe = last ? 0 : (1u << LOG_R);  // staged Shoup pairs of the last step
+  static constexpr int occupancy = on ? 3 : 4;                     // workgroups per CU the LDS allows
 };
 
-// LDS data image of a pass, element index i = (row << log_b) + column.  STARK_NTT_XSPLIT=1 keeps the
-// two 16-B halves of each element in separate planes (lo at v[i], hi at v[n + i]), so the 16 lanes of a
-// ds_read_b128 group read 16 adjacent 16-B slots instead of every other one; STARK_NTT_XSWZ=1 also
-// XORs index bit 4 into bits 2 and 3 (a bijection), which spreads the radix-4 step s = 0's rows
-// (4q + k) over both halves of the 256-B bank window.
-#ifndef STARK_NTT_XSPLIT
-#define STARK_NTT_XSPLIT 1
-#endif
-#ifndef STARK_NTT_XSWZ
-#define STARK_NTT_XSWZ 0
-#endif
-// STARK_NTT_FUSE_FIRST=1: the first butterfly step runs in registers on the loaded elements (each
-// thread loads the rows of its own first butterflies).  Measured slower at 2^23/2^24 (1.663-1.670 vs
-// 1.623-1.624 ms), faster only at 2^20: off.
-#ifndef STARK_NTT_FUSE_FIRST
-#define STARK_NTT_FUSE_FIRST 0
-#endif
-// STARK_NTT_FUSE_STORE=1: the last radix-4 step stores from registers (see the pass kernel).
-#ifndef STARK_NTT_FUSE_STORE
-#define STARK_NTT_FUSE_STORE 1
-#endif
-// STARK_NTT_JJ_MAJOR=1: the first radix-4 step with twiddles (s = 2, or s = 1 for an odd radix) runs
-// jj-major (see the pass kernel).
-#ifndef STARK_NTT_JJ_MAJOR
-#define STARK_NTT_JJ_MAJOR 1
-#endif
+// LDS data image of a pass, element index i = (row << log_b) + column.  The two 16-B halves of each
+// element sit in separate planes (lo at v[i], hi at v[n + i]), so the 16 lanes of a ds_read_b128 group
+// read 16 adjacent 16-B slots instead of every other one.
 struct XImage {
   fe* base;
   uint32_t n;  // elements
-  __device__ __forceinline__ static uint32_t swz(uint32_t i) {
-#if STARK_NTT_XSWZ
-    return i ^ (((i >> 4) & 1u) * 12u);
-#else
-    return i;
-#endif
-  }
   __device__ __forceinline__ fe ld(uint32_t i) const {
-#if STARK_NTT_XSPLIT
     const uint4* v = reinterpret_cast<const uint4*>(base);
-    i = swz(i);
     const uint4 lo = v[i], hi = v[n + i];
     fe r;
     r.w[0] = lo.x; r.w[1] = lo.y; r.w[2] = lo.z; r.w[3] = lo.w;
     r.w[4] = hi.x; r.w[5] = hi.y; r.w[6] = hi.z; r.w[7] = hi.w;
     return r;
-#else
-    return base[swz(i)];
-#endif
   }
   __device__ __forceinline__ void st(uint32_t i, const fe& x) const {
-#if STARK_NTT_XSPLIT
     uint4* v = reinterpret_cast<uint4*>(base);
-    i = swz(i);
     v[i] = make_uint4(x.w[0], x.w[1], x.w[2], x.w[3]);
     v[n + i] = make_uint4(x.w[4], x.w[5], x.w[6], x.w[7]);
-#else
-    base[swz(i)] = x;
-#endif
   }
 };
 
-template <int LOG_R, bool PERSIST, int COL>
-__global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(const fe* __restrict__ in, fe* __restrict__ out,
-                                                          uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
-                                                          const fe* __restrict__ small, const uint32_t* __restrict__ db,
-                                                          fe scale, int do_scale,
-                                                          uint32_t log_tiles, uint32_t total_tiles, Sparse sp) {
+template <int LOG_R, int COL>
+__global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(
+    const fe* __restrict__ in, fe* __restrict__ out, uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
+    const fe* __restrict__ small, const uint32_t* __restrict__ db, fe scale, int do_scale, uint32_t log_tiles,
+    uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
   using DB = DbPlan<LOG_R, COL>;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
@@ -210,6 +126,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   const uint32_t log_cols = log_n - LOG_R;
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
   const uint32_t tile_mask = (1u << log_tiles) - 1;
+  const uint32_t tile = blockIdx.x;
+  if (tile >= total_tiles) return;  // (uniform per workgroup)
 
   if (DB::shoup_fe)
     for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
@@ -221,7 +139,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           reinterpret_cast<const uint4*>(db)[(e * DB::stride) * 18 + (k - e * 18)];
     }
 
-  // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row) as stored.
+  // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row) as stored and loaded.
   uint32_t eb[4], er[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -231,285 +149,193 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   }
   const uint32_t b = tid & (B - 1);
   const uint32_t q = tid >> log_b;  // radix-4 group within the column
-  // Rows as loaded (el[t]).  With STARK_NTT_FUSE_FIRST the thread loads rows rev(q) + t R/4 (rev over
-  // LOG_R - 2 bits), whose bit-reversed positions are 4q + rev2(t): the inputs of its own first
-  // butterfly step, which it then computes in registers before the first LDS write.
-  const bool fuse_first = STARK_NTT_FUSE_FIRST && LOG_R >= 4 && LOG_R <= 8 && sp.skip == 0;  // 2^9: spills
-  uint32_t el[4];
-  {
-    const uint32_t rq = fuse_first ? (__builtin_bitreverse32(q) >> (34 - LOG_R)) : q;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) el[t] = rq + (uint32_t)t * (nthr >> log_b);
-  }
-  __syncthreads();  // the staged tables are read before the first barrier of the tile loop
 
   // Sparse first pass (sp.skip > 0): only rows < R >> sp.zero_log are
   // non-zero (read from a compact input of batch stride 2^sp.log_in), and the
   // first sp.skip radix-2 stages are copies; rows < R >> sp.skip are loaded.
   const uint32_t live_rows = R >> sp.skip, nz_rows = R >> sp.zero_log;
   const uint32_t log_in = sp.zero_log ? sp.log_in : log_n;
-  uint32_t tile = blockIdx.x;
   fe v[4];
-  if (active && tile < total_tiles) {
+  if (active) {
     const fe* src = in + ((size_t)(tile >> log_tiles) << log_in) + ((size_t)(tile & tile_mask) << log_b);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      v[t] = el[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)el[t] << log_cols)) : fe_zero();
+      v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
   }
+  const size_t boff = (size_t)(tile >> log_tiles) << log_n;
+  const size_t j0 = (size_t)(tile & tile_mask) << log_b;
 
-  for (; tile < total_tiles; tile += gridDim.x) {
-    const size_t boff = (size_t)(tile >> log_tiles) << log_n;
-    const size_t j0 = (size_t)(tile & tile_mask) << log_b;
-
-    // ---- column twiddle, scatter into the bit-reversed LDS image ----
-    if (active) {
-      if (COL != kColNone) {
-        const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
-        fe tw[4];
-        if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
+  // ---- column twiddle, scatter into the bit-reversed LDS image ----
+  if (active) {
+    if (COL != kColNone) {
+      const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
+      fe tw[4];
+      if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + el[t]];
-          // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
-          // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
-          mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
-          mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
-        } else if (COL == kColT16) {
-          // Shoup pairs from the L2-resident t16 table: v < 2^256 -> [0, 2p)
-          const fe* e[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * el[t]) & (((uint64_t)1 << lnr) - 1);
-            e[t] = ct.t16 + 2 * (k << (ct.l16 - lnr));
-          }
-          shoup2(v[0], v[1], v[0], e[0][0], e[0][1], v[1], e[1][0], e[1][1]);
-          shoup2(v[2], v[3], v[2], e[2][0], e[2][1], v[3], e[3][0], e[3][1]);
-        } else {
-          const uint32_t unit = log_n - lnr;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * el[t]) << unit;
-            tw[t] = fe_mul(ct.lo[ex & (((uint64_t)1 << ct.kb) - 1)], ct.hi[ex >> ct.kb]);
-          }
-          mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
-          mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
-        }
-      }
-      if (fuse_first) {
-        // v[t] sits at bit-reversed position 4q + rev2(t): the first step's inputs x0..x3
-        fe x0 = v[0], x1 = v[2], x2 = v[1], x3 = v[3];
-        if (LOG_R & 1) {  // radix-2 stage 0 (twiddles 1)
-          fe_csub2p(x1);
-          fe_bfly_lazy(x0, x1, x1);
-          fe_csub2p(x3);
-          fe_bfly_lazy(x2, x3, x3);
-        } else {  // radix-4 step s = 0 (as the peeled step below)
-          fe_csub2p(x1);
-          fe_csub2p(x3);
-          fe_bfly_lazy(x0, x1, x1);
-          fe_bfly_lazy(x2, x3, x3);
-          fe t3;
-          if (DB::on) {
-            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
-          } else {
-            const fe* shp = DB::shoup_global ? small : sm;
-            const uint32_t ic = 2 * (1u << (LOG_R - 2));
-            t3 = shoup_b(x3, shp[ic], shp[ic + 1]);
-          }
-          fe_csub2p(x2);
-          fe_bfly_lazy(x0, x2, x2);
-          fe_bfly_lazy(x1, x3, t3);
-        }
-        const uint32_t p0 = ((q << 2) << log_b) + b, st1 = 1u << log_b;
-        XI.st(p0, x0);
-        XI.st(p0 + st1, x1);
-        XI.st(p0 + 2 * st1, x2);
-        XI.st(p0 + 3 * st1, x3);
-      } else if (sp.skip == 0) {
+        for (int t = 0; t < 4; ++t) tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
+        // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
+        // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
+        mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
+        mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
+      } else if (COL == kColT16) {
+        // Shoup pairs from the L2-resident t16 table: v < 2^256 -> [0, 2p)
+        const fe* e[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const uint32_t rr = __builtin_bitreverse32(el[t]) >> (32 - LOG_R);
-          XI.st((rr << log_b) + eb[t], v[t]);
+          const uint64_t k = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) & (((uint64_t)1 << lnr) - 1);
+          e[t] = ct.t16 + 2 * (k << (ct.l16 - lnr));
         }
+        shoup2(v[0], v[1], v[0], e[0][0], e[0][1], v[1], e[1][0], e[1][1]);
+        shoup2(v[2], v[3], v[2], e[2][0], e[2][1], v[3], e[3][0], e[3][1]);
       } else {
-        // Rows >= live_rows are zero, so after sp.skip DIT stages every
-        // position of a group of 2^skip holds the group's one live input.
+        const uint32_t unit = log_n - lnr;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          if (el[t] >= live_rows) continue;
-          const uint32_t rr = __builtin_bitreverse32(el[t]) >> (32 - LOG_R);
-          for (uint32_t k = 0; k < (1u << sp.skip); ++k) XI.st(((rr + k) << log_b) + eb[t], v[t]);
+          const uint64_t ex = ((uint64_t)((j0 + eb[t]) & ns_mask) * er[t]) << unit;
+          tw[t] = fe_mul(ct.lo[ex & (((uint64_t)1 << ct.kb) - 1)], ct.hi[ex >> ct.kb]);
         }
+        mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
+        mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
+      }
+    }
+    if (sp.skip == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+        XI.st((rr << log_b) + eb[t], v[t]);
+      }
+    } else {
+      // Rows >= live_rows are zero, so after sp.skip DIT stages every
+      // position of a group of 2^skip holds the group's one live input.
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (er[t] >= live_rows) continue;
+        const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
+        for (uint32_t k = 0; k < (1u << sp.skip); ++k) XI.st(((rr + k) << log_b) + eb[t], v[t]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- R-point DIT over the bit-reversed image ----
+  // Lazy representation: every value in LDS is in [0, 4p); products are
+  // left in [0, 2p) and each radix-2 butterfly reduces only its X input
+  // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
+  // it is the transform's last pass.
+  int s = (int)sp.skip;
+  if ((LOG_R & 1) && sp.skip == 0) {
+    if (active) {  // radix-2 stage 0: twiddles are all 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t g = q * 2 + h;
+        const uint32_t ia = ((2 * g) << log_b) + b, ib = ((2 * g + 1) << log_b) + b;
+        fe a = XI.ld(ia), c = XI.ld(ib);
+        fe_csub2p(c);
+        fe_bfly_lazy(a, c, c);
+        XI.st(ia, a);
+        XI.st(ib, c);
       }
     }
     __syncthreads();
-
-    // ---- prefetch the next tile while this one is transformed ----
-    const uint32_t nt = tile + gridDim.x;
-    if (PERSIST && active && nt < total_tiles) {
-      const fe* src = in + ((size_t)(nt >> log_tiles) << log_in) + ((size_t)(nt & tile_mask) << log_b);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        v[t] = el[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)el[t] << log_cols)) : fe_zero();
-    }
-
-    // ---- R-point DIT over the bit-reversed image ----
-    // Lazy representation: every value in LDS is in [0, 4p); products are
-    // left in [0, 2p) and each radix-2 butterfly reduces only its X input
-    // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
-    // it is the transform's last pass.
-    int s = fuse_first ? ((LOG_R & 1) ? 1 : 2) : (int)sp.skip;
-    if ((LOG_R & 1) && sp.skip == 0 && !fuse_first) {
-      if (active) {  // radix-2 stage 0: twiddles are all 1
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t g = q * 2 + h;
-          const uint32_t ia = ((2 * g) << log_b) + b, ib = ((2 * g + 1) << log_b) + b;
-          fe a = XI.ld(ia), c = XI.ld(ib);
-          fe_csub2p(c);
-          fe_bfly_lazy(a, c, c);
-          XI.st(ia, a);
-          XI.st(ib, c);
-        }
+    s = 1;
+  }
+  if (s == 0) {
+    // Radix-4 step s = 0 (peeled: its twiddles are 1 except w_4^1, and the loop below stays
+    // branch-free, so no register shuffles at merge points).
+    if (active) {
+      const uint32_t base = q << 2;
+      fe x0 = XI.ld((base << log_b) + b);
+      fe x1 = XI.ld(((base + 1) << log_b) + b);
+      fe x2 = XI.ld(((base + 2) << log_b) + b);
+      fe x3 = XI.ld(((base + 3) << log_b) + b);
+      fe_csub2p(x1);
+      fe_csub2p(x3);
+      fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
+      fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
+      fe t3;
+      if (DB::on) {
+        t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
+      } else {
+        const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
+        t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
       }
-      __syncthreads();
-      s = 1;
+      fe_csub2p(x2);
+      fe_bfly_lazy(x0, x2, x2);
+      fe_bfly_lazy(x1, x3, t3);
+      XI.st((base << log_b) + b, x0);
+      XI.st(((base + 2) << log_b) + b, x2);
+      XI.st(((base + 1) << log_b) + b, x1);
+      XI.st(((base + 3) << log_b) + b, x3);
     }
-    if (s == 0) {
-      // Radix-4 step s = 0 (peeled: its twiddles are 1 except w_4^1, and the loop below stays
-      // branch-free, so no register shuffles at merge points).
-      if (active) {
-        const uint32_t base = q << 2;
-        fe x0 = XI.ld((base << log_b) + b);
-        fe x1 = XI.ld(((base + 1) << log_b) + b);
-        fe x2 = XI.ld(((base + 2) << log_b) + b);
-        fe x3 = XI.ld(((base + 3) << log_b) + b);
+    __syncthreads();
+    s = 2;
+  }
+  // The first radix-4 step with twiddles (s0 = 2, m = 4 for an even radix; s0 = 1, m = 2 after the
+  // radix-2 stage of an odd one) with a jj-major thread mapping: each 1/m of the threads takes one
+  // jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products by
+  // w_{2m}^0 = w_{4m}^0 = 1 (3 of 4; branch uniform per wave; lane masking was measured slower,
+  // DESIGN section 5): 3n/16 products per even pass, 3n/8 per odd one.
+  constexpr int kS0 = (LOG_R & 1) ? 1 : 2;
+  if (LOG_R >= 5 && s == kS0) {
+    if (active) {
+      const uint32_t lq = LOG_R + log_b - 2 - kS0;  // log2(threads per jj)
+      const uint32_t jj = tid >> lq;
+      const uint32_t rest = tid & ((1u << lq) - 1);
+      const uint32_t i0 = ((((rest >> log_b) << (kS0 + 2)) + jj) << log_b) + (rest & (B - 1));
+      const uint32_t st = (1u << kS0) << log_b;  // m rows
+      fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
+      if (jj == 0) {
         fe_csub2p(x1);
         fe_csub2p(x3);
-        fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
-        fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
+        fe_bfly_lazy(x0, x1, x1);
+        fe_bfly_lazy(x2, x3, x3);
         fe t3;
         if (DB::on) {
-          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
+          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_{4m}^m = w_4^1
         } else {
-          const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
-          t3 = shoup_b(x3, sm[ic], sm[ic + 1]);
+          const uint32_t ic = 2 * (1u << (LOG_R - 2));
+          t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
         }
         fe_csub2p(x2);
         fe_bfly_lazy(x0, x2, x2);
         fe_bfly_lazy(x1, x3, t3);
-        XI.st((base << log_b) + b, x0);
-        XI.st(((base + 2) << log_b) + b, x2);
-        XI.st(((base + 1) << log_b) + b, x1);
-        XI.st(((base + 3) << log_b) + b, x3);
+      } else if (DB::on && DB::s_end > kS0) {
+        constexpr uint32_t S = DB::stride;
+        const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - kS0)) / S);  // w_{2m}^jj
+        const fe t1 = fe_mul_db(x1, wa);
+        fe t3 = fe_mul_db(x3, wa);
+        fe_bfly_lazy(x0, x1, t1);
+        fe_bfly_lazy(x2, x3, t3);
+        const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - kS0)) / S));                // w_{4m}^jj
+        t3 = fe_mul_db(x3, dbt(sdb, ((jj + (1u << kS0)) << (LOG_R - 2 - kS0)) / S));  // w_{4m}^(jj+m)
+        fe_bfly_lazy(x0, x2, t2);
+        fe_bfly_lazy(x1, x3, t3);
+      } else {
+        fe t1, t3;
+        const uint32_t ia = 2 * (jj << (LOG_R - 1 - kS0));
+        const fe ta = sm[ia], taq = sm[ia + 1];
+        shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
+        fe_bfly_lazy(x0, x1, t1);
+        fe_bfly_lazy(x2, x3, t3);
+        const uint32_t ic = 2 * ((jj + (1u << kS0)) << (LOG_R - 2 - kS0));
+        const fe tc = sm[ic], tcq = sm[ic + 1];
+        const uint32_t ib = 2 * (jj << (LOG_R - 2 - kS0));
+        const fe t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
+        t3 = fe_mul_shoup(x3, tc, tcq);
+        fe_bfly_lazy(x0, x2, t2);
+        fe_bfly_lazy(x1, x3, t3);
       }
-      __syncthreads();
-      s = 2;
+      XI.st(i0, x0);
+      XI.st(i0 + 2 * st, x2);
+      XI.st(i0 + st, x1);
+      XI.st(i0 + 3 * st, x3);
     }
-    // The first radix-4 step with twiddles (s0 = 2, m = 4 for an even radix; s0 = 1, m = 2 after the
-    // radix-2 stage of an odd one) with a jj-major thread mapping: each 1/m of the threads takes one
-    // jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products by
-    // w_{2m}^0 = w_{4m}^0 = 1 (3 of 4; branch uniform per wave; lane masking was measured slower,
-    // DESIGN §5): 3n/16 products per even pass, 3n/8 per odd one.
-    constexpr int kS0 = (LOG_R & 1) ? 1 : 2;
-    if (STARK_NTT_JJ_MAJOR && LOG_R >= 5 && s == kS0) {
-      if (active) {
-        const uint32_t lq = LOG_R + log_b - 2 - kS0;  // log2(threads per jj)
-        const uint32_t jj = tid >> lq;
-        const uint32_t rest = tid & ((1u << lq) - 1);
-        const uint32_t i0 = ((((rest >> log_b) << (kS0 + 2)) + jj) << log_b) + (rest & (B - 1));
-        const uint32_t st = (1u << kS0) << log_b;  // m rows
-        fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
-        if (jj == 0) {
-          fe_csub2p(x1);
-          fe_csub2p(x3);
-          fe_bfly_lazy(x0, x1, x1);
-          fe_bfly_lazy(x2, x3, x3);
-          fe t3;
-          if (DB::on) {
-            t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_{4m}^m = w_4^1
-          } else {
-            const fe* shp = DB::shoup_global ? small : sm;
-            const uint32_t ic = 2 * (1u << (LOG_R - 2));
-            t3 = shoup_b(x3, shp[ic], shp[ic + 1]);
-          }
-          fe_csub2p(x2);
-          fe_bfly_lazy(x0, x2, x2);
-          fe_bfly_lazy(x1, x3, t3);
-        } else if (DB::on && DB::s_end > kS0) {
-          constexpr uint32_t S = DB::stride;
-          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - kS0)) / S);  // w_{2m}^jj
-          const fe t1 = fe_mul_db(x1, wa);
-          fe t3 = fe_mul_db(x3, wa);
-          fe_bfly_lazy(x0, x1, t1);
-          fe_bfly_lazy(x2, x3, t3);
-          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - kS0)) / S));                // w_{4m}^jj
-          t3 = fe_mul_db(x3, dbt(sdb, ((jj + (1u << kS0)) << (LOG_R - 2 - kS0)) / S));  // w_{4m}^(jj+m)
-          fe_bfly_lazy(x0, x2, t2);
-          fe_bfly_lazy(x1, x3, t3);
-        } else {
-          const fe* shp = DB::shoup_global ? small : sm;
-          fe t1, t3;
-          const uint32_t ia = 2 * (jj << (LOG_R - 1 - kS0));
-          const fe ta = shp[ia], taq = shp[ia + 1];
-          shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
-          fe_bfly_lazy(x0, x1, t1);
-          fe_bfly_lazy(x2, x3, t3);
-          const uint32_t ic = 2 * ((jj + (1u << kS0)) << (LOG_R - 2 - kS0));
-          const fe tc = shp[ic], tcq = shp[ic + 1];
-          const uint32_t ib = 2 * (jj << (LOG_R - 2 - kS0));
-          const fe t2 = shoup_a(x2, shp[ib], shp[ib + 1]);
-          t3 = shoup_b(x3, tc, tcq);
-          fe_bfly_lazy(x0, x2, t2);
-          fe_bfly_lazy(x1, x3, t3);
-        }
-        XI.st(i0, x0);
-        XI.st(i0 + 2 * st, x2);
-        XI.st(i0 + st, x1);
-        XI.st(i0 + 3 * st, x3);
-      }
-      __syncthreads();
-      s = kS0 + 2;
-    }
-    if (DB::on) {
+    __syncthreads();
+    s = kS0 + 2;
+  }
+  if (DB::on) {
 #pragma unroll 1
-      for (; s < DB::s_end; s += 2) {
-        if (active) {
-          const uint32_t m = 1u << s;
-          const uint32_t jj = q & (m - 1);
-          const uint32_t base = ((q >> s) << (s + 2)) + jj;
-          fe x0 = XI.ld((base << log_b) + b);
-          fe x1 = XI.ld(((base + m) << log_b) + b);
-          fe x2 = XI.ld(((base + 2 * m) << log_b) + b);
-          fe x3 = XI.ld(((base + 3 * m) << log_b) + b);
-          // exponents (in w_R units) jj R/2m, jj R/4m, (jj + m) R/4m: multiples of 4 before the last step
-          constexpr uint32_t S = DB::stride;
-          const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) / S);  // w_{2m}^jj
-          const fe t1 = fe_mul_db(x1, wa);
-          fe t3 = fe_mul_db(x3, wa);
-          fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
-          fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
-          const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) / S));  // w_{4m}^jj
-          t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) / S));   // w_{4m}^(jj+m)
-          fe_bfly_lazy(x0, x2, t2);
-          fe_bfly_lazy(x1, x3, t3);
-          XI.st((base << log_b) + b, x0);
-          XI.st(((base + 2 * m) << log_b) + b, x2);
-          XI.st(((base + m) << log_b) + b, x1);
-          XI.st(((base + 3 * m) << log_b) + b, x3);
-        }
-        __syncthreads();
-      }
-    }
-    // The last radix-4 step (m = R/4) leaves thread tid the rows q + k R/4 of column b: exactly the
-    // elements (er[k], eb[k]) it stores.  With the standard store it keeps them in registers (no LDS
-    // round trip and one barrier less per tile).
-    const bool fuse = STARK_NTT_FUSE_STORE && LOG_R <= 8 && ((size_t)1 << log_ns) >= B;  // 2^9: spills at 128 VGPRs
-    bool kept = false;
-    fe yl[4];
-#pragma unroll 1
-    for (; s < (DB::last ? LOG_R - 2 : LOG_R); s += 2) {
-      const bool keep = fuse && s == LOG_R - 2;  // uniform
+    for (; s < DB::s_end; s += 2) {
       if (active) {
         const uint32_t m = 1u << s;
         const uint32_t jj = q & (m - 1);
@@ -518,116 +344,147 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         fe x1 = XI.ld(((base + m) << log_b) + b);
         fe x2 = XI.ld(((base + 2 * m) << log_b) + b);
         fe x3 = XI.ld(((base + 3 * m) << log_b) + b);
-        fe t1, t3;
-        // Shoup pairs staged in LDS, or (DbPlan mode 2) read from the global table through L1
-        const fe* shp = DB::shoup_global ? small : sm;
-        const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj
-        const fe ta = shp[ia], taq = shp[ia + 1];
-        shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
-        fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
-        fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
-        const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
-        const fe tc = shp[ic], tcq = shp[ic + 1];
-        const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
-        const fe t2 = shoup_a(x2, shp[ib], shp[ib + 1]);
-        t3 = shoup_b(x3, tc, tcq);
-        fe_bfly_lazy(x0, x2, t2);
-        fe_bfly_lazy(x1, x3, t3);
-        if (keep) {
-          yl[0] = x0;
-          yl[1] = x1;
-          yl[2] = x2;
-          yl[3] = x3;
-        } else {
-          XI.st((base << log_b) + b, x0);
-          XI.st(((base + 2 * m) << log_b) + b, x2);
-          XI.st(((base + m) << log_b) + b, x1);
-          XI.st(((base + 3 * m) << log_b) + b, x3);
-        }
-      }
-      kept = keep;
-      if (!keep) __syncthreads();
-    }
-    if (DB::last && s == LOG_R - 2) {  // (a sparse first pass whose copy stages cover all of R has none)
-      // Last step (s = LOG_R - 2, m = R/4: thread q owns rows q + k m of column b) by the digit basis:
-      // read the inputs, then stage the R/2 constants over the data image (L2-resident table).
-      const uint32_t m = 1u << (LOG_R - 2);
-      const uint32_t i0 = (q << log_b) + b, st = m << log_b;
-      fe x0, x1, x2, x3;
-      if (active) {
-        x0 = XI.ld(i0);
-        x1 = XI.ld(i0 + st);
-        x2 = XI.ld(i0 + 2 * st);
-        x3 = XI.ld(i0 + 3 * st);
-      }
-      __syncthreads();
-      uint32_t* ft = reinterpret_cast<uint32_t*>(X);
-      for (uint32_t k = tid; k < DB::full_entries * 18; k += blockDim.x) {
-        const uint32_t e = k / 18;
-        reinterpret_cast<uint4*>(ft)[k + (e >> 3)] = reinterpret_cast<const uint4*>(db)[k];
-      }
-      __syncthreads();
-      if (active) {
-        const uint32_t jj = q;
-        const uint32_t* wa = dbt(ft, 2 * jj);  // w_{2m}^jj = w_R^(2 jj)
+        // exponents (in w_R units) jj R/2m, jj R/4m, (jj + m) R/4m: multiples of 4 before the last step
+        constexpr uint32_t S = DB::stride;
+        const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) / S);  // w_{2m}^jj
         const fe t1 = fe_mul_db(x1, wa);
         fe t3 = fe_mul_db(x3, wa);
-        fe_bfly_lazy(x0, x1, t1);
-        fe_bfly_lazy(x2, x3, t3);
-        const fe t2 = fe_mul_db(x2, dbt(ft, jj));  // w_{4m}^jj
-        t3 = fe_mul_db(x3, dbt(ft, jj + m));       // w_{4m}^(jj+m)
+        fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
+        fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
+        const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) / S));  // w_{4m}^jj
+        t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) / S));   // w_{4m}^(jj+m)
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
+        XI.st((base << log_b) + b, x0);
+        XI.st(((base + 2 * m) << log_b) + b, x2);
+        XI.st(((base + m) << log_b) + b, x1);
+        XI.st(((base + 3 * m) << log_b) + b, x3);
+      }
+      __syncthreads();
+    }
+  }
+  // The last radix-4 step (m = R/4) leaves thread tid the rows q + k R/4 of column b: exactly the
+  // elements (er[k], eb[k]) it stores.  With the standard store it keeps them in registers (no LDS
+  // round trip and one barrier less per tile; radix 2^9 spills at its 128-register budget).
+  const bool fuse = LOG_R <= 8 && ((size_t)1 << log_ns) >= B;
+  bool kept = false;
+  fe yl[4];
+#pragma unroll 1
+  for (; s < (DB::last ? LOG_R - 2 : LOG_R); s += 2) {
+    const bool keep = fuse && s == LOG_R - 2;  // uniform
+    if (active) {
+      const uint32_t m = 1u << s;
+      const uint32_t jj = q & (m - 1);
+      const uint32_t base = ((q >> s) << (s + 2)) + jj;
+      fe x0 = XI.ld((base << log_b) + b);
+      fe x1 = XI.ld(((base + m) << log_b) + b);
+      fe x2 = XI.ld(((base + 2 * m) << log_b) + b);
+      fe x3 = XI.ld(((base + 3 * m) << log_b) + b);
+      fe t1, t3;
+      const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj, Shoup pairs staged in LDS
+      const fe ta = sm[ia], taq = sm[ia + 1];
+      shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
+      fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
+      fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
+      const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
+      const fe tc = sm[ic], tcq = sm[ic + 1];
+      const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
+      const fe t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
+      t3 = fe_mul_shoup(x3, tc, tcq);
+      fe_bfly_lazy(x0, x2, t2);
+      fe_bfly_lazy(x1, x3, t3);
+      if (keep) {
         yl[0] = x0;
         yl[1] = x1;
         yl[2] = x2;
         yl[3] = x3;
-      }
-      kept = fuse;
-      if (!fuse) {  // the store reads the image: write it back once the table is no longer read
-        __syncthreads();
-        if (active) {
-          XI.st(i0, yl[0]);
-          XI.st(i0 + st, yl[1]);
-          XI.st(i0 + 2 * st, yl[2]);
-          XI.st(i0 + 3 * st, yl[3]);
-        }
-        __syncthreads();
-      }
-    }
-
-    // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
-    const bool last = log_ns + LOG_R == log_n;  // the transform's last pass stores canonical values
-    if (active) {
-      fe* dst = out + boff;
-      if (((size_t)1 << log_ns) >= B) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const size_t j = j0 + eb[t];
-          const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
-          fe val = kept ? yl[t] : XI.ld((er[t] << log_b) + eb[t]);
-          if (last) fe_reduce_lazy(val);
-          if (do_scale) val = fe_mul(val, scale);
-          fe_store(dst + o, val);
-        }
       } else {
-        // Ns < B: the tile's output is the contiguous run [j0 R, (j0 + B) R).
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint32_t o = tid + (uint32_t)t * nthr;
-          const uint32_t qq = o >> (log_ns + LOG_R);
-          const uint32_t rem = o & ((1u << (log_ns + LOG_R)) - 1);
-          const uint32_t r = rem >> log_ns;
-          const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
-          fe val = XI.ld((r << log_b) + bb);
-          if (last) fe_reduce_lazy(val);
-          if (do_scale) val = fe_mul(val, scale);
-          fe_store(dst + (j0 << LOG_R) + o, val);
-        }
+        XI.st((base << log_b) + b, x0);
+        XI.st(((base + 2 * m) << log_b) + b, x2);
+        XI.st(((base + m) << log_b) + b, x1);
+        XI.st(((base + 3 * m) << log_b) + b, x3);
       }
     }
-    if (!PERSIST) break;
-    __syncthreads();  // X is rewritten by the next tile
+    kept = keep;
+    if (!keep) __syncthreads();
+  }
+  if (DB::last && s == LOG_R - 2) {  // (a sparse first pass whose copy stages cover all of R has none)
+    // Last step (s = LOG_R - 2, m = R/4: thread q owns rows q + k m of column b) by the digit basis:
+    // read the inputs, then stage the R/2 constants over the data image (L2-resident table).
+    const uint32_t m = 1u << (LOG_R - 2);
+    const uint32_t i0 = (q << log_b) + b, st = m << log_b;
+    fe x0, x1, x2, x3;
+    if (active) {
+      x0 = XI.ld(i0);
+      x1 = XI.ld(i0 + st);
+      x2 = XI.ld(i0 + 2 * st);
+      x3 = XI.ld(i0 + 3 * st);
+    }
+    __syncthreads();
+    uint32_t* ft = reinterpret_cast<uint32_t*>(X);
+    for (uint32_t k = tid; k < DB::full_entries * 18; k += blockDim.x) {
+      const uint32_t e = k / 18;
+      reinterpret_cast<uint4*>(ft)[k + (e >> 3)] = reinterpret_cast<const uint4*>(db)[k];
+    }
+    __syncthreads();
+    if (active) {
+      const uint32_t jj = q;
+      const uint32_t* wa = dbt(ft, 2 * jj);  // w_{2m}^jj = w_R^(2 jj)
+      const fe t1 = fe_mul_db(x1, wa);
+      fe t3 = fe_mul_db(x3, wa);
+      fe_bfly_lazy(x0, x1, t1);
+      fe_bfly_lazy(x2, x3, t3);
+      const fe t2 = fe_mul_db(x2, dbt(ft, jj));  // w_{4m}^jj
+      t3 = fe_mul_db(x3, dbt(ft, jj + m));       // w_{4m}^(jj+m)
+      fe_bfly_lazy(x0, x2, t2);
+      fe_bfly_lazy(x1, x3, t3);
+      yl[0] = x0;
+      yl[1] = x1;
+      yl[2] = x2;
+      yl[3] = x3;
+    }
+    kept = fuse;
+    if (!fuse) {  // the store reads the image: write it back once the table is no longer read
+      __syncthreads();
+      if (active) {
+        XI.st(i0, yl[0]);
+        XI.st(i0 + st, yl[1]);
+        XI.st(i0 + 2 * st, yl[2]);
+        XI.st(i0 + 3 * st, yl[3]);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- store: out[(j / Ns) Ns R + (j mod Ns) + r Ns] ----
+  const bool last = log_ns + LOG_R == log_n;  // the transform's last pass stores canonical values
+  if (active) {
+    fe* dst = out + boff;
+    if (((size_t)1 << log_ns) >= B) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const size_t j = j0 + eb[t];
+        const size_t o = ((j >> log_ns) << (log_ns + LOG_R)) + (j & ns_mask) + ((size_t)er[t] << log_ns);
+        fe val = kept ? yl[t] : XI.ld((er[t] << log_b) + eb[t]);
+        if (last) fe_reduce_lazy(val);
+        if (do_scale) val = fe_mul(val, scale);
+        fe_store(dst + o, val);
+      }
+    } else {
+      // Ns < B: the tile's output is the contiguous run [j0 R, (j0 + B) R).
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t o = tid + (uint32_t)t * nthr;
+        const uint32_t qq = o >> (log_ns + LOG_R);
+        const uint32_t rem = o & ((1u << (log_ns + LOG_R)) - 1);
+        const uint32_t r = rem >> log_ns;
+        const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
+        fe val = XI.ld((r << log_b) + bb);
+        if (last) fe_reduce_lazy(val);
+        if (do_scale) val = fe_mul(val, scale);
+        fe_store(dst + (j0 << LOG_R) + o, val);
+      }
+    }
   }
 }
 
@@ -663,18 +520,10 @@ struct PassPlan {
 };
 
 constexpr uint32_t kMaxLogR = 9;  // largest radix with a kernel instance and small-root table
-// Radix cap of a size: 2^8 up to 2^24 (three passes of 256 at the headline size); 2^9 from 2^25 on,
-// so 2^25 and 2^26 take three passes, not four (2^26: 13.25 n products instead of 14.5 n, with the
-// column-twiddle table of 2^18 entries below).
-// Radix 2^9 passes (three passes instead of four) at 2^25 and from 2^27 on.  At 2^26 the four
-// digit-basis passes (6, 6, 7, 7) beat (8, 9, 9): 7.56 vs 7.73 ms; at 2^25 (8, 8, 9) beats
-// (6, 6, 6, 7): 3.49-3.51 vs 3.55-3.56 ms.
+// Radix cap of a size: 2^8 (three passes of 256 at the headline 2^24).  Radix 2^9 passes (three
+// passes instead of four) at 2^25 and from 2^27 on.  At 2^26 the four digit-basis passes (6, 6, 7, 7)
+// beat (8, 9, 9): 7.56 vs 7.73 ms; at 2^25 (8, 8, 9) beats (6, 6, 6, 7): 3.49-3.51 vs 3.55-3.56 ms.
 inline uint32_t max_log_r(uint32_t log_n) { return (log_n == 25 || log_n >= 27) ? 9 : 8; }
-// Workgroups of a persistent pass: 256 CUs x the resident 256-thread groups its LDS allows.
-#ifndef STARK_NTT_PERSISTENT
-#define STARK_NTT_PERSISTENT 0
-#endif
-constexpr bool kPersistent = STARK_NTT_PERSISTENT != 0;
 
 // The smaller radices lead: a sparse first pass of odd radix can skip 3 copy
 // stages, an even one only 2.  (Every plan of a size has the same last radix,
@@ -685,7 +534,7 @@ PassPlan plan_passes(uint32_t log_n) {
   p.n_pass = (int)((log_n + cap - 1) / cap);
   const uint32_t base = log_n / p.n_pass, extra = log_n % p.n_pass;
   for (int i = 0; i < p.n_pass; ++i)
-    p.log_r[i] = base + ((uint32_t)(STARK_NTT_SMALL_LAST ? i : p.n_pass - 1 - i) < extra ? 1 : 0);
+    p.log_r[i] = base + ((uint32_t)(p.n_pass - 1 - i) < extra ? 1 : 0);
   return p;
 }
 
@@ -735,26 +584,6 @@ size_t db_lds_fe_c(uint32_t log_r) {
     default: return (size_t)1 << log_r;
   }
 }
-template <int COL>
-int occupancy_c(uint32_t log_r) {
-  switch (log_r) {
-    case 4: return DbPlan<4, COL>::occupancy;
-    case 5: return DbPlan<5, COL>::occupancy;
-    case 6: return DbPlan<6, COL>::occupancy;
-    case 7: return DbPlan<7, COL>::occupancy;
-    case 8: return DbPlan<8, COL>::occupancy;
-    case 9: return DbPlan<9, COL>::occupancy;
-    default: return 4;
-  }
-}
-int pass_occupancy(uint32_t log_r, int col) {
-  switch (col) {
-    case kColNone: return occupancy_c<kColNone>(log_r);
-    case kColFull: return occupancy_c<kColFull>(log_r);
-    case kColT16: return occupancy_c<kColT16>(log_r);
-    default: return occupancy_c<kColTwoLevel>(log_r);
-  }
-}
 size_t db_lds_fe(uint32_t log_r, int col) {
   switch (col) {
     case kColNone: return db_lds_fe_c<kColNone>(log_r);
@@ -765,33 +594,25 @@ size_t db_lds_fe(uint32_t log_r, int col) {
 }
 
 template <int LOG_R>
-pass_fn pass_kernel_r(bool persist, int col) {
-  if (kPersistent && persist) {
-    switch (col) {
-      case kColNone: return ntt_pass_kernel<LOG_R, kPersistent, kColNone>;
-      case kColFull: return ntt_pass_kernel<LOG_R, kPersistent, kColFull>;
-      case kColT16: return ntt_pass_kernel<LOG_R, kPersistent, kColT16>;
-      default: return ntt_pass_kernel<LOG_R, kPersistent, kColTwoLevel>;
-    }
-  }
+pass_fn pass_kernel_r(int col) {
   switch (col) {
-    case kColNone: return ntt_pass_kernel<LOG_R, false, kColNone>;
-    case kColFull: return ntt_pass_kernel<LOG_R, false, kColFull>;
-    case kColT16: return ntt_pass_kernel<LOG_R, false, kColT16>;
-    default: return ntt_pass_kernel<LOG_R, false, kColTwoLevel>;
+    case kColNone: return ntt_pass_kernel<LOG_R, kColNone>;
+    case kColFull: return ntt_pass_kernel<LOG_R, kColFull>;
+    case kColT16: return ntt_pass_kernel<LOG_R, kColT16>;
+    default: return ntt_pass_kernel<LOG_R, kColTwoLevel>;
   }
 }
 
-pass_fn pass_kernel(uint32_t log_r, bool persist, int col) {
+pass_fn pass_kernel(uint32_t log_r, int col) {
   switch (log_r) {
-    case 2: return pass_kernel_r<2>(persist, col);
-    case 3: return pass_kernel_r<3>(persist, col);
-    case 4: return pass_kernel_r<4>(persist, col);
-    case 5: return pass_kernel_r<5>(persist, col);
-    case 6: return pass_kernel_r<6>(persist, col);
-    case 7: return pass_kernel_r<7>(persist, col);
-    case 8: return pass_kernel_r<8>(persist, col);
-    case 9: return pass_kernel_r<9>(persist, col);
+    case 2: return pass_kernel_r<2>(col);
+    case 3: return pass_kernel_r<3>(col);
+    case 4: return pass_kernel_r<4>(col);
+    case 5: return pass_kernel_r<5>(col);
+    case 6: return pass_kernel_r<6>(col);
+    case 7: return pass_kernel_r<7>(col);
+    case 8: return pass_kernel_r<8>(col);
+    case 9: return pass_kernel_r<9>(col);
     default: return nullptr;
   }
 }
@@ -956,14 +777,6 @@ static stark_status full_table(stark_ctx* ctx, const Twiddles& tw_c, uint32_t lo
   return STARK_OK;
 }
 
-bool ntt_full_table_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("STARK_NTT_FULL_TW");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 }  // namespace stark
 
 extern "C" uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap) {
@@ -974,9 +787,6 @@ extern "C" uint32_t stark_ntt_plan(uint32_t log_n, uint32_t* log_r, uint32_t cap
 }
 
 namespace stark {
-
-// (the radix-2^29 pass kernels keep 2^10-element tiles)
-uint32_t ntt_choose_log_b(uint32_t log_n, uint32_t log_r) { return choose_log_b_impl(log_n, log_r, 10); }
 
 uint32_t ntt_first_log_r(uint32_t log_n) { return log_n < 2 ? log_n : plan_passes(log_n).log_r[0]; }
 
@@ -1011,8 +821,6 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     return STARK_OK;
   }
   const PassPlan plan = plan_passes(log_n);
-  if (ntt29_enabled()) return ntt29_device_from(ctx, src, zero_log, d_data, log_n, batch, tw, inverse, stream,
-                                                plan.log_r, plan.n_pass);
   stark_status st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
   if (st != STARK_OK) return st;
   fe* scratch = (fe*)ctx->scratch.ptr;
@@ -1041,7 +849,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     // when that pass has them (log_ns > 0), else it is an explicit product.
     const bool fold = inverse && last && log_ns > 0;
     const fe* full = nullptr;
-    if (last && log_ns > 0 && log_n > tw.l16 && log_n >= 17 && log_n <= 26 && ntt_full_table_enabled()) {
+    if (last && log_ns > 0 && log_n > tw.l16 && log_n >= 17 && log_n <= 26) {
       st = full_table(ctx, tw, lr, fold, stream, &full);
       if (st != STARK_OK) return st;
     }
@@ -1050,10 +858,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
     const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
     const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
-    const uint64_t persistent_grid = 256 * (uint64_t)pass_occupancy(lr, col);
-    const bool persist = kPersistent && total > persistent_grid;
-    const unsigned grid = (unsigned)(persist ? persistent_grid : total);
-    hipLaunchKernelGGL(pass_kernel(lr, persist, col), dim3(grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
+    hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)total), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
                        (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total, sp);

@@ -1,5 +1,5 @@
 """Board power and clocks while one kernel stream runs back to back (is the pass kernel power-bound?).
-Runs stark_ntt_dev 2^24 (WHAT=ntt, STARK_NTT29 as set) or the Merkle build (WHAT=merkle) for ~SECS
+Runs stark_ntt_dev 2^24 (WHAT=ntt) or the Merkle build (WHAT=merkle) for ~SECS
 seconds and samples `rocm-smi --showpower --showclocks` from a side thread; prints one JSON line."""
 import json
 import os
@@ -53,7 +53,7 @@ def main():
         k += 50
     stop.set()
     th.join()
-    print(json.dumps({"what": what, "ntt29": os.environ.get("STARK_NTT29", "0"), "steps": k,
+    print(json.dumps({"what": what, "steps": k,
                       "ms_per_step": (time.time() - t0) * 1e3 / k, "idle": idle, "busy": samples[:6]}))
 
 
