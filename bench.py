@@ -325,13 +325,22 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
         out["prove_poseidon3_distributed_bitexact_vs_golden"] = \
             hashlib.sha256(jsp.encode()).hexdigest() == golden["poseidon3_test"]["json_sha256"]
     out["prove_poseidon3_distributed_ms"] = timed(r1p, wtp, 3)
+    # The sha256_2_test stand-in (synthetic 2^20 steps, precision 2^23): the untimed first proof (it
+    # also warms the twiddles and arenas) is checked against the oracle's StarkProof digest
+    # (tests/golden/large_digests.json), so the timing below never stands without its parity flag.
+    want = large_digests().get("prove_synth_2^20_steps", {}).get("json_sha256")
     rs, ws = synth_r1cs.for_steps(20)
-    prove_distributed(ops, rs, ws)   # warm: twiddles, arenas
+    js20 = prove_distributed(ops, rs, ws)
+    if rank == 0:
+        out["prove_synth_2^20_steps_distributed_bitexact_vs_oracle_digest"] = sha256(js20) == want
     out["prove_synth_2^20_steps_distributed_ms"] = timed(rs, ws, 3)
     # Prepared circuit per rank (DistCircuit: the .r1cs-only work outside the timed region), labelled.
     from stark_amd.dprove import DistCircuit
     circ = DistCircuit(ctx, rs)
-    prove_distributed(ops, None, ws, circuit=circ)
+    js20 = prove_distributed(ops, None, ws, circuit=circ)
+    if rank == 0:
+        out["prove_synth_2^20_steps_distributed_prepared_circuit_bitexact_vs_oracle_digest"] = sha256(js20) == want
+    del js20
     out["prove_synth_2^20_steps_distributed_prepared_circuit_ms"] = timed(None, ws, 3, circ)
     del circ
     return out

@@ -194,6 +194,13 @@ size_t stark_fri_proof_num_layers(const stark_fri_proof* proof);
 stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, int* is_last, uint8_t root2[32],
                                         size_t* n_column, size_t* column_depth, size_t* n_poly,
                                         size_t* poly_depth, size_t* n_last);
+/* Layer i's bytes (any pointer may be NULL): n_column 32-B column leaves and n_column x column_depth
+ * 32-B siblings (leaf to root), the same for the n_poly poly openings, and n_last 32-B values of the
+ * Last entry -- everything a caller needs to build FriProof<H> values itself (fri.rs:16-26) without
+ * going through serde. */
+stark_status stark_fri_proof_layer_data(const stark_fri_proof* proof, size_t i, uint8_t* column_leaves,
+                                        uint8_t* column_nodes, uint8_t* poly_leaves, uint8_t* poly_nodes,
+                                        uint8_t* last_values);
 
 /* ---- R1CS STARK prover (packages/r1cs-stark) -------------------------------- */
 /* mk_r1cs_proof<Fp, BlakeDigest>(witness_trace, computational_trace, public_wires,
@@ -212,6 +219,14 @@ stark_status stark_mk_r1cs_proof(stark_ctx* ctx, const uint64_t* witness_trace, 
 stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, size_t cap, size_t* len);
 stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_root[32], uint8_t l_root[32],
                                     uint8_t a_root[32]);
+/* StarkProof's openings (utils.rs:122-130): which = 0 main_branches (k = 320, 256-B leaves),
+ * 1 linear_comb_branches (k = 80, 32-B leaves); leaves k x leaf_len bytes, nodes k x depth x 32 bytes
+ * (siblings leaf to root).  Any output pointer may be NULL (query the sizes first). */
+stark_status stark_r1cs_proof_branches(const stark_r1cs_proof* proof, int which, size_t* k, size_t* leaf_len,
+                                       size_t* depth, uint8_t* leaves, uint8_t* nodes);
+/* StarkProof's fri_proof, borrowed (valid until stark_r1cs_proof_free); read it with the
+ * stark_fri_proof_* accessors. */
+const stark_fri_proof* stark_r1cs_proof_fri(const stark_r1cs_proof* proof);
 void stark_r1cs_proof_free(stark_r1cs_proof* proof);
 
 /* R1CS front end (host): read_r1cs (circom2bellman_core/src/reader.rs:4-89) +

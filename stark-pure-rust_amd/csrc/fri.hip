@@ -546,4 +546,20 @@ stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, 
   return STARK_OK;
 }
 
+stark_status stark_fri_proof_layer_data(const stark_fri_proof* proof, size_t i, uint8_t* column_leaves,
+                                        uint8_t* column_nodes, uint8_t* poly_leaves, uint8_t* poly_nodes,
+                                        uint8_t* last_values) {
+  if (!proof || i >= proof->layers.size()) return STARK_ERR_BAD_ARG;
+  const stark_fri_layer& L = proof->layers[i];
+  auto put = [](uint8_t* dst, const std::vector<uint8_t>& v) {
+    if (dst && !v.empty()) memcpy(dst, v.data(), v.size());
+  };
+  put(column_leaves, L.col_leaves);
+  put(column_nodes, L.col_nodes);
+  put(poly_leaves, L.poly_leaves);
+  put(poly_nodes, L.poly_nodes);
+  put(last_values, L.last_values);
+  return STARK_OK;
+}
+
 }  // extern "C"

@@ -40,6 +40,12 @@ void fri_proof_json_string(const stark_fri_proof* proof, std::string& o);
 struct stark_r1cs_proof {
   uint8_t m_root[32], l_root[32], a_root[32];
   std::string json;
+  // The parts, for callers that build their own StarkProof value (stark_r1cs_proof_branches / _fri):
+  // main and linear-combination openings (leaves, then depth siblings per opening, leaf to root).
+  size_t depth = 0;
+  std::vector<uint8_t> m_leaves, m_nodes, l_leaves, l_nodes;
+  stark_fri_proof* fri = nullptr;
+  ~stark_r1cs_proof() { stark_fri_proof_free(fri); }
 };
 
 namespace stark {
@@ -989,7 +995,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   stark_fri_proof* fri = nullptr;
   STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
   clk.mark("indices + gather batch");
-  std::unique_ptr<stark_fri_proof, void (*)(stark_fri_proof*)> fri_guard(fri, stark_fri_proof_free);
+  proof->fri = fri;  // owned by the proof from here on
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
   std::string& o = proof->json;
   JsonPieces j;
@@ -1008,6 +1014,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   j.text("}");
   j.render(o);
   clk.mark("proof JSON");
+  proof->depth = log_prec;
+  proof->m_leaves = std::move(m_leaves);
+  proof->m_nodes = std::move(m_nodes);
+  proof->l_leaves = std::move(l_leaves);
+  proof->l_nodes = std::move(l_nodes);
   *out = proof.release();
   return STARK_OK;
 }
@@ -1377,6 +1388,22 @@ stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_roo
   if (a_root) memcpy(a_root, proof->a_root, 32);
   return STARK_OK;
 }
+
+stark_status stark_r1cs_proof_branches(const stark_r1cs_proof* proof, int which, size_t* k, size_t* leaf_len,
+                                       size_t* depth, uint8_t* leaves, uint8_t* nodes) {
+  if (!proof || (which != 0 && which != 1)) return STARK_ERR_BAD_ARG;
+  const size_t ll = which == 0 ? 256 : 32;
+  const std::vector<uint8_t>& lv = which == 0 ? proof->m_leaves : proof->l_leaves;
+  const std::vector<uint8_t>& nd = which == 0 ? proof->m_nodes : proof->l_nodes;
+  if (k) *k = lv.size() / ll;
+  if (leaf_len) *leaf_len = ll;
+  if (depth) *depth = proof->depth;
+  if (leaves) memcpy(leaves, lv.data(), lv.size());
+  if (nodes) memcpy(nodes, nd.data(), nd.size());
+  return STARK_OK;
+}
+
+const stark_fri_proof* stark_r1cs_proof_fri(const stark_r1cs_proof* proof) { return proof ? proof->fri : nullptr; }
 
 void stark_r1cs_proof_free(stark_r1cs_proof* proof) { delete proof; }
 

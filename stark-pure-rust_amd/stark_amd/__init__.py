@@ -80,11 +80,14 @@ _SIGNATURES = {
     "stark_fri_proof_num_layers": ([_vp], ctypes.c_size_t),
     "stark_fri_proof_layer_info": ([_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), _u8p, _szp, _szp, _szp,
                                     _szp, _szp], ctypes.c_int),
+    "stark_fri_proof_layer_data": ([_vp, ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p], ctypes.c_int),
     "stark_mk_r1cs_proof": ([_vp, _u64p, _u64p, ctypes.c_size_t, _u64p, ctypes.c_size_t, _szp, ctypes.c_size_t,
                              _szp, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_size_t,
                              ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_proof_json": ([_vp, ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
     "stark_r1cs_proof_roots": ([_vp, _u8p, _u8p, _u8p], ctypes.c_int),
+    "stark_r1cs_proof_branches": ([_vp, ctypes.c_int, _szp, _szp, _szp, _u8p, _u8p], ctypes.c_int),
+    "stark_r1cs_proof_fri": ([_vp], _vp),
     "stark_r1cs_proof_free": ([_vp], None),
     "stark_r1cs_trace_build": ([_u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_trace_dims": ([_vp, _szp, _szp, _szp, _szp, _szp], ctypes.c_int),

@@ -7,6 +7,10 @@ to the DFT definition:
 * ntt 2^24 forward and inverse (fft.rs:327-379 best_fft / inv_best_fft) on bench.py's rank-0
   input: random_elements(2^24, 0x5EED0000 + 24), w = 7^((p-1)/2^24);
 * ntt 2^20 forward and inverse (config 2) on random_elements(2^20, 0x5EED0000 + 20);
+* ntt 2^25, 2^26 and 2^27 forward and inverse on random_elements(2^k, 0x5EED0000 + k): the plans
+  (8, 8, 9), (6, 6, 7, 7) and (9, 9, 9) -- the radix-2^9 passes, the four-pass digit-basis plan with
+  its two-level-table column twiddles, and (2^27, past the full last-pass table) the lo * hi column
+  twiddle of the last pass;
 * prove_low_degree (fri.rs:46-224) at precision 2^23 on bench.py's FRI input: the evaluations of
   random_elements(2^21, 0x5EED0000 + 23) zero-padded to 2^23, maxdeg 2^21, exclude 8;
 * mk_r1cs_proof (prove.rs:14-378) on the synthetic 2^20-step circuit tools/synth_r1cs.for_steps(20)
@@ -14,7 +18,8 @@ to the DFT definition:
 
 Digests are over the raw little-endian limb bytes (vectors) or the StarkProof/FriProof JSON.
 
-    python tests/golden/make_large_golden.py [--threads T]      (~3-5 min on 8 cores)
+    python tests/golden/make_large_golden.py [--threads T] [--ntt 20,24,25,26,27] [--ntt-only]
+    (~3-5 min on 8 cores for the default sizes and the proofs; 2^25..2^27 add ~10 min)
 """
 import argparse
 import hashlib
@@ -50,12 +55,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--skip-proof", action="store_true")
+    ap.add_argument("--ntt", default="20,24", help="NTT sizes (log2) to digest")
+    ap.add_argument("--ntt-only", action="store_true", help="only the NTT digests")
     args = ap.parse_args()
     T = 1 << (args.threads.bit_length() - 1)
     o = O.Oracle()
     out = json.load(open(OUT)) if os.path.exists(OUT) else {}
     out["generator"] = "tests/golden/make_large_golden.py (oracle C restatement)"
-    for log_n in (20, 24):
+    for log_n in [int(x) for x in args.ntt.split(",") if x]:
         t0 = time.time()
         c = O.random_elements(1 << log_n, 0x5EED0000 + log_n)
         w = O.root_of_unity(log_n)
@@ -66,6 +73,10 @@ def main():
                                  "input_sha256": sha(c), "forward_sha256": sha(fwd), "inverse_sha256": sha(inv),
                                  "forward_head": [str(x) for x in O.from_limbs(fwd[:2])]}
         print(f"ntt 2^{log_n}: {time.time() - t0:.1f} s", flush=True)
+        del c, fwd, inv
+        json.dump(out, open(OUT, "w"), indent=1)
+    if args.ntt_only:
+        return
     lf = 23
     t0 = time.time()
     nf = 1 << lf

@@ -1,8 +1,12 @@
-"""The C ABI from a non-Python caller: tests/abi_client/shim_flow.cpp makes exactly the calls of the
-Rust shim in INTEGRATION.md (best_fft -> MerkleProofInPlace new/update/gen_proofs/get_root ->
-prove_low_degree -> serde JSON).  CPU: the program builds and links against libstark_hip.so.
-GPU: its outputs equal the oracle's best_fft (fft.rs:327-357), Merkle root and paths
-(merkle_proof_in_place.rs:106-206) and FRI proof JSON (fri.rs:46-224)."""
+"""The C ABI from non-Python callers making exactly the calls of the Rust shim in INTEGRATION.md:
+* tests/abi_client/shim_flow.cpp: best_fft -> MerkleProofInPlace new/update/gen_proofs/get_root ->
+  prove_low_degree -> serde JSON; its outputs equal the oracle's best_fft (fft.rs:327-357), Merkle root
+  and paths (merkle_proof_in_place.rs:106-206) and FRI proof JSON (fri.rs:46-224);
+* tests/abi_client/prover_flow.cpp: the whole-prover routes (prove_with_witness on raw bytes, run.rs:
+  310-452; mk_r1cs_proof on the exported trace vectors, prove.rs:14) and a StarkProof rebuilt from the
+  structured parts (roots, branches, FRI layers) as the shim builds StarkProof<H> without serde; all
+  four texts equal the golden StarkProof digests.
+CPU: the programs build and link against libstark_hip.so."""
 import os
 import struct
 import subprocess
@@ -15,12 +19,31 @@ import oracle as O
 HERE = os.path.dirname(os.path.abspath(__file__))
 CLIENT = os.path.join(HERE, "abi_client")
 BIN = os.path.join(CLIENT, "shim_flow")
+PROVER = os.path.join(CLIENT, "prover_flow")
+FIX = os.path.join(HERE, "golden", "r1cs")
 
 
-def test_client_builds_and_links():
+@pytest.mark.parametrize("prog", [BIN, PROVER])
+def test_client_builds_and_links(prog):
     subprocess.run(["make", "-s", "-C", CLIENT], check=True)
-    out = subprocess.run(["ldd", BIN], capture_output=True, text=True, check=True).stdout
+    out = subprocess.run(["ldd", prog], capture_output=True, text=True, check=True).stdout
     assert "libstark_hip.so" in out and "not found" not in out.split("libstark_hip.so")[1].splitlines()[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["compute", "pedersen_test"])
+def test_prover_client_matches_golden(tmp_path, name):
+    """Both whole-prover routes, as the library serialises them and as rebuilt from the parts, equal
+    the golden StarkProof (tests/golden/r1cs_proofs.json, oracle/r1cs.c restating prove.rs:14-378)."""
+    import hashlib
+    import json
+    assert os.path.exists(PROVER), "build() compiles tests/abi_client/prover_flow"
+    want = json.load(open(os.path.join(HERE, "golden", "r1cs_proofs.json")))[name]["json_sha256"]
+    r = subprocess.run([PROVER, os.path.join(FIX, f"{name}.r1cs"), os.path.join(FIX, f"{name}.wtns"), str(tmp_path)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    for f in ("bytes.json", "bytes_parts.json", "mk.json", "mk_parts.json"):
+        assert hashlib.sha256((tmp_path / f).read_bytes()).hexdigest() == want, f
 
 
 @pytest.mark.gpu

@@ -142,3 +142,55 @@ def test_prove_distributed_prepared_circuit(world):
             p.kill()
         assert p.exitcode == 0
     assert res[0] == [True, True, True]
+
+
+def _worker_synth20(rank, world, port, prepared, out_q):
+    """The sha256_2_test stand-in (synthetic 2^20-step circuit, precision 2^23) through the multi-rank
+    prover: rank 0's StarkProof JSON digest, to be compared with the oracle's
+    (tests/golden/large_digests.json, mk_r1cs_proof restated in oracle/r1cs.c, prove.rs:14-378)."""
+    import faulthandler
+    faulthandler.dump_traceback_later(200, exit=True)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=180))
+    import stark_amd as S
+    from stark_amd.dprove import DistCircuit, GpuProverOps, prove_distributed
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth_r1cs
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = S.Context(0)
+    r1, wt = synth_r1cs.for_steps(20)
+    if prepared:
+        circ = DistCircuit(ctx, r1)
+        js = prove_distributed(GpuProverOps(ctx), None, wt, circuit=circ)
+    else:
+        circ = None
+        js = prove_distributed(GpuProverOps(ctx), r1, wt)
+    out_q.put((rank, hashlib.sha256(js.encode()).hexdigest() if rank == 0 else None))
+    dist.barrier()
+    del circ
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,prepared", [(4, False), (8, False), (8, True)])
+def test_prove_distributed_synth_2_20_vs_oracle_digest(world, prepared):
+    """BASELINE config 5's stand-in at its size: one proof of the synthetic 2^20-step circuit over
+    `world` ranks (cold, and from a DistCircuit) equals the oracle's StarkProof byte for byte
+    (the digest tests/test_gpu_large.py pins the single-GPU prover to)."""
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "large_digests.json")))["prove_synth_2^20_steps"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_synth20, args=(r, world, port, prepared, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=230) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+        assert p.exitcode == 0
+    assert res[0] == want["json_sha256"]

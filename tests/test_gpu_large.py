@@ -63,6 +63,22 @@ def test_ntt_dense_full_vector_vs_oracle(ctx, oracle, log_n):
     assert np.array_equal(inv, oracle.inv_best_fft(c, w, log_n, cpus=CPUS))
 
 
+@pytest.mark.parametrize("log_n", [25, 26, 27])
+def test_ntt_dense_digest_beyond_bench(ctx, log_n):
+    """Dense forward and inverse transforms past the bench size hash to the oracle's digests
+    (tests/golden/make_large_golden.py --ntt 25,26,27): 2^25 = radices (8, 8, 9), 2^26 = the four
+    digit-basis passes (6, 6, 7, 7) whose third pass takes the two-level column twiddle with the
+    digit-basis last step, 2^27 = (9, 9, 9) past the full last-pass table (lo * hi column twiddle)."""
+    rec = BIG.get(f"ntt_2^{log_n}")
+    if rec is None:
+        pytest.fail(f"large_digests.json has no ntt_2^{log_n} (run make_large_golden.py --ntt {log_n})")
+    c = O.random_elements(1 << log_n, 0x5EED0000 + log_n)
+    assert _sha(c) == rec["input_sha256"]
+    w = O.root_of_unity(log_n)
+    assert _sha(_ntt_dev(ctx, c, log_n, w, inverse=False)) == rec["forward_sha256"]
+    assert _sha(_ntt_dev(ctx, c, log_n, w, inverse=True)) == rec["inverse_sha256"]
+
+
 def test_ntt_2_24_host_entry_point(ctx):
     """best_fft on a host vector (H2D + the same passes + D2H) gives the same 2^24 output."""
     rec = BIG["ntt_2^24"]

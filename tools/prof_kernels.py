@@ -1,6 +1,8 @@
 """Workload for rocprofv3 counter passes (tools/pmc_round.sh): the bench's dominant kernels on
 device-resident synthetic data, a few dispatches each, nothing else.
-    WHAT=ntt|merkle|all (default all); REPS=5; STARK_LIB=<path> times another build of the library
+    WHAT=ntt|merkle|all (default all) | prover (the synthetic 2^20-step proof, the sha256_2_test stand-in:
+    REPS cold prove_with_witness calls, then REPS from a prepared circuit); REPS=5;
+    STARK_LIB=<path> times another build of the library
 """
 import ctypes
 import os
@@ -23,6 +25,20 @@ def main():
     if os.environ.get("STARK_LIB"):
         S.load_library(os.path.abspath(os.environ["STARK_LIB"]))
     ctx = S.Context(0)
+    if what == "prover":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import synth_r1cs
+        from stark_amd.r1cs import R1csCircuit, prove_with_witness
+        rs, ws = synth_r1cs.for_steps(int(os.environ.get("LOG_STEPS", "20")))
+        for _ in range(reps):
+            prove_with_witness(ctx, rs, ws).to_json()
+        c = R1csCircuit(ctx, rs)
+        for _ in range(reps):
+            c.prove(ws).to_json()
+        del c
+        ctx.close()
+        print("prof_kernels done", what, reps)
+        return
     host = O.random_elements(n, 0x5EED0000 + log_n)
     d = ctx.alloc(n * 32)
     ctx.h2d(d, host)
