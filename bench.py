@@ -35,8 +35,10 @@ import torch.distributed as dist  # noqa: E402
 S = None  # stark_amd, imported in main() once this process is known to be a rank
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
-# Issue cost of these VALU streams (64-bit mads, carry chains, alignbit/xor mixes): 4.0 cycles per
-# wave64 instruction at the in-kernel clock (tools/microbench/mix_rates.hip, profiles/r02_mix_rates.txt).
+# Issue cost of a wave64 VALU instruction on a 16-lane SIMD: one quad-cycle.  The hardware's own count
+# of VALU quad-cycles (SQ_ACTIVE_INST_VALU) equals SQ_INSTS_VALU on these kernels, and the measured
+# mixed streams (64-bit mads, carry chains, alignbit/xor) issue at 4.0 cycles per instruction
+# (tools/microbench/mix_rates.hip, profiles/r02_mix_rates.txt).
 ISSUE_CYCLES = 4.0
 SIMDS = 1024
 # The constant products alone with their constants in LDS, 4 waves/SIMD, same run
@@ -44,8 +46,8 @@ SIMDS = 1024
 SHOUP_PRODUCT_PEAK = 138.71e9
 DB_PRODUCT_PEAK = 199.98e9
 LOG_N = 24
-PROFILE = os.path.join(ROOT, "profiles", "r02_summary.json")
-PMC = os.path.join(ROOT, "profiles", "r02_pmc.json")
+PROFILE = os.path.join(ROOT, "profiles", "r03_summary.json")
+PMC = os.path.join(ROOT, "profiles", "r03_pmc_ntt.json")
 LARGE = os.path.join(ROOT, "tests", "golden", "large_digests.json")
 
 
@@ -346,30 +348,38 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
     return out
 
 
-MERKLE_SQ = os.path.join(ROOT, "profiles", "r02_merkle_sq_counters.json")
+MERKLE_SQ = os.path.join(ROOT, "profiles", "r03_pmc_merkle32.json")
 
 
 def merkle_valu_roofline(n: int, ms: float) -> dict:
     """Blake2s issue roofline of a 2^log n x 32-B tree build: n leaf compressions (one 32-B block
-    each) + n - 1 node compressions (64-B blocks) = 2n - 1.  The VALU instructions per compression
-    (SQ_INSTS_VALU of the leaf-level kernel x 64 / its compressions) and the clock under load come
-    from the committed rocprofv3 pass (MERKLE_SQ); each wave64 instruction issues in ISSUE_CYCLES
-    (the Blake2s G stream, tools/microbench/mix_rates.hip).  `leaf_kernel_issue_frac` is the leaf
-    kernel's own issue-bound time over its measured time (same profile)."""
+    each) + n - 1 node compressions (64-B blocks) = 2n - 1.  From the committed counter passes over
+    2^24 x 32-B tree builds alone (tools/pmc_round.sh ... merkle32): per build, the VALU instructions
+    of every launch (SQ_INSTS_VALU, weighted by launches per build) x 4 cycles / 1024 SIMDs over the
+    launches' elapsed cycles (GRBM_GUI_ACTIVE / 8) -- each dispatch at its own clock, so clock-free;
+    and the instructions per compression."""
     comp = 2 * n - 1
     out = {"compressions": comp, "achieved_compressions_per_s": comp / (ms / 1000.0)}
     try:
-        prof = json.load(open(MERKLE_SQ))
-        per = prof["valu_insts_per_compression"]
-        cyc = per * ISSUE_CYCLES / 64.0                  # SIMD cycles per compression (one lane's share)
-        ghz = prof["effective_clock_ghz"]
-        peak = SIMDS * ghz * 1e9 / cyc                   # compressions/s with every SIMD issuing
-        out.update({"valu_insts_per_compression": per, "issue_cycles_per_wave64_instruction": ISSUE_CYCLES,
-                    "clock_ghz": ghz, "peak_compressions_per_s": peak,
-                    "frac": round(out["achieved_compressions_per_s"] / peak, 4),
-                    "leaf_kernel_issue_frac": prof["leaf_kernel_issue_frac"],
+        prof = json.load(open(MERKLE_SQ))["kernels"]
+        builds = min(v["dispatches_per_pass"] for k, v in prof.items() if "merkle_build_kernel<true>" in k)
+        need = took = insts = 0.0
+        for k, v in prof.items():
+            if "merkle" not in k or "GRBM_GUI_ACTIVE" not in v or "SQ_INSTS_VALU" not in v:
+                continue
+            w = v["dispatches_per_pass"] / builds
+            insts += w * v["SQ_INSTS_VALU"]
+            need += w * v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS
+            took += w * v["GRBM_GUI_ACTIVE"] / 8
+        leaf = next(v for k, v in prof.items() if "merkle_build_kernel<true>" in k)
+        out.update({"valu_insts_per_compression": round(insts * 64 / comp, 1),
+                    "issue_cycles_per_wave64_instruction": ISSUE_CYCLES,
+                    "issue_cycles_per_build": round(need), "elapsed_cycles_per_build": round(took),
+                    "frac": round(need / took, 4),
+                    "leaf_kernel_issue_frac": round(leaf["valu_issue_frac"], 4),
+                    "leaf_kernel_clock_ghz": round(leaf.get("effective_clock_ghz", 0), 3),
                     "sq_profile": os.path.relpath(MERKLE_SQ, ROOT)})
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, StopIteration):
         pass
     return out
 
@@ -692,57 +702,69 @@ def main():
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     plan = S.ntt_plan(log_n)
     passes = len(plan)
-    # The pass kernels of this transform (csrc/ntt.hip: ntt_pass_kernel<LOG_R, persistent, COL>, COL =
-    # 0 first pass, 2 Shoup t16 column twiddles, 1 the last pass's full table): per-launch HBM bytes,
-    # rocprof times and SQ counters from the committed round-2 profiles of this exact command line.
-    knames = []
-    for i, r in enumerate(plan):
-        col = 0 if i == 0 else (1 if i == passes - 1 and 17 <= log_n <= 26 else 2)
-        knames.append(f"stark::ntt_pass_kernel<{r}, false, {col}>")
+    # The pass kernels of this transform (csrc/ntt.hip: ntt_wave_kernel<COL> for radix-2^8 passes,
+    # ntt_pass_kernel<LOG_R, COL> otherwise; COL = 0 first pass, 2 Shoup t16 column twiddles, 1 the last
+    # pass's full table): per-launch HBM bytes and rocprof times from the committed profile of this exact
+    # command line (tools/profile_round.sh), VALU issue from the committed counter passes over 2^24
+    # transforms alone (tools/pmc_round.sh ... ntt).
     traffic = prof_avg = prof_med = None
-    sq = {}
+    knames, sq = [], {}
     try:
         prof = json.load(open(PROFILE))
-        pmc = json.load(open(PMC))["kernels"]
-        if log_n == 24 and all(k in prof["pmc_bytes_per_launch"] for k in knames):
+        knames = sorted(k for k in prof["kernels"] if "ntt_pass_kernel" in k or "ntt_wave_kernel" in k)
+        if log_n == 24 and knames and all(k in prof["pmc_bytes_per_launch"] for k in knames):
             # HBM bytes of one transform: per-launch FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md)
             # summed over the transform's launches.
             traffic = sum(prof["pmc_bytes_per_launch"][k]["hbm_bytes"] for k in knames)
             prof_avg = sum(prof["kernels"][k]["avg_ns"] for k in knames) / 1e6
             prof_med = sum(prof["kernels"][k]["steady_median_ns"] for k in knames) / 1e6
-            sq = {k: pmc[k] for k in knames}
+        if log_n == 24:
+            pmc = json.load(open(PMC))["kernels"]
+            sq = {k: v for k, v in pmc.items() if ("ntt_pass_kernel" in k or "ntt_wave_kernel" in k)
+                  and "valu_issue_frac" in v}
     except (OSError, KeyError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_over_algorithmic": round(traffic / ntt_bytes, 3) if traffic else None,
-                "kernel": f"ntt_pass_kernel x {passes} launches (radices 2^{plan}) per 2^{log_n} transform",
+                "kernel": f"{passes} NTT pass launches (radices 2^{plan}) per 2^{log_n} transform",
                 "ms_per_transform": round(ev_ms, 4), "avg_launch_ms": round(ev_ms / passes, 4),
                 "rocprof_ms_per_transform_avg": round(prof_avg, 4) if prof_avg else None,
                 "rocprof_ms_per_transform_steady_median": round(prof_med, 4) if prof_med else None,
-                "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
+                "rocprof_kernels": knames, "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
     modmuls, db_muls = ntt_products(log_n, plan)
     # The transform's products at the standalone rates of their two forms (the rest of the pass, the
     # butterflies, LDS traffic and the Montgomery full-table column twiddle, priced at nothing).
     peak = modmuls / (db_muls / DB_PRODUCT_PEAK + (modmuls - db_muls) / SHOUP_PRODUCT_PEAK)
-    valu = {"bound": f"VALU issue ({ISSUE_CYCLES} cycles per wave64 instruction, measured)",
+    valu = {"bound": "VALU issue: one quad-cycle (4 cycles) per wave64 VALU instruction on a 16-lane SIMD",
             "modmuls_per_transform": modmuls, "digit_basis_modmuls_per_transform": db_muls,
             "achieved_modmul_per_s": modmuls / (ev_ms / 1000.0),
             "product_peak_per_s": round(peak), "shoup_product_peak_per_s": SHOUP_PRODUCT_PEAK,
             "digit_basis_product_peak_per_s": DB_PRODUCT_PEAK}
     valu["product_frac"] = round(valu["achieved_modmul_per_s"] / peak, 4)
     if sq:
-        # Issue-bound time of the transform: each pass's SQ_INSTS_VALU x ISSUE_CYCLES over the chip's
-        # 1024 SIMDs at that pass's measured clock (GRBM_GUI_ACTIVE / 8 XCDs / duration); frac =
-        # that time over the measured transform time (HIP events above).
-        issue_ms = sum(v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS / (v["effective_clock_ghz"] * 1e9) * 1e3
-                       for v in sq.values())
+        # Issue fraction of the transform, each dispatch priced at ITS OWN clock: per pass,
+        # SQ_INSTS_VALU x 4 / 1024 SIMDs = the SIMD cycles its VALU instructions need, over
+        # GRBM_GUI_ACTIVE / 8 XCDs = the cycles it took, both from the same dispatch
+        # (tools/pmc_summary.py); summed over the transform's passes.  Clock-free and <= 1.
+        need = sum(v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS for v in sq.values())
+        took = sum(v["GRBM_GUI_ACTIVE"] / 8 for v in sq.values())
         insts = sum(v["SQ_INSTS_VALU"] for v in sq.values())
         valu.update({"sq_insts_valu_per_transform": insts,
                      "valu_lane_insts_per_element": round(insts * 64 / n, 1),
-                     "measured_clock_ghz": [round(v["effective_clock_ghz"], 3) for v in sq.values()],
-                     "issue_bound_ms_per_transform": round(issue_ms, 4),
-                     "frac": round(issue_ms / ev_ms, 4), "sq_profile": os.path.relpath(PMC, ROOT)})
+                     "issue_cycles_per_transform": round(need), "elapsed_cycles_per_transform": round(took),
+                     "frac": round(need / took, 4),
+                     "per_pass": {k: {"frac": round(v["valu_issue_frac"], 4),
+                                      "clock_ghz": round(v.get("effective_clock_ghz", 0), 3),
+                                      "dual_issue_share": round(v.get("valu_dual_issue_share", 0), 4),
+                                      "class_share": {c: round(x, 3) for c, x in v.get("valu_class_share", {}).items()}}
+                                  for k, v in sq.items()},
+                     "sq_profile": os.path.relpath(PMC, ROOT)})
+        # The same instruction count priced at the clock rocm-smi sampled under this bench's NTT loop
+        # (reads up to ~10 % above the in-kernel clock, so this figure is a lower estimate).
+        sclk = extras.get("power_during_ntt", {}).get("sclk_mhz")
+        if sclk:
+            valu["frac_at_sampled_sclk"] = round(need / (sclk * 1e6) * 1e3 / ev_ms, 4)
         roofline["valu_issue_frac"] = valu["frac"]
     if "power_during_ntt" in extras:
         roofline["power_during_ntt"] = extras["power_during_ntt"]

@@ -1,6 +1,6 @@
 """Workload for rocprofv3 counter passes (tools/pmc_round.sh): the bench's dominant kernels on
 device-resident synthetic data, a few dispatches each, nothing else.
-    WHAT=ntt|merkle|all (default all) | prover (the synthetic 2^20-step proof, the sha256_2_test stand-in:
+    WHAT=ntt|merkle|merkle32 (2^24 x 32-B trees alone)|all (default all) | prover (the synthetic 2^20-step proof, the sha256_2_test stand-in:
     REPS cold prove_with_witness calls, then REPS from a prepared circuit); REPS=5;
     STARK_LIB=<path> times another build of the library
 """
@@ -48,11 +48,11 @@ def main():
         for _ in range(reps):
             ctx.ntt_dev(d, log_n, 1, w)
         ctx.synchronize()
-    if what in ("merkle", "all"):
+    if what in ("merkle", "merkle32", "all"):
         t = S.MerkleProofInPlace(ctx)
         for _ in range(reps):
             t.update_dev(d, n, 32)
-        for _ in range(reps):
+        for _ in range(reps if what != "merkle32" else 0):
             t.update_dev(d, n // 8, 256)
         ctx.synchronize()
         del t
