@@ -369,7 +369,7 @@ def merkle_valu_roofline(n: int, ms: float) -> dict:
                 continue
             w = v["dispatches_per_pass"] / builds
             insts += w * v["SQ_INSTS_VALU"]
-            need += w * v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS
+            need += w * (v["SQ_INSTS_VALU"] - v.get("SQ_ACTIVE_INST_VALU2", 0.0)) * ISSUE_CYCLES / SIMDS
             took += w * v["GRBM_GUI_ACTIVE"] / 8
         leaf = next(v for k, v in prof.items() if "merkle_build_kernel<true>" in k)
         out.update({"valu_insts_per_compression": round(insts * 64 / comp, 1),
@@ -744,10 +744,12 @@ def main():
     valu["product_frac"] = round(valu["achieved_modmul_per_s"] / peak, 4)
     if sq:
         # Issue fraction of the transform, each dispatch priced at ITS OWN clock: per pass,
-        # SQ_INSTS_VALU x 4 / 1024 SIMDs = the SIMD cycles its VALU instructions need, over
+        # (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) x 4 / 1024 SIMDs = the SIMD cycles its VALU
+        # instructions occupy (one quad-cycle each, less the quad-cycles that issued two), over
         # GRBM_GUI_ACTIVE / 8 XCDs = the cycles it took, both from the same dispatch
         # (tools/pmc_summary.py); summed over the transform's passes.  Clock-free and <= 1.
-        need = sum(v["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS for v in sq.values())
+        need = sum((v["SQ_INSTS_VALU"] - v.get("SQ_ACTIVE_INST_VALU2", 0.0)) * ISSUE_CYCLES / SIMDS
+                   for v in sq.values())
         took = sum(v["GRBM_GUI_ACTIVE"] / 8 for v in sq.values())
         insts = sum(v["SQ_INSTS_VALU"] for v in sq.values())
         valu.update({"sq_insts_valu_per_transform": insts,
@@ -755,6 +757,7 @@ def main():
                      "issue_cycles_per_transform": round(need), "elapsed_cycles_per_transform": round(took),
                      "frac": round(need / took, 4),
                      "per_pass": {k: {"frac": round(v["valu_issue_frac"], 4),
+                                      "frac_4cyc": round(v.get("valu_issue_frac_4cyc", 0), 4),
                                       "clock_ghz": round(v.get("effective_clock_ghz", 0), 3),
                                       "dual_issue_share": round(v.get("valu_dual_issue_share", 0), 4),
                                       "class_share": {c: round(x, 3) for c, x in v.get("valu_class_share", {}).items()}}

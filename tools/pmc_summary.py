@@ -4,13 +4,14 @@ clock and the HBM bytes, plus these derived figures, each computed WITHIN one di
 of a pass and its timestamps come from the same dispatch, so no clock of another run enters):
 
 * effective_clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICROARCH.md "DVFS give-back");
-* valu_issue_frac = (SQ_INSTS_VALU x 4 cycles / 1024 SIMDs) / (GRBM_GUI_ACTIVE / 8): the cycles the
-  SIMDs need to issue the dispatch's VALU instructions, one quad-cycle each (a wave64 instruction
-  passes a 16-lane SIMD in 4 cycles; SQ_ACTIVE_INST_VALU, the hardware's own count of VALU quad-cycles,
-  equals SQ_INSTS_VALU on these kernels), over the dispatch's elapsed cycles -- clock-free, <= 1 on a
-  balanced chip;
-* valu_dual_issue_share = SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU (quad-cycles in which a second VALU
-  instruction issued: the pricing above over-counts by this share);
+* valu_issue_frac = ((SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) x 4 cycles / 1024 SIMDs) / (GRBM_GUI_ACTIVE
+  / 8): the SIMD quad-cycles in which the dispatch's VALU instructions issue -- one per instruction (a
+  wave64 instruction passes a 16-lane SIMD in 4 cycles; SQ_ACTIVE_INST_VALU, the hardware's own count,
+  equals SQ_INSTS_VALU on these kernels) less the quad-cycles that issued two (SQ_ACTIVE_INST_VALU2) --
+  over the dispatch's elapsed cycles: clock-free, <= 1;
+* valu_issue_frac_4cyc: the same without the dual-issue correction (every instruction its own
+  quad-cycle; above 1 where dual issue is frequent);
+* valu_dual_issue_share = SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU;
 * valu_class_share: INT32 / INT64 / CVT / FMA_F64 ... instructions over SQ_INSTS_VALU;
 * hbm_bytes = FETCH_SIZE x 2 (gfx950 tallies 128-B read requests at 64 B) + WRITE_SIZE, both KiB.
 
@@ -38,6 +39,7 @@ def main():
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     durs = collections.defaultdict(list)
     fracs = collections.defaultdict(list)
+    fracs4 = collections.defaultdict(list)
     clocks = collections.defaultdict(list)
     for d in dirs:
         for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
@@ -59,7 +61,9 @@ def main():
                     durs[key].append(dur)
                 g = cs.get("GRBM_GUI_ACTIVE")
                 if g and "SQ_INSTS_VALU" in cs:
-                    fracs[key].append(cs["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS / (g / 8))
+                    fracs4[key].append(cs["SQ_INSTS_VALU"] * ISSUE_CYCLES / SIMDS / (g / 8))
+                    busy = cs["SQ_INSTS_VALU"] - cs.get("SQ_ACTIVE_INST_VALU2", 0.0)
+                    fracs[key].append(busy * ISSUE_CYCLES / SIMDS / (g / 8))
                 if g and dur:
                     clocks[key].append(g / 8 / dur)
     summary = {}
@@ -76,6 +80,7 @@ def main():
         if fracs[key]:
             rec["valu_issue_frac"] = sum(fracs[key]) / len(fracs[key])
             rec["valu_issue_frac_range"] = [min(fracs[key]), max(fracs[key])]
+            rec["valu_issue_frac_4cyc"] = sum(fracs4[key]) / len(fracs4[key])
         iv = rec.get("SQ_INSTS_VALU")
         if iv:
             if "SQ_ACTIVE_INST_VALU2" in rec:
@@ -89,7 +94,7 @@ def main():
             rec["hbm_bytes"] = rec["fetch_bytes_corrected"] + rec["write_bytes"]
         summary[f"{k} grid={grid}"] = rec
     doc = {"kernels": summary,
-           "derived": "per-dispatch: valu_issue_frac = SQ_INSTS_VALU*4/1024/(GRBM_GUI_ACTIVE/8); "
+           "derived": "per-dispatch: valu_issue_frac = (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2)*4/1024/(GRBM_GUI_ACTIVE/8); "
                       "effective_clock_ghz = GRBM_GUI_ACTIVE/8/duration; hbm_bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB)"}
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc, indent=1))
