@@ -364,9 +364,9 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     }
   }
   // The last radix-4 step (m = R/4) leaves thread tid the rows q + k R/4 of column b: exactly the
-  // elements (er[k], eb[k]) it stores.  With the standard store it keeps them in registers (no LDS
-  // round trip and one barrier less per tile; radix 2^9 spills at its 128-register budget).
-  const bool fuse = LOG_R <= 8 && ((size_t)1 << log_ns) >= B;
+  // elements (er[k], eb[k]) it stores, so it keeps them in registers (no LDS round trip and one
+  // barrier less per tile; radix 2^9 spills at its 128-register budget).
+  constexpr bool fuse = LOG_R <= 8;
   bool kept = false;
   fe yl[4];
 #pragma unroll 1
@@ -460,7 +460,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   const bool last = log_ns + LOG_R == log_n;  // the transform's last pass stores canonical values
   if (active) {
     fe* dst = out + boff;
-    if (((size_t)1 << log_ns) >= B) {
+    if (kept || ((size_t)1 << log_ns) >= B) {
+      // (Ns < B from registers, the first pass: each wave stores B runs of 16 adjacent outputs.)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const size_t j = j0 + eb[t];
