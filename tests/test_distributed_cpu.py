@@ -2,23 +2,14 @@
 (stark_amd/distributed.py) at world sizes 2 and 4, with the local steps done
 by the oracle, checked bit-exactly against the oracle's single-process NTT."""
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import oracle as O
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+from ranks import run_ranks  # noqa: E402
 
 
 class OracleOps:
@@ -130,15 +121,7 @@ def _local_after(shard, log_n, w, ops):
 def test_cyclic_ntt_pipelined_gloo(world, log_n):
     """bench.py's N > 1 schedule (exchange i overlapping local NTT i+1, two buffer pairs) produces
     exactly cyclic_ntt's result for every transform."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, log_n, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
+    res = dict(run_ranks(_worker_pipelined, world, (log_n,), timeout=300))
     assert all(res.values())
 
 
@@ -160,16 +143,7 @@ def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
                                                  (8, 12, False), (8, 9, True)])
 def test_cyclic_ntt_gloo(world, log_n, inverse):
     """One-exchange layout: rank r gets X[r c + i + M k1] at out[k1 c + i]."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    parts = dict(q.get(timeout=300) for _ in range(world))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    parts = dict(run_ranks(_worker_cyclic, world, (log_n, inverse), timeout=300))
     n = 1 << log_n
     M, c = n // world, n // world // world
     got = np.zeros((n, 4), dtype=np.uint64)
@@ -187,16 +161,7 @@ def test_cyclic_ntt_gloo(world, log_n, inverse):
 @pytest.mark.parametrize("world,log_n,inverse", [(2, 6, False), (2, 9, True), (4, 8, False), (4, 10, True),
                                                  (8, 12, False)])
 def test_four_step_ntt_gloo(world, log_n, inverse):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    parts = dict(q.get(timeout=300) for _ in range(world))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    parts = dict(run_ranks(_worker, world, (log_n, inverse), timeout=300))
     got = np.concatenate([parts[r] for r in range(world)])
     o = O.Oracle()
     n = 1 << log_n
@@ -228,16 +193,7 @@ def _worker_merkle(rank, world, port, log_m, leaf_len, out_q):
 @pytest.mark.parametrize("world,log_m,leaf_len", [(2, 5, 32), (4, 6, 40), (8, 3, 256)])
 def test_distributed_merkle_gloo(world, log_m, leaf_len):
     """Per-rank subtrees + all-gathered roots = the single tree (root and paths)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_merkle, args=(r, world, port, log_m, leaf_len, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    res = run_ranks(_worker_merkle, world, (log_m, leaf_len), timeout=300)
     m = 1 << log_m
     n = world * m
     rng = np.random.default_rng(7)

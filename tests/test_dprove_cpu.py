@@ -7,27 +7,18 @@ transcript, the per-class FRI folds and the opening assembly."""
 import hashlib
 import json
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import oracle as O
+from ranks import run_ranks  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIX = os.path.join(ROOT, "tests", "golden", "r1cs")
 P = O.P
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _u8(b: bytes) -> torch.Tensor:
@@ -169,16 +160,7 @@ def _worker(rank, world, port, name, tail_log, out_q):
 def test_prove_distributed_gloo(name, world, tail_log):
     """tail_log 0: every FRI layer distributed; else layers of <= 2^tail_log values on rank 0."""
     golden = json.load(open(os.path.join(ROOT, "tests", "golden", "r1cs_proofs.json")))
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, tail_log, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=600) for _ in range(world))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    res = dict(run_ranks(_worker, world, (name, tail_log), timeout=600))
     assert res[0] == golden[name]["json_sha256"]
     assert all(res[r] is None for r in range(1, world))
 
@@ -204,14 +186,5 @@ def _worker_bad(rank, world, port, out_q):
 def test_prove_distributed_failure_raises_on_every_rank():
     """A rank whose set-up fails must not leave the others blocked in a collective."""
     world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_bad, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=300) for _ in range(world))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    res = dict(run_ranks(_worker_bad, world, (), timeout=300))
     assert all(v != "no error" for v in res.values()), res

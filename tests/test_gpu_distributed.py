@@ -3,25 +3,16 @@ one-GPU test box both ranks share GPU 0 and exchange through gloo; the 8-GPU
 bench uses the same code with RCCL ("nccl")."""
 import datetime
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import oracle as O
+from ranks import run_ranks  # noqa: E402
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
@@ -49,18 +40,7 @@ def _worker_cyclic(rank, world, port, log_n, inverse, out_q):
 
 @pytest.mark.parametrize("world,log_n,inverse", [(2, 12, False), (2, 17, True), (4, 16, False), (8, 15, True)])
 def test_cyclic_ntt_gpu(world, log_n, inverse):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_cyclic, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    parts = dict(q.get(timeout=110) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    parts = dict(run_ranks(_worker_cyclic, world, (log_n, inverse), timeout=110))
     n = 1 << log_n
     M, c = n // world, n // world // world
     got = np.zeros((n, 4), dtype=np.uint64)
@@ -145,18 +125,7 @@ def _worker_merkle(rank, world, port, log_m, out_q):
 
 @pytest.mark.parametrize("world,log_m", [(2, 12), (4, 10)])
 def test_distributed_merkle_gpu(world, log_m):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_merkle, args=(r, world, port, log_m, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=110) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    res = run_ranks(_worker_merkle, world, (log_m,), timeout=110)
     n = world << log_m
     blob = O.random_elements(n, 99).tobytes()
     idx = [0, n - 1, 3, n // 2 + 7, 3]
@@ -194,18 +163,7 @@ def _worker(rank, world, port, log_n, inverse, out_q):
 
 @pytest.mark.parametrize("world,log_n,inverse", [(2, 12, False), (2, 17, True), (4, 16, False)])
 def test_four_step_ntt_gpu(world, log_n, inverse):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, log_n, inverse, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    parts = dict(q.get(timeout=110) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    parts = dict(run_ranks(_worker, world, (log_n, inverse), timeout=110))
     got = np.concatenate([parts[r] for r in range(world)])
     o = O.Oracle()
     n = 1 << log_n
@@ -238,7 +196,7 @@ def test_transpose_and_twiddle(ctx):
         ctx.free(e)
 
 
-def _worker_rccl_world1(port, out_q):
+def _worker_rccl_world1(rank, world, port, out_q):
     """Backend "nccl" (RCCL) at world 1 on the box's one GPU: the code the 8-GPU bench runs --
     cyclic_ntt_pipelined's async all_to_all_single on RCCL's stream, the plain cyclic_ntt exchange
     and DistributedMerkle's all_gather_object -- with trivial exchanges."""
@@ -275,15 +233,7 @@ def _worker_rccl_world1(port, out_q):
 
 
 def test_rccl_world1_pipelined_and_merkle():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_worker_rccl_world1, args=(_free_port(), q))
-    p.start()
-    res = q.get(timeout=110)
-    p.join(timeout=60)
-    if p.is_alive():
-        p.kill()
-    assert p.exitcode == 0
+    res = run_ranks(_worker_rccl_world1, 1, timeout=110)[0]
     o = O.Oracle()
     log_n = 14
     w = O.root_of_unity(log_n)

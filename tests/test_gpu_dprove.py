@@ -6,26 +6,17 @@ import datetime
 import hashlib
 import json
 import os
-import socket
 import sys
 
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
+from ranks import run_ranks
 
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIX = os.path.join(ROOT, "tests", "golden", "r1cs")
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
 
 
 def _worker(rank, world, port, name, log_synth, tail_log, out_q):
@@ -58,18 +49,7 @@ def _worker(rank, world, port, name, log_synth, tail_log, out_q):
 
 
 def _run(world, name, log_synth=0, tail_log=16):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, log_synth, tail_log, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = {r: (a, b) for r, a, b in (q.get(timeout=110) for _ in range(world))}
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    res = {r: (a, b) for r, a, b in run_ranks(_worker, world, (name, log_synth, tail_log), timeout=110)}
     assert all(res[r][0] is None for r in range(1, world))
     return res[0]
 
@@ -129,18 +109,7 @@ def _worker_circuit(rank, world, port, out_q):
 def test_prove_distributed_prepared_circuit(world):
     """DistCircuit: two witnesses of one synthetic circuit equal the single-GPU proofs; pedersen_test
     equals the golden digest."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_circuit, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=110) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    res = dict(run_ranks(_worker_circuit, world, (), timeout=110))
     assert res[0] == [True, True, True]
 
 
@@ -181,16 +150,5 @@ def test_prove_distributed_synth_2_20_vs_oracle_digest(world, prepared):
     `world` ranks (cold, and from a DistCircuit) equals the oracle's StarkProof byte for byte
     (the digest tests/test_gpu_large.py pins the single-GPU prover to)."""
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "large_digests.json")))["prove_synth_2^20_steps"]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker_synth20, args=(r, world, port, prepared, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=230) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        if p.is_alive():
-            p.kill()
-        assert p.exitcode == 0
+    res = dict(run_ranks(_worker_synth20, world, (prepared,), timeout=230))
     assert res[0] == want["json_sha256"]
