@@ -725,16 +725,15 @@ def main():
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     plan = S.ntt_plan(log_n)
     passes = len(plan)
-    # The pass kernels of this transform (csrc/ntt.hip: ntt_wave_kernel<COL> for radix-2^8 passes,
-    # ntt_pass_kernel<LOG_R, COL> otherwise; COL = 0 first pass, 2 Shoup t16 column twiddles, 1 the last
-    # pass's full table): per-launch HBM bytes and rocprof times from the committed profile of this exact
-    # command line (tools/profile_round.sh), VALU issue from the committed counter passes over 2^24
-    # transforms alone (tools/pmc_round.sh ... ntt).
+    # The pass kernels of this transform (csrc/ntt.hip ntt_pass_kernel<LOG_R, COL>: COL = 0 first pass,
+    # 2 Shoup t16 column twiddles, 1 the last pass's full table): per-launch HBM bytes and rocprof times
+    # from the committed profile of this exact command line (tools/profile_round.sh), VALU issue from the
+    # committed counter passes over 2^24 transforms alone (tools/pmc_round.sh ... ntt).
     traffic = prof_avg = prof_med = None
     knames, sq = [], {}
     try:
         prof = json.load(open(PROFILE))
-        knames = sorted(k for k in prof["kernels"] if "ntt_pass_kernel" in k or "ntt_wave_kernel" in k)
+        knames = sorted(k for k in prof["kernels"] if "ntt_pass_kernel" in k)
         if log_n == 24 and knames and all(k in prof["pmc_bytes_per_launch"] for k in knames):
             # HBM bytes of one transform: per-launch FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md)
             # summed over the transform's launches.
@@ -746,8 +745,7 @@ def main():
     try:
         if log_n == 24:
             pmc = json.load(open(PMC))["kernels"]
-            sq = {k: v for k, v in pmc.items() if ("ntt_pass_kernel" in k or "ntt_wave_kernel" in k)
-                  and "valu_issue_frac" in v}
+            sq = {k: v for k, v in pmc.items() if "ntt_pass_kernel" in k and "valu_issue_frac" in v}
     except (OSError, KeyError, ValueError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
