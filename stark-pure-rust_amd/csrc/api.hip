@@ -244,6 +244,8 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (stark_merkle_tree* t : ctx->fri_trees) stark_merkle_free(t);
   for (void* p : ctx->pinned)
     if (p) hipHostFree(p);
+  for (auto& kv : ctx->ext_idx)
+    if (kv.second.ptr) hipFree(kv.second.ptr);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde})

@@ -108,6 +108,10 @@ struct stark_ctx {
   size_t pinned_bytes[3] = {0, 0, 0};
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
+  // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
+  // (prove.rs:160-163) at that rank's points: it depends on the trace length only, so every
+  // proof of that size shares it (r1cs.hip ext_index_column).
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, stark::DevBuf> ext_idx;
 };
 
 namespace stark {

@@ -708,6 +708,46 @@ static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint3
   return coset_lde(ctx, coef, batch, out, log_steps, log_prec, 0, 0, tw_g1_inv, tw_g2, tw_g2, s);
 }
 
+__global__ void iota_kernel(fe* __restrict__ out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) fe_store(out + i, fe_from_u64(i));
+}
+
+// ext_indices (prove.rs:160-163): the extension of IDX[i] = i over the rank's points (coset_lde with
+// log_g, r; the whole domain for log_g = r = 0).  It depends on the trace length only, so it is
+// computed on a context's first proof of that size and shared by every later one.  Call it before
+// the proof enqueues work on `s`: a first call synchronises s once.
+static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t log_g,
+                                     uint32_t r, const Twiddles& tw_g1_inv, const Twiddles& tw_g2,
+                                     const Twiddles& tw_h, hipStream_t s, const fe** out) {
+  const auto key = std::make_tuple(log_steps, log_prec, log_g, r);
+  auto it = ctx->ext_idx.find(key);
+  if (it != ctx->ext_idx.end()) {
+    *out = (const fe*)it->second.ptr;
+    return STARK_OK;
+  }
+  const uint64_t steps = (uint64_t)1 << log_steps, P = (uint64_t)1 << (log_prec - log_g);
+  void *col = nullptr, *coef = nullptr;
+  if (hipMalloc(&col, P * sizeof(fe)) != hipSuccess) return STARK_ERR_OOM;
+  if (hipMalloc(&coef, steps * sizeof(fe)) != hipSuccess) {
+    hipFree(col);
+    return STARK_ERR_OOM;
+  }
+  hipLaunchKernelGGL(iota_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (fe*)coef, steps);
+  stark_status st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
+  if (st == STARK_OK)
+    st = coset_lde(ctx, (fe*)coef, 1, (fe*)col, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s);
+  if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
+  hipFree(coef);
+  if (st != STARK_OK) {
+    hipFree(col);
+    return st;
+  }
+  ctx->ext_idx[key] = DevBuf{col, P * sizeof(fe)};
+  *out = (const fe*)col;
+  return STARK_OK;
+}
+
 // The proof's roots (prove.rs:71-94): g2 = 7^((p-1)/precision), g1 = g2^skips = xs[skips], and
 // h = g2^world (the generator of one rank's residue class of the domain), with the twiddle
 // tables of g2, g1^-1 (the LDE's iNTT) and h.
@@ -805,6 +845,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   const Twiddles* tw2 = roots.tw2;
   const Twiddles* tw1i = roots.tw1i;
   const Mont mc = mont();
+  const fe* idx_ext = nullptr;  // the shared extension of IDX (prepared circuits carry their own)
+  if (!pre) STARK_TRY(ext_index_column(ctx, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &idx_ext));
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
   uint64_t* perm;
@@ -812,7 +854,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   Transcript* d_tr;
   const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
   Carve cv;
-  cv.add(&raw, 8 * steps);  // K F0 F1 F2 S P IDX PIDX (then A's coefficients reuse K's slot)
+  cv.add(&raw, 8 * steps);  // K F0 F1 F2 S P PIDX IDX (then A's coefficients reuse K's slot)
   cv.add(&wcopy, steps);
   cv.add(&perm, steps);
   cv.add(&acc_leaves, 5 * steps);
@@ -855,8 +897,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   clk.mark("setup + uploads enqueued");
   STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
+  // (IDX lands in slot 7 and is not extended: idx_ext is the shared extension.)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 7 * steps, raw + 6 * steps, acc_leaves);
   STARK_HIP(ctx, hipGetLastError());
 
   auto proof = std::make_unique<stark_r1cs_proof>();
@@ -868,14 +911,14 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
   if (pre)  // S and P only: K, the flags, IDX and PIDX are the circuit's
     STARK_TRY(lde(ctx, raw + 4 * steps, 2, cols + 4 * prec, log_steps, log_prec, *tw1i, *tw2, s));
-  else
-    STARK_TRY(lde(ctx, raw, 8, cols, log_steps, log_prec, *tw1i, *tw2, s));
+  else  // K F0 F1 F2 S P PIDX
+    STARK_TRY(lde(ctx, raw, 7, cols, log_steps, log_prec, *tw1i, *tw2, s));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(acc_tree),
                      (uint32_t)(prec - 1), mc.r2, d_tr);
   STARK_HIP(ctx, hipGetLastError());
   // A (utils.rs:293-339, prove.rs:183-184).
-  const fe* ext_idx = pre ? pre + 4 * prec : cols + 6 * prec;
-  const fe* ext_pidx = pre ? pre + 5 * prec : cols + 7 * prec;
+  const fe* ext_idx = pre ? pre + 4 * prec : idx_ext;
+  const fe* ext_pidx = pre ? pre + 5 * prec : cols + 6 * prec;
   hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
                      (const fe*)ext_pidx, (const uint64_t*)nullptr, (uint64_t)0, (const fe*)wcopy, steps,
                      (const Transcript*)d_tr, mc.r2, nmr, dnm);
@@ -899,11 +942,10 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // Constraint kernel.
   ConstraintArgs ca;
   for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * prec;
-  if (pre) {
+  ca.col[6] = ext_idx;
+  ca.col[7] = ext_pidx;
+  if (pre)
     for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * prec;
-    ca.col[6] = pre + 4 * prec;
-    ca.col[7] = pre + 5 * prec;
-  }
   ca.inv_zb = pre ? pre + 6 * prec : inv_zb;
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
@@ -1072,7 +1114,17 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                        raw + steps);
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
-    st = coset_lde(ctx, raw, 6, (fe*)out.ptr, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+    // K F0 F1 F2, then PIDX; IDX is the shared extension (ext_index_column), copied into its slot.
+    const fe* idx_ext = nullptr;
+    st = ext_index_column(ctx, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext);
+    if (st == STARK_OK)
+      st = coset_lde(ctx, raw, 4, (fe*)out.ptr, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+    if (st == STARK_OK)
+      st = coset_lde(ctx, raw + 5 * steps, 1, (fe*)out.ptr + 5 * P, log_steps, log_prec, log_g, rank, *tw1i, *tw2,
+                     *twh, s);
+    if (st == STARK_OK && hipMemcpyAsync((fe*)out.ptr + 4 * P, idx_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) !=
+                              hipSuccess)
+      st = STARK_ERR_HIP;
     // Zb2 = prod_k (x - x_k), Zb3 = x - x_last (utils.rs:438-474) and their inverses (0 -> 0).
     const uint64_t skips = prec / steps;
     std::vector<fe> xk(n_pfi + 1);
@@ -1221,6 +1273,8 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   memcpy(d.g2c, roots.g2c, 32);
   const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   const Mont mc = mont();
+  const fe* idx_ext = nullptr;  // this rank's share of the extension of IDX (shared across proofs)
+  if (!pre) STARK_TRY(ext_index_column(ctx, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext));
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts;
   uint64_t* perm;
@@ -1266,16 +1320,17 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(d.d_tr, 0, sizeof(Transcript), s));
+  // (PIDX in slot 6, IDX in slot 7, not extended: idx_ext)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, raw + 7 * steps, acc_leaves);
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 7 * steps, raw + 6 * steps, acc_leaves);
   STARK_HIP(ctx, hipGetLastError());
   // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
   STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
   STARK_TRY(merkle_build(ctx, d.acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
   if (pre)
     STARK_TRY(lde_coset(d, raw + 4 * steps, 2, cols + 4 * P, *tw1i, *tw2, *twh));
-  else
-    STARK_TRY(lde_coset(d, raw, 8, cols, *tw1i, *tw2, *twh));
+  else  // K F0 F1 F2 S P PIDX
+    STARK_TRY(lde_coset(d, raw, 7, cols, *tw1i, *tw2, *twh));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
                      (uint32_t)(prec - 1), mc.r2, d.d_tr);
   STARK_HIP(ctx, hipGetLastError());
@@ -1301,11 +1356,10 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   ConstraintArgs ca;
   for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * P;
   ca.inv_zb = pre ? pre + 6 * P : inv_zb;
-  if (pre) {
+  ca.col[6] = pre ? pre + 4 * P : idx_ext;
+  ca.col[7] = pre ? pre + 5 * P : cols + 6 * P;
+  if (pre)
     for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * P;
-    ca.col[6] = pre + 4 * P;
-    ca.col[7] = pre + 5 * P;
-  }
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
   ca.lo = tw2->d_lo;
