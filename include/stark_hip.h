@@ -217,6 +217,9 @@ stark_status stark_mk_r1cs_proof(stark_ctx* ctx, const uint64_t* witness_trace, 
                                  size_t n_constraints, size_t n_wires, stark_r1cs_proof** out);
 /* serde_json::to_string(&StarkProof<BlakeDigest>) (utils.rs:122-130, run.rs:549). */
 stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, size_t cap, size_t* len);
+/* The same text without a copy: *data points into the proof (NUL-terminated, *len bytes) and stays
+ * valid until stark_r1cs_proof_free(proof). */
+stark_status stark_r1cs_proof_json_view(const stark_r1cs_proof* proof, const char** data, size_t* len);
 stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_root[32], uint8_t l_root[32],
                                     uint8_t a_root[32]);
 /* StarkProof's openings (utils.rs:122-130): which = 0 main_branches (k = 320, 256-B leaves),

@@ -246,6 +246,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
     if (p) hipHostFree(p);
   for (auto& kv : ctx->ext_idx)
     if (kv.second.ptr) hipFree(kv.second.ptr);
+  if (ctx->staged) hipEventDestroy(ctx->staged);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde})

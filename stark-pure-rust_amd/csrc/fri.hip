@@ -17,6 +17,7 @@
 // reference's, with 7 modular products per row and no batch inverse.
 #include <string.h>
 
+#include <algorithm>
 #include <array>
 #include <string>
 
@@ -338,21 +339,48 @@ void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, c
   text("]");
 }
 
-void JsonPieces::render(std::string& o) {
-  std::vector<std::string> out(fns.size());
+// Renders every piece into its own string on up to 8 host workers.
+static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, std::vector<std::string>& out) {
+  out.assign(fns.size(), std::string());
   std::atomic<size_t> next{0};
-  auto work = [&] {
-    for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
-  };
   unsigned nt = host_threads();
   if (nt > 8) nt = 8;
   if (fns.size() < 8) nt = 1;
-  host_parallel(nt, [&](unsigned) { work(); });
+  host_parallel(nt, [&](unsigned) {
+    for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
+  });
+  fns.clear();
+}
+
+void JsonPieces::render(std::string& o) {
+  std::vector<std::string> out;
+  render_pieces(fns, out);
   size_t total = o.size();
   for (const std::string& x : out) total += x.size();
   o.reserve(total);
   for (const std::string& x : out) o += x;
-  fns.clear();
+}
+
+void JsonPieces::render(JsonText& o) {
+  std::vector<std::string> out;
+  render_pieces(fns, out);
+  std::vector<size_t> off(out.size() + 1, 0);
+  for (size_t i = 0; i < out.size(); ++i) off[i + 1] = off[i] + out[i].size();
+  o.n = off.back();
+  o.p.reset(new char[o.n + 1]);  // uninitialised; its pages fault in on the threads that copy
+  o.p[o.n] = 0;
+  char* dst = o.p.get();
+  // contiguous runs of pieces of about equal bytes per worker
+  unsigned nt = host_threads();
+  if (nt > 8) nt = 8;
+  if (o.n < ((size_t)1 << 20)) nt = 1;
+  host_parallel(nt, [&](unsigned t) {
+    const size_t lo = o.n * t / nt, hi = o.n * (t + 1) / nt;
+    for (size_t i = std::upper_bound(off.begin(), off.end(), lo) - off.begin() - 1; i < out.size() && off[i] < hi; ++i) {
+      const size_t a = std::max(off[i], lo), b = std::min(off[i + 1], hi);
+      if (b > a) memcpy(dst + a, out[i].data() + (a - off[i]), b - a);
+    }
+  });
 }
 
 // serde_json of Vec<FriProof<BlakeDigest>> (fri.rs:16-26) as pieces.

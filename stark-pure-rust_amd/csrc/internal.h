@@ -104,8 +104,9 @@ struct stark_ctx {
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<stark_merkle_tree*> fri_trees;  // one per FRI layer (+ the input's), reused across proofs
   stark::DevBuf fri_misc;                     // per-layer special_x (device transcript)
-  void* pinned[3] = {nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
-  size_t pinned_bytes[3] = {0, 0, 0};
+  void* pinned[4] = {nullptr, nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
+  size_t pinned_bytes[4] = {0, 0, 0, 0};
+  hipEvent_t staged = nullptr;  // the last DMA out of pinned slot 3 (r1cs_trace_dev.hip staged_upload)
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
   // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
@@ -126,7 +127,7 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
 // Context-owned pinned host scratch of at least `bytes` (async copy target).
 // Slot 0: gather batches; slot 1: transcript values and roots; slot 2: the device trace builder's
-// record-walk tables.
+// record-walk tables; slot 3: its upload staging (the raw .r1cs constraint section and witness).
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
 
 // Host worker threads shared by the host-side stages (trace build, proof
@@ -178,6 +179,15 @@ struct GatherReq {
 // All requests in one pinned upload, one download, one synchronisation.
 stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream);
 
+// A rendered JSON text: one uninitialised allocation written once (a std::string would be
+// zero-filled first), so a multi-MB proof is assembled by several threads in parallel.
+struct JsonText {
+  std::unique_ptr<char[]> p;
+  size_t n = 0;
+  const char* data() const { return p.get(); }
+  size_t size() const { return n; }
+};
+
 // serde_json text rendered in pieces on a few host threads, then
 // concatenated in order (fri.hip).
 struct JsonPieces {
@@ -187,6 +197,7 @@ struct JsonPieces {
   void branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes, size_t k,
                 size_t depth);
   void render(std::string& o);
+  void render(JsonText& o);  // pieces rendered and copied to their offsets on the host workers
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
 

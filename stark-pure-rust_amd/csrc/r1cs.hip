@@ -39,7 +39,7 @@ void fri_proof_json_string(const stark_fri_proof* proof, std::string& o);
 
 struct stark_r1cs_proof {
   uint8_t m_root[32], l_root[32], a_root[32];
-  std::string json;
+  stark::JsonText json;
   // The parts, for callers that build their own StarkProof value (stark_r1cs_proof_branches / _fri):
   // main and linear-combination openings (leaves, then depth siblings per opening, leaf to root).
   size_t depth = 0;
@@ -1039,7 +1039,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   clk.mark("indices + gather batch");
   proof->fri = fri;  // owned by the proof from here on
   // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
-  std::string& o = proof->json;
+  JsonText& o = proof->json;
   JsonPieces j;
   j.text("{\"m_root\":");
   j.bytes(proof->m_root, 32);
@@ -1431,6 +1431,13 @@ stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, siz
     memcpy(buf, proof->json.data(), k);
     if (k < cap) buf[k] = 0;
   }
+  return STARK_OK;
+}
+
+stark_status stark_r1cs_proof_json_view(const stark_r1cs_proof* proof, const char** data, size_t* len) {
+  if (!proof || !data || !len) return STARK_ERR_BAD_ARG;
+  *data = proof->json.data();
+  *len = proof->json.size();
   return STARK_OK;
 }
 

@@ -17,6 +17,8 @@
 // device and reported as STARK_ERR_BAD_ARG, like the host builder.
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -216,6 +218,60 @@ stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, st
 
 }  // namespace
 
+// Host-to-device copies of caller (pageable) memory through the context's pinned staging buffer:
+// the copy is split in 2 MB chunks that `workers` host threads memcpy into the staging buffer, each
+// thread enqueueing the DMA of a chunk as soon as it is staged, so the DMAs overlap the memcpys.  A
+// pageable hipMemcpyAsync blocks the caller and stages through the runtime's own small buffers.
+// Returns once every DMA is enqueued on s; ctx->staged marks their completion, which the next call
+// waits for before it writes the staging buffer again.
+struct Upload {
+  void* dst;
+  const void* src;
+  size_t len;
+};
+static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups, hipStream_t s, unsigned workers,
+                                  const std::function<void()>& beside) {
+  constexpr size_t kChunk = (size_t)2 << 20;
+  size_t total = 0;
+  for (const Upload& u : ups) total += u.len;
+  if (!ctx->staged) STARK_HIP(ctx, hipEventCreateWithFlags(&ctx->staged, hipEventDisableTiming));
+  STARK_HIP(ctx, hipEventSynchronize(ctx->staged));  // the previous call's DMAs have left the buffer
+  uint8_t* stage = nullptr;
+  stark_status st = ctx_pinned(ctx, 3, total, (void**)&stage);
+  if (st != STARK_OK) return st;
+  struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint8_t* stage;
+    size_t len;
+  };
+  std::vector<Piece> pieces;
+  size_t at = 0;
+  for (const Upload& u : ups)
+    for (size_t o = 0; o < u.len; o += kChunk) {
+      const size_t len = std::min(kChunk, u.len - o);
+      pieces.push_back({(uint8_t*)u.dst + o, (const uint8_t*)u.src + o, stage + at, len});
+      at += len;
+    }
+  std::atomic<size_t> next{0};
+  std::atomic<int> failed{0};
+  // thread 1 runs `beside` (the record walk); every other thread stages chunks in order of claim
+  host_parallel(workers + 1, [&](unsigned t) {
+    if (t == 1) {
+      beside();
+      return;
+    }
+    for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+      const Piece& p = pieces[i];
+      memcpy(p.stage, p.src, p.len);
+      if (hipMemcpyAsync(p.dst, p.stage, p.len, hipMemcpyHostToDevice, s) != hipSuccess) failed = 1;
+    }
+  });
+  if (failed) return hip_fail(ctx, hipGetLastError(), "r1cs/wtns upload");
+  STARK_HIP(ctx, hipEventRecord(ctx->staged, s));
+  return STARK_OK;
+}
+
 stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
                                size_t wtns_len, DevTrace* out) {
   PhaseClock clk("r1cs trace build (device)");
@@ -258,17 +314,11 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   if (st != STARK_OK) return st;
   uint8_t* RAW = (uint8_t*)ctx->trace_raw.ptr;
   hipStream_t s = ctx->stream;
-  stark_status walk_st = STARK_OK, up_st = STARK_OK;
-  host_parallel(2, [&](unsigned t) {
-    if (t == 1) {
-      walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
-      return;
-    }
-    if (hipMemcpyAsync(RAW, cons, cons_len, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(RAW + o_raw_w, wv, wbytes, hipMemcpyHostToDevice, s) != hipSuccess)
-      up_st = STARK_ERR_HIP;
-  });
-  if (up_st != STARK_OK) return hip_fail(ctx, hipGetLastError(), "r1cs/wtns upload");
+  stark_status walk_st = STARK_OK;
+  const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
+  st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers,
+                     [&] { walk_st = walk_records_into(cons, cons_len, n_c, fac, base); });
+  if (st != STARK_OK) return st;
   if (walk_st != STARK_OK) return walk_st;
   const uint64_t a_len = base[n_c];
   const uint64_t os = 3 * a_len;

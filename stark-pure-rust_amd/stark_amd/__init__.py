@@ -85,6 +85,7 @@ _SIGNATURES = {
                              _szp, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_size_t,
                              ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_proof_json": ([_vp, ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
+    "stark_r1cs_proof_json_view": ([_vp, ctypes.POINTER(ctypes.c_void_p), _szp], ctypes.c_int),
     "stark_r1cs_proof_roots": ([_vp, _u8p, _u8p, _u8p], ctypes.c_int),
     "stark_r1cs_proof_branches": ([_vp, ctypes.c_int, _szp, _szp, _szp, _u8p, _u8p], ctypes.c_int),
     "stark_r1cs_proof_fri": ([_vp], _vp),

@@ -17,6 +17,16 @@ import numpy as np
 
 from . import Context, StarkError, _elems, _p64, _szp, _vp, load_library
 
+# PyUnicode_DecodeASCII(const char*, Py_ssize_t, errors): one pass from the library's buffer to a str.
+_decode_ascii = ctypes.pythonapi.PyUnicode_DecodeASCII
+_decode_ascii.restype = ctypes.py_object
+_decode_ascii.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_char_p]
+
+
+def ascii_at(ptr: int, n: int) -> str:
+    """The n ASCII bytes at address ptr as a str (UnicodeDecodeError on a non-ASCII byte)."""
+    return _decode_ascii(ptr, n, None) if n else ""
+
 
 class StarkProof:
     """StarkProof<BlakeDigest> held by the library (r1cs-stark/src/utils.rs:122-130)."""
@@ -33,12 +43,12 @@ class StarkProof:
             pass
 
     def to_json(self) -> str:
-        """serde_json::to_string(&proof) (run.rs:549)."""
+        """serde_json::to_string(&proof) (run.rs:549), decoded straight from the proof's own
+        text (stark_r1cs_proof_json_view: no intermediate buffers for a multi-MB proof)."""
+        p = ctypes.c_void_p()
         n = ctypes.c_size_t(0)
-        self.lib.stark_r1cs_proof_json(self.h, None, 0, ctypes.byref(n))
-        buf = ctypes.create_string_buffer(n.value + 1)
-        self.lib.stark_r1cs_proof_json(self.h, buf, n.value + 1, ctypes.byref(n))
-        return buf.raw[:n.value].decode()
+        self.lib.stark_r1cs_proof_json_view(self.h, ctypes.byref(p), ctypes.byref(n))
+        return ascii_at(p.value, n.value)
 
     def roots(self) -> dict:
         m, l, a = (ctypes.create_string_buffer(32) for _ in range(3))

@@ -72,3 +72,16 @@ def test_no_gpu_fails_loudly():
             "else:\n    print('gpu')\n") % os.path.join(os.path.dirname(HERE), "stark-pure-rust_amd")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120).stdout
     assert out.strip() in ("refused 6", "gpu")
+
+
+def test_json_view_decode():
+    """StarkProof.to_json decodes the library's JSON text in place (stark_r1cs_proof_json_view)."""
+    import ctypes
+    from stark_amd.r1cs import ascii_at
+    text = '{"m_root":[1,2,3],"x":[255,0]}' * 1000
+    buf = ctypes.create_string_buffer(text.encode())
+    assert ascii_at(ctypes.addressof(buf), len(text)) == text
+    assert ascii_at(ctypes.addressof(buf), 0) == ""
+    bad = ctypes.create_string_buffer(b"[1,\xff]")
+    with pytest.raises(UnicodeDecodeError):
+        ascii_at(ctypes.addressof(bad), 5)
