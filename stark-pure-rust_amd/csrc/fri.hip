@@ -339,12 +339,12 @@ void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, c
   text("]");
 }
 
-// Renders every piece into its own string on up to 8 host workers.
+// Renders every piece into its own string on the host workers.
 static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, std::vector<std::string>& out) {
   out.assign(fns.size(), std::string());
   std::atomic<size_t> next{0};
   unsigned nt = host_threads();
-  if (nt > 8) nt = 8;
+  if (nt > 16) nt = 16;
   if (fns.size() < 8) nt = 1;
   host_parallel(nt, [&](unsigned) {
     for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
@@ -372,7 +372,7 @@ void JsonPieces::render(JsonText& o) {
   char* dst = o.p.get();
   // contiguous runs of pieces of about equal bytes per worker
   unsigned nt = host_threads();
-  if (nt > 8) nt = 8;
+  if (nt > 16) nt = 16;
   if (o.n < ((size_t)1 << 20)) nt = 1;
   host_parallel(nt, [&](unsigned t) {
     const size_t lo = o.n * t / nt, hi = o.n * (t + 1) / nt;

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -44,11 +45,26 @@ struct ProofIn {
   std::vector<FriIn> fri;
 };
 
+class Json;
+
+// Merkle openings parsed ahead of the sequential reader, in parallel: every `{"leaf":` of the text
+// starts a Branch object (leaf and node contents are numbers, so the key occurs nowhere else), and
+// serde_json writes no whitespace.  The reader takes a pre-parsed Branch only when it reaches that
+// exact offset itself, so the result is the sequential parse.
+struct PreBranches {
+  std::vector<size_t> off, end;
+  std::vector<Branch> br;
+  std::vector<uint8_t> good;
+  size_t next = 0;
+};
+
 // A reader for exactly this schema: objects with string keys, arrays, u8 numbers.
 class Json {
  public:
-  Json(const char* s, size_t n) : p_(s), e_(s + n) {}
+  Json(const char* s, size_t n, PreBranches* pre = nullptr) : p_(s), e_(s + n), base_(s), pre_(pre) {}
+  Json(const char* base, size_t n, size_t at) : p_(base + at), e_(base + n), base_(base) {}
   bool ok = true;
+  size_t pos() const { return (size_t)(p_ - base_); }
 
   bool accept(char c) {
     ws();
@@ -144,7 +160,7 @@ class Json {
     if (!ok || accept(']')) return;
     do {
       v.emplace_back();
-      branch(v.back());
+      if (!take_pre(v.back())) branch(v.back());
     } while (ok && accept(','));
     expect(']');
   }
@@ -220,10 +236,63 @@ class Json {
   void ws() {
     while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
   }
+  // The pre-parsed Branch starting exactly here, if any (offsets ascend with the reader).
+  bool take_pre(Branch& b) {
+    if (!pre_) return false;
+    ws();
+    const size_t at = pos();
+    PreBranches& P = *pre_;
+    while (P.next < P.off.size() && P.off[P.next] < at) ++P.next;
+    if (P.next == P.off.size() || P.off[P.next] != at) return false;
+    const size_t i = P.next++;
+    if (!P.good[i]) {
+      ok = false;
+      return true;
+    }
+    b = std::move(P.br[i]);
+    p_ = base_ + P.end[i];
+    return true;
+  }
   const char* p_;
   const char* e_;
+  const char* base_;
+  PreBranches* pre_ = nullptr;
   std::vector<uint8_t> tmp_;
 };
+
+// Finds every Branch start and parses each from its offset on the host workers.
+void pre_parse_branches(const char* s, size_t n, PreBranches& P) {
+  static const char kKey[] = "{\"leaf\":";
+  const size_t klen = sizeof(kKey) - 1;
+  const unsigned parts = n < ((size_t)1 << 18) ? 1u : host_threads();
+  std::vector<std::vector<size_t>> found(parts);
+  host_parallel(parts, [&](unsigned t) {
+    const size_t lo = n * t / parts, hi = n * (t + 1) / parts;  // starts in [lo, hi)
+    const char* p = s + lo;
+    const char* end = s + std::min(n, hi + klen - 1);
+    while (p < end) {
+      const void* q = memmem(p, (size_t)(end - p), kKey, klen);
+      if (!q) break;
+      found[t].push_back((size_t)((const char*)q - s));
+      p = (const char*)q + 1;
+    }
+  });
+  for (auto& f : found) P.off.insert(P.off.end(), f.begin(), f.end());
+  const size_t k = P.off.size();
+  P.end.assign(k, 0);
+  P.good.assign(k, 0);
+  P.br.assign(k, Branch());
+  std::atomic<size_t> next{0};
+  host_parallel(std::min<unsigned>(host_threads(), (unsigned)((k + 15) / 16)), [&](unsigned) {
+    for (size_t c; (c = next.fetch_add(16)) < k;)
+      for (size_t i = c; i < std::min(k, c + 16); ++i) {
+        Json j(s, n, P.off[i]);
+        j.branch(P.br[i]);
+        P.good[i] = j.ok;
+        P.end[i] = j.pos();
+      }
+  });
+}
 
 // ---- field helpers ----
 
@@ -407,6 +476,7 @@ uint32_t log2_ceil_ref(size_t v) {  // log2_ceil (r1cs-stark/src/utils.rs:14-23)
 static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const uint8_t* pub_bytes, size_t n_public,
                                 const ProofIn& pr) {
   const FieldHost& F = FieldHost::get();
+  PhaseClock clk("verify_r1cs_proof");
   if (c.world != 1) return STARK_ERR_BAD_ARG;
   // The reference builds its boundary points from every supplied wire (run.rs:503-509); a prepared
   // circuit holds the first uses of the header's 1 + n_pub_in + n_pub_out wires only, so any other
@@ -427,6 +497,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
   // FRI on the linear combination (verify.rs:80-84).
   stark_status st = verify_fri(pr.l_root, g2, pr.fri, prec / 4, (uint32_t)skips);
   if (st != STARK_OK) return st;
+  clk.mark("FRI layers");
   // Spot checks (verify.rs:86-118).
   std::vector<size_t> positions, aug;
   if (!sampler(pr.l_root, prec, 80, (uint32_t)skips, positions)) return STARK_ERR_CHECK;
@@ -438,6 +509,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
   }
   if (!branches_valid(pr.m_root, aug, pr.main) || !branches_valid(pr.l_root, positions, pr.lcomb))
     return STARK_ERR_CHECK;
+  clk.mark("main + L Merkle paths");
   for (size_t i = 0; i < aug.size(); ++i)
     if (pr.main[i].leaf.size() < 256) return STARK_ERR_CHECK;  // m_branch[k] chunks (verify.rs:185-200)
   // K, F0-F2, IDX, PIDX at the positions: the circuit's extensions (K, F0-F2 stored as Montgomery
@@ -452,6 +524,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     st = stark_open_batch(ctx, req, 6, nullptr);
     if (st != STARK_OK) return st;
   }
+  clk.mark("extension values gathered");
   auto col_val = [&](int k, size_t i) {
     HostFp v;
     memcpy(v.v, got.data() + ((size_t)k * n_pos + i) * 32, 32);
@@ -536,6 +609,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     l = F.add(l, F.mul(kk[10], s_x));
     if (!FieldHost::eq(fe_from_bytes(pr.lcomb[i].leaf), l)) return STARK_ERR_CHECK;
   }
+  clk.mark("spot checks");
   return STARK_OK;
 }
 
@@ -580,10 +654,15 @@ stark_status stark_verify_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit*
   if (!ctx || !circuit || circuit->ctx != ctx || !public_wires || !proof_json || n_public == 0)
     return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
+  PhaseClock clk("verify: read proof");
   ProofIn pr;
-  Json j(proof_json, json_len);
+  PreBranches pre;
+  pre_parse_branches(proof_json, json_len, pre);
+  clk.mark("openings parsed (parallel)");
+  Json j(proof_json, json_len, &pre);
   j.stark_proof(pr);
   if (!j.ok) return STARK_ERR_BAD_ARG;  // serde_json::from_reader fails (run.rs:579)
+  clk.mark("StarkProof JSON parsed");
   return verify_r1cs(ctx, circuit->c, public_wires, n_public, pr);
 }
 
@@ -598,8 +677,10 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
   circ.ctx = ctx;
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
+  PhaseClock clk("verify: circuit");
   stark_status st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
   hipStreamSynchronize(ctx->stream);
+  clk.mark("circuit build");
   if (st == STARK_OK) st = stark_verify_r1cs_circuit(ctx, &circ, public_wires, n_public, proof_json, json_len);
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
