@@ -329,21 +329,25 @@ bool branch_valid(const uint8_t root[32], size_t index, const Branch& b) {
   return memcmp(cur, root, 32) == 0;
 }
 
-// Proof::validate (merkle_tree.rs:25-43) for each (index, proof) pair; verify_multi_branch
-// (:46-58) zips, so every index needs its proof.  The paths are checked on the host workers.
-bool branches_valid(const uint8_t root[32], const std::vector<size_t>& idx, const std::vector<Branch>& br) {
-  if (br.size() < idx.size()) return false;
-  const size_t k = idx.size();
-  const unsigned parts = (unsigned)std::min<size_t>(host_threads(), (k + 31) / 32);
-  if (parts <= 1) {
-    for (size_t i = 0; i < k; ++i)
-      if (!branch_valid(root, idx[i], br[i])) return false;
-    return true;
-  }
-  std::vector<uint8_t> good(parts, 1);
-  host_parallel(parts, [&](unsigned t) {
-    for (size_t i = k * t / parts; i < k * (t + 1) / parts; ++i)
-      if (!branch_valid(root, idx[i], br[i])) {
+// Proof::validate (merkle_tree.rs:25-43) for many (root, index, opening) triples of different trees
+// in one pass over the host workers, split by node count (verify_multi_branch, :46-58, zips indices
+// and openings: the callers check that every index has one).
+struct PathCheck {
+  const uint8_t* root;
+  size_t index;
+  const Branch* b;
+};
+bool paths_valid(const std::vector<PathCheck>& v) {
+  std::vector<size_t> cost(v.size() + 1, 0);
+  for (size_t i = 0; i < v.size(); ++i) cost[i + 1] = cost[i] + 1 + v[i].b->nodes.size() / 32;
+  const unsigned parts = (unsigned)std::min<size_t>(host_threads(), (v.size() + 31) / 32);
+  std::vector<uint8_t> good(std::max(parts, 1u), 1);
+  host_parallel(std::max(parts, 1u), [&](unsigned t) {
+    const unsigned np = std::max(parts, 1u);
+    const size_t lo = std::lower_bound(cost.begin(), cost.end(), cost.back() * t / np) - cost.begin();
+    const size_t hi = std::lower_bound(cost.begin(), cost.end(), cost.back() * (t + 1) / np) - cost.begin();
+    for (size_t i = lo; i < hi && i < v.size(); ++i)
+      if (!branch_valid(v[i].root, v[i].index, *v[i].b)) {
         good[t] = 0;
         return;
       }
@@ -378,17 +382,43 @@ stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std
   if (rou_deg >= 4)
     for (int j = 1; j < 4; ++j) quartic[j] = F.pow_u64(root, rou_deg / 4 * (uint64_t)j);
   const HostFp inv4 = F.inv(F.from_u64(4));
+  // Every layer's indices follow from the proof's own roots, so all the layers' Merkle paths are
+  // checked first, in one parallel pass (the reference checks them layer by layer, fri.rs:288-316;
+  // the accept/reject outcome is the same).  A layer whose shape the reference would reject before
+  // its paths keeps that order: the pass stops at it.
+  std::vector<std::vector<size_t>> ys_l, pos_l;
+  {
+    std::vector<PathCheck> checks;
+    const uint8_t* root_l = merkle_root_in;
+    uint64_t deg = rou_deg;
+    for (size_t l = 0; l + 1 < proof.size(); ++l) {
+      const FriIn& L = proof[l];
+      if (L.last || deg < 4) break;  // reported in order below
+      std::vector<size_t> ys, poly_pos;
+      if (!sampler(L.root2, deg / 4, 40, excl, ys)) break;
+      for (size_t y : ys)
+        for (size_t j = 0; j < 4; ++j) poly_pos.push_back(j * (deg / 4) + y);
+      if (L.col.size() < ys.size() || L.poly.size() < poly_pos.size()) return STARK_ERR_CHECK;  // zip (:46-58)
+      ys_l.push_back(std::move(ys));
+      pos_l.push_back(std::move(poly_pos));
+      deg /= 4;
+      root_l = L.root2;
+    }
+    root_l = merkle_root_in;
+    for (size_t l = 0; l < ys_l.size(); ++l) {
+      const FriIn& L = proof[l];
+      for (size_t i = 0; i < ys_l[l].size(); ++i) checks.push_back({L.root2, ys_l[l][i], &L.col[i]});
+      for (size_t i = 0; i < pos_l[l].size(); ++i) checks.push_back({root_l, pos_l[l][i], &L.poly[i]});
+      root_l = L.root2;
+    }
+    if (!paths_valid(checks)) return STARK_ERR_CHECK;
+  }
   for (size_t l = 0; l + 1 < proof.size(); ++l) {
     const FriIn& L = proof[l];
     if (L.last) return STARK_ERR_BAD_ARG;  // "FRI proofs must consist of FriProof::Middle except the last element."
     const HostFp special_x = F.from_bytes_le(m_root, 32);
-    const size_t q = rou_deg / 4;
-    std::vector<size_t> ys;
-    if (!sampler(L.root2, q, 40, excl, ys)) return STARK_ERR_CHECK;  // get_pseudorandom_indices panics
-    std::vector<size_t> poly_pos;
-    for (size_t y : ys)
-      for (size_t j = 0; j < 4; ++j) poly_pos.push_back(j * q + y);
-    if (!branches_valid(L.root2, ys, L.col) || !branches_valid(m_root, poly_pos, L.poly)) return STARK_ERR_CHECK;
+    if (l >= ys_l.size()) return STARK_ERR_CHECK;  // get_pseudorandom_indices panics
+    const std::vector<size_t>& ys = ys_l[l];
     // x1 = root^y per row and 1 / x1^3 for all rows with one inversion (Montgomery's trick).
     const size_t k_rows = ys.size();
     std::vector<HostFp> x1s(k_rows), inv_x13(k_rows), pre(k_rows + 1);
@@ -507,8 +537,13 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     aug.push_back((j + os / 3 * skips) % prec);
     aug.push_back((j + os / 3 * 2 * skips) % prec);
   }
-  if (!branches_valid(pr.m_root, aug, pr.main) || !branches_valid(pr.l_root, positions, pr.lcomb))
-    return STARK_ERR_CHECK;
+  if (pr.main.size() < aug.size() || pr.lcomb.size() < positions.size()) return STARK_ERR_CHECK;  // zip
+  {
+    std::vector<PathCheck> checks;
+    for (size_t i = 0; i < aug.size(); ++i) checks.push_back({pr.m_root, aug[i], &pr.main[i]});
+    for (size_t i = 0; i < positions.size(); ++i) checks.push_back({pr.l_root, positions[i], &pr.lcomb[i]});
+    if (!paths_valid(checks)) return STARK_ERR_CHECK;
+  }
   clk.mark("main + L Merkle paths");
   for (size_t i = 0; i < aug.size(); ++i)
     if (pr.main[i].leaf.size() < 256) return STARK_ERR_CHECK;  // m_branch[k] chunks (verify.rs:185-200)
@@ -567,7 +602,8 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     for (int b = 0; b < 32; ++b) le[b] = h[31 - b];  // from_str of the big-endian integer
     kk[i] = F.from_bytes_le(le, 32);
   }
-  for (size_t i = 0; i < positions.size(); ++i) {
+  // The 80 spot checks are independent: checked on the host workers.
+  auto spot = [&](size_t i) -> bool {
     const HostFp x = F.pow_u64(g2, positions[i]);
     auto leaf = [&](int b, int chunk) {
       std::vector<uint8_t> v(pr.main[4 * i + b].leaf.begin() + 32 * chunk,
@@ -582,18 +618,18 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     const HostFp ext_idx = col_val(4, i), ext_pidx = col_val(5, i);
     // Q1 = Z D1, Q2 = Z D2 (verify.rs:208-219)
     if (!FieldHost::eq(F.mul(f0, F.sub(F.sub(p_x, F.mul(f1, p_prev)), F.mul(k_x, s_x))), F.mul(z, d1)))
-      return STARK_ERR_CHECK;
-    if (!FieldHost::eq(F.mul(f2, F.sub(p_2w, F.mul(p_x, p_w))), F.mul(z, d2))) return STARK_ERR_CHECK;
+      return false;
+    if (!FieldHost::eq(F.mul(f2, F.sub(p_2w, F.mul(p_x, p_w))), F.mul(z, d2))) return false;
     // Q3 = Z D3 (verify.rs:221-225)
     const HostFp rs = F.mul(r[2], s_x);
     const HostFp nmr = F.add(F.add(r[0], F.mul(r[1], ext_idx)), rs);
     const HostFp dnm = F.add(F.add(r[0], F.mul(r[1], ext_pidx)), rs);
-    if (!FieldHost::eq(F.sub(F.mul(a_x, dnm), F.mul(a_prev, nmr)), F.mul(z, d3))) return STARK_ERR_CHECK;
+    if (!FieldHost::eq(F.sub(F.mul(a_x, dnm), F.mul(a_prev, nmr)), F.mul(z, d3))) return false;
     // Boundary constraints (verify.rs:227-238)
     HostFp zb2 = F.one();
     for (const HostFp& xk : bx) zb2 = F.mul(zb2, F.sub(x, xk));
-    if (!FieldHost::eq(F.sub(s_x, eval_poly(interp2, x)), F.mul(zb2, b2))) return STARK_ERR_CHECK;
-    if (!FieldHost::eq(F.sub(a_x, eval_poly(interp3, x)), F.mul(F.sub(x, x_last), b3))) return STARK_ERR_CHECK;
+    if (!FieldHost::eq(F.sub(s_x, eval_poly(interp2, x)), F.mul(zb2, b2))) return false;
+    if (!FieldHost::eq(F.sub(a_x, eval_poly(interp3, x)), F.mul(F.sub(x, x_last), b3))) return false;
     // The linear combination (verify.rs:240-254)
     const HostFp xs = F.pow_u64(x, steps);
     HostFp l = F.mul(kk[0], d1);
@@ -607,8 +643,16 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     l = F.add(l, F.mul(F.mul(kk[8], b3), xs));
     l = F.add(l, F.mul(kk[9], a_x));
     l = F.add(l, F.mul(kk[10], s_x));
-    if (!FieldHost::eq(fe_from_bytes(pr.lcomb[i].leaf), l)) return STARK_ERR_CHECK;
-  }
+    if (!FieldHost::eq(fe_from_bytes(pr.lcomb[i].leaf), l)) return false;
+    return true;
+  };
+  std::vector<uint8_t> spot_ok(positions.size(), 0);
+  std::atomic<size_t> next_spot{0};
+  host_parallel(std::min<unsigned>(host_threads(), (unsigned)((positions.size() + 4) / 5)), [&](unsigned) {
+    for (size_t i; (i = next_spot.fetch_add(1)) < positions.size();) spot_ok[i] = spot(i);
+  });
+  for (uint8_t g : spot_ok)
+    if (!g) return STARK_ERR_CHECK;
   clk.mark("spot checks");
   return STARK_OK;
 }
