@@ -65,7 +65,9 @@ constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
 
 // Which radix-4 steps multiply by the digit-basis product (fe_db.h), radices 2^4..2^8:
 //   * every step before the pass's last one: constants w_R^(4k), k < R/8 (32 for R = 256, 9 KB of
-//     LDS, staged once per workgroup);
+//     LDS, staged once per workgroup).  Where a wave's constant is uniform (the peeled step's w_4 and
+//     the jj-major first twiddled step) its table is read from the global one into SGPRs instead
+//     (scalar loads; the column sums take it as the SGPR operand of v_mad_u64_u32): no LDS reads;
 //   * the last step too for radices <= 2^7: once the step has read its inputs, all R/2 constants
 //     (L2-resident, <= 18 KB) are staged over the data image (two more barriers per tile).  For R = 2^8
 //     (36 KB) that measured slower, so its last step multiplies by Shoup pairs staged in LDS (8 KB).
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
       fe t3;
       if (DB::on) {
-        t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_4^1 = w_R^(R/4)
+        t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_4^1 = w_R^(R/4), wave-uniform: SGPRs
       } else {
         const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
         t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
@@ -291,13 +293,25 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         fe_bfly_lazy(x2, x3, x3);
         fe t3;
         if (DB::on) {
-          t3 = fe_mul_db(x3, dbt(sdb, (1u << (LOG_R - 2)) / DB::stride));  // w_{4m}^m = w_4^1
+          t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_{4m}^m = w_4^1
         } else {
           const uint32_t ic = 2 * (1u << (LOG_R - 2));
           t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
         }
         fe_csub2p(x2);
         fe_bfly_lazy(x0, x2, x2);
+        fe_bfly_lazy(x1, x3, t3);
+      } else if (DB::on && DB::s_end > kS0 && lq >= 6) {
+        // every wave has one jj: the constants come from the global table into SGPRs (no LDS reads)
+        const uint32_t ju = __builtin_amdgcn_readfirstlane(jj);
+        const uint32_t* wa = db + 72u * (ju << (LOG_R - 1 - kS0));  // w_{2m}^jj
+        const fe t1 = fe_mul_db(x1, wa);
+        fe t3 = fe_mul_db(x3, wa);
+        fe_bfly_lazy(x0, x1, t1);
+        fe_bfly_lazy(x2, x3, t3);
+        const fe t2 = fe_mul_db(x2, db + 72u * (ju << (LOG_R - 2 - kS0)));                // w_{4m}^jj
+        t3 = fe_mul_db(x3, db + 72u * ((ju + (1u << kS0)) << (LOG_R - 2 - kS0)));  // w_{4m}^(jj+m)
+        fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
       } else if (DB::on && DB::s_end > kS0) {
         constexpr uint32_t S = DB::stride;
