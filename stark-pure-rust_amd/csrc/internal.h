@@ -59,6 +59,7 @@ struct DevBuf {
 //   lo[i] = w^i                   i < 2^kb
 //   hi[i] = w^(i * 2^kb)          i < 2^(log_n - kb)
 //   small_off[l] = offset (in fe) into `small` of the Shoup pairs of w_R^k = w^(k * n / R), k < R/2, R = 2^l
+//     (k < R for R = 2^8)
 struct Twiddles {
   uint32_t log_n = 0, kb = 0;
   fe* d_lo = nullptr;

@@ -73,18 +73,25 @@ constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
 //     (36 KB) that measured slower, so its last step multiplies by Shoup pairs staged in LDS (8 KB).
 // (Measured and dropped, DESIGN.md section 5: no digit basis, the R/2-constant table resident (2
 // workgroups per CU), the m <= 4 steps only with global Shoup pairs, the tables read through L1.)
+// Radix 2^8 runs as 16 x 16 inside the tile (`four`): after the first two radix-4 steps (a 16-point
+// DFT over each group of 16 image rows) every element is multiplied by its twiddle w_R^(r1 k1), and the
+// last two steps are a 16-point DFT across the groups, whose constants (w_4, and w_16^a for the wave's
+// a) are wave-uniform.  Every digit-basis constant of the pass then comes from SGPRs; the only
+// per-lane constants are the twiddles, Shoup pairs of w_R^e, e < R, staged in LDS (16 KB).
 template <int LOG_R, int COL>
 struct DbPlan {
   static constexpr bool on = LOG_R >= 4 && LOG_R <= 8;
+  static constexpr bool four = LOG_R == 8;
   static constexpr int s_end = on ? LOG_R - 2 : 0;  // DB for steps s < s_end
   static constexpr uint32_t stride = 4;             // the table holds w_R^(4 k), k < R / 8
-  static constexpr uint32_t entries = on ? (1u << LOG_R) / (2 * stride) : 0;
+  static constexpr uint32_t entries = (on && !four) ? (1u << LOG_R) / (2 * stride) : 0;
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
-  static constexpr uint32_t lds_fe = !on ? 0 : entries * 9 + entries / 16;
+  static constexpr uint32_t lds_fe = entries * 9 + entries / 16;
   static constexpr bool last = on && LOG_R <= 7;
   static constexpr uint32_t full_entries = last ? (1u << LOG_R) / 2 : 0;
   static constexpr uint32_t full_fe = full_entries * 9 + full_entries / 16;
-  static constexpr uint32_t shoup_fe = last ? 0 : (1u << LOG_R);  // staged Shoup pairs of the last step
+  // staged Shoup pairs: the last step's w_R^k, k < R/2, or the twiddles' w_R^e, e < R (four)
+  static constexpr uint32_t shoup_fe = last ? 0 : four ? 2 * (1u << LOG_R) : (1u << LOG_R);
   static constexpr int occupancy = on ? 3 : 4;                     // workgroups per CU the LDS allows
 };
 
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   if (tile >= total_tiles) return;  // (uniform per workgroup)
 
   if (DB::shoup_fe)
-    for (uint32_t k = tid; k < R; k += blockDim.x) sm[k] = small[k];
+    for (uint32_t k = tid; k < DB::shoup_fe; k += blockDim.x) sm[k] = small[k];
   // The global table holds every w_R^k, k < R/2; the LDS copy every stride-th one.
   if (DB::on)
     for (uint32_t k = tid; k < DB::entries * 18; k += blockDim.x) {
@@ -315,13 +322,15 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         fe_bfly_lazy(x1, x3, t3);
       } else if (DB::on && DB::s_end > kS0) {
         constexpr uint32_t S = DB::stride;
-        const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - kS0)) / S);  // w_{2m}^jj
+        // (four: no LDS table; small tiles read the global one per lane)
+        auto tab = [&](uint32_t e) { return DB::four ? db + 72u * e : dbt(sdb, e / S); };
+        const uint32_t* wa = tab(jj << (LOG_R - 1 - kS0));  // w_{2m}^jj
         const fe t1 = fe_mul_db(x1, wa);
         fe t3 = fe_mul_db(x3, wa);
         fe_bfly_lazy(x0, x1, t1);
         fe_bfly_lazy(x2, x3, t3);
-        const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - kS0)) / S));                // w_{4m}^jj
-        t3 = fe_mul_db(x3, dbt(sdb, ((jj + (1u << kS0)) << (LOG_R - 2 - kS0)) / S));  // w_{4m}^(jj+m)
+        const fe t2 = fe_mul_db(x2, tab(jj << (LOG_R - 2 - kS0)));                // w_{4m}^jj
+        t3 = fe_mul_db(x3, tab((jj + (1u << kS0)) << (LOG_R - 2 - kS0)));  // w_{4m}^(jj+m)
         fe_bfly_lazy(x0, x2, t2);
         fe_bfly_lazy(x1, x3, t3);
       } else {
@@ -347,7 +356,77 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     __syncthreads();
     s = kS0 + 2;
   }
-  if (DB::on) {
+  // ---- radix 2^8 as 16 x 16 (DbPlan::four): twiddles, then a 16-point DFT across the groups ----
+  // Image row 16 g + t now holds Z[r1][k1 = t], the 16-point DFT of the natural inputs r1 + 16 r2
+  // with r1 = rev4(g); Y[k1 + 16 k2] = sum_r1 w_16^(r1 k2) (w_R^(r1 k1) Z[r1][k1]).  Both steps below
+  // keep the generic steps' thread mapping (s = 4: rows 64 a + t + 16 k; s = 6: rows q + 64 k), so the
+  // last one still ends in the store's registers.  (A sparse pass that skips more than the first 4
+  // stages arrives here with s > 4 and runs the generic last step: its copies span the twiddles.)
+  bool kept = false;  // the pass's last step left its outputs in yl (the store's mapping)
+  fe yl[4];
+  if (DB::four && s == 4) {
+    if (active) {
+      const uint32_t t = q & 15, a = q >> 4;
+      const uint32_t i0 = (((a << 6) + t) << log_b) + b, st = 16u << log_b;
+      fe x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const fe v = XI.ld(i0 + k * st);
+        const uint32_t e = (__builtin_bitreverse32((a << 2) + k) >> 28) * t;  // rev4(g) k1, < 256
+        x[k] = fe_mul_shoup(v, sm[2 * e], sm[2 * e + 1]);                      // [0, 2p)
+      }
+      // 16-point DFT across the groups, first radix-4 step (stride 16 rows): only w_4 (SGPRs)
+      fe_bfly_lazy(x[0], x[1], x[1]);
+      fe_bfly_lazy(x[2], x[3], x[3]);
+      const fe t3 = fe_mul_db(x[3], db + 72u * (1u << (LOG_R - 2)));
+      fe_csub2p(x[2]);
+      fe_bfly_lazy(x[0], x[2], x[2]);
+      fe_bfly_lazy(x[1], x[3], t3);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) XI.st(i0 + k * st, x[k]);
+    }
+    __syncthreads();
+    if (active) {
+      // second radix-4 step (stride 64 rows, jj = a = q >> 4): w_8^a, w_16^a, w_16^(a + 4)
+      const uint32_t i0 = (q << log_b) + b, st = 64u << log_b;
+      fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
+      auto step = [&](const uint32_t a) {
+        if (a == 0) {
+          fe_csub2p(x1);
+          fe_csub2p(x3);
+          fe_bfly_lazy(x0, x1, x1);
+          fe_bfly_lazy(x2, x3, x3);
+          const fe t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_4
+          fe_csub2p(x2);
+          fe_bfly_lazy(x0, x2, x2);
+          fe_bfly_lazy(x1, x3, t3);
+        } else {
+          const uint32_t* wa = db + 72u * (a << 5);  // w_8^a = w_R^(32 a)
+          const fe t1 = fe_mul_db(x1, wa);
+          fe t3 = fe_mul_db(x3, wa);
+          fe_bfly_lazy(x0, x1, t1);
+          fe_bfly_lazy(x2, x3, t3);
+          const fe t2 = fe_mul_db(x2, db + 72u * (a << 4));  // w_16^a
+          t3 = fe_mul_db(x3, db + 72u * ((a + 4) << 4));     // w_16^(a + 4)
+          fe_bfly_lazy(x0, x2, t2);
+          fe_bfly_lazy(x1, x3, t3);
+        }
+      };
+      // a wave holds 16 consecutive q when B = 4 (the 1024-element tile): a is uniform, its constants
+      // come from SGPRs; smaller tiles read them per lane
+      if (log_b == 2)
+        step(__builtin_amdgcn_readfirstlane(q >> 4));
+      else
+        step(q >> 4);
+      yl[0] = x0;
+      yl[1] = x1;
+      yl[2] = x2;
+      yl[3] = x3;
+    }
+    kept = true;
+    s = LOG_R;
+  }
+  if (DB::on && !DB::four) {
 #pragma unroll 1
     for (; s < DB::s_end; s += 2) {
       if (active) {
@@ -381,8 +460,6 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   // elements (er[k], eb[k]) it stores, so it keeps them in registers (no LDS round trip and one
   // barrier less per tile; radix 2^9 spills at its 128-register budget).
   constexpr bool fuse = LOG_R <= 8;
-  bool kept = false;
-  fe yl[4];
 #pragma unroll 1
   for (; s < (DB::last ? LOG_R - 2 : LOG_R); s += 2) {
     const bool keep = fuse && s == LOG_R - 2;  // uniform
@@ -671,13 +748,14 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     h_hi[i] = to_dev(acc);
     acc = F.mul(acc, step);
   }
-  // Small-root tables for every radix 2^l (l <= min(log_n, 8)): w^(k n / R), k < R/2.
+  // Small-root tables for every radix 2^l (l <= min(log_n, 9)): w^(k n / R), k < R/2 (k < R for
+  // R = 2^8: the 16 x 16 passes' twiddles, DbPlan::four).
   std::vector<fe> h_small;
   for (uint32_t l = 1; l <= kMaxLogR && l <= log_n; ++l) {
     tw->small_off[l] = (uint32_t)h_small.size();
     const HostFp wr = F.pow_u64(w, (uint64_t)1 << (log_n - l));
     HostFp a = F.one();
-    for (uint32_t k = 0; k < (1u << (l - 1)); ++k) {
+    for (uint32_t k = 0; k < (l == 8 ? 256u : (1u << (l - 1))); ++k) {
       fe pr[2];
       shoup_pair(a, pr);
       h_small.push_back(pr[0]);
