@@ -405,21 +405,25 @@ def ntt_products(log_n: int, plan: list) -> tuple:
     before the last one of every pass use the digit-basis product (ntt.hip DbPlan,
     radices 2^4..2^8).  Radices >= 2^5 run their first step with twiddles (s = 2 even, s = 1 odd)
     jj-major, and its jj = 0 butterflies (n/16 even, n/8 odd) skip the products by w^0 = 1 (three of
-    their four; ntt.hip STARK_NTT_JJ_MAJOR)."""
+    their four).  Radix 2^8 runs 16 x 16 (ntt.hip DbPlan::four): w_4 (n/4), the jj-major step (13n/16),
+    one Shoup twiddle per element (n), w_4 (n/4), the last step (13n/16: its a = 0 waves multiply by w_4
+    only); every product but the twiddles by the digit basis."""
     n = 1 << log_n
     l16 = 18 if log_n >= 25 else min(log_n, 16)
     total, db, ns = 0, 0, 0
     for i, r in enumerate(plan):
-        if r % 2:
+        if r == 8:
+            total += 50 * n // 16
+            db += 34 * n // 16
+        elif r % 2:
             steps = n * ((r - 1) // 2)
         else:
             steps = n * (r // 2 - 1) + n // 4
-        skip = 0 if r < 5 else 3 * n // 8 if r % 2 else 3 * n // 16
-        total += steps - skip
-        if 4 <= r <= 8:
-            db += steps - n - skip  # all but the last radix-4 step (every pass: ntt.hip STARK_NTT_DB_FIRST)
-            if r <= 7:
-                db += n  # the last step too, from the table staged per tile (ntt.hip STARK_NTT_DB_LAST[_FIRST])
+        if r != 8:
+            skip = 0 if r < 5 else 3 * n // 8 if r % 2 else 3 * n // 16
+            total += steps - skip
+            if 4 <= r <= 7:
+                db += steps - skip  # every radix-4 step, the last from the table staged per tile
         if ns:
             last = i == len(plan) - 1
             table = ns + r <= l16 or (last and log_n > l16 and 17 <= log_n <= 26)
