@@ -65,7 +65,7 @@ constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
 
 // Which radix-4 steps multiply by the digit-basis product (fe_db.h), radices 2^4..2^8:
 //   * every step before the pass's last one: constants w_R^(4k), k < R/8 (32 for R = 256, 9 KB of
-//     LDS, staged once per workgroup).  Where a wave's constant is uniform (the peeled step's w_4 and
+//     LDS, staged once per workgroup).  Where a wave's constant is uniform (the first step's w_4 and
 //     the jj-major first twiddled step) its table is read from the global one into SGPRs instead
 //     (scalar loads; the column sums take it as the SGPR operand of v_mad_u64_u32): no LDS reads;
 //   * the last step too for radices <= 2^7: once the step has read its inputs, all R/2 constants
@@ -208,6 +208,30 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       }
     }
     if (sp.skip == 0) {
+      // The first stage in registers: the thread holds rows r0 + t R/4 of column eb, whose image rows
+      // are 4 rev(r0) + {0, 2, 1, 3}[t], i.e. exactly one group of the first radix-4 step (w_4 only)
+      // or two pairs of the odd radices' radix-2 stage 0.  No LDS round trip, one barrier less.
+      if ((LOG_R & 1) == 0) {  // x0..x3 = v[0], v[2], v[1], v[3]
+        fe_csub2p(v[2]);
+        fe_csub2p(v[3]);
+        fe_bfly_lazy(v[0], v[2], v[2]);
+        fe_bfly_lazy(v[1], v[3], v[3]);
+        fe t3;
+        if (DB::on) {
+          t3 = fe_mul_db(v[3], db + 72u * (1u << (LOG_R - 2)));  // w_4^1 = w_R^(R/4), wave-uniform: SGPRs
+        } else {
+          const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1 (sm is not staged yet: the global table)
+          t3 = fe_mul_shoup(v[3], small[ic], small[ic + 1]);
+        }
+        fe_csub2p(v[1]);
+        fe_bfly_lazy(v[0], v[1], v[1]);
+        fe_bfly_lazy(v[2], v[3], t3);
+      } else {
+        fe_csub2p(v[2]);
+        fe_bfly_lazy(v[0], v[2], v[2]);
+        fe_csub2p(v[3]);
+        fe_bfly_lazy(v[1], v[3], v[3]);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
@@ -231,54 +255,9 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   // left in [0, 2p) and each radix-2 butterfly reduces only its X input
   // (fe_bfly_lazy).  The pass's last store reduces to canonical only when
   // it is the transform's last pass.
-  int s = (int)sp.skip;
-  if ((LOG_R & 1) && sp.skip == 0) {
-    if (active) {  // radix-2 stage 0: twiddles are all 1
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t g = q * 2 + h;
-        const uint32_t ia = ((2 * g) << log_b) + b, ib = ((2 * g + 1) << log_b) + b;
-        fe a = XI.ld(ia), c = XI.ld(ib);
-        fe_csub2p(c);
-        fe_bfly_lazy(a, c, c);
-        XI.st(ia, a);
-        XI.st(ib, c);
-      }
-    }
-    __syncthreads();
-    s = 1;
-  }
-  if (s == 0) {
-    // Radix-4 step s = 0 (peeled: its twiddles are 1 except w_4^1, and the loop below stays
-    // branch-free, so no register shuffles at merge points).
-    if (active) {
-      const uint32_t base = q << 2;
-      fe x0 = XI.ld((base << log_b) + b);
-      fe x1 = XI.ld(((base + 1) << log_b) + b);
-      fe x2 = XI.ld(((base + 2) << log_b) + b);
-      fe x3 = XI.ld(((base + 3) << log_b) + b);
-      fe_csub2p(x1);
-      fe_csub2p(x3);
-      fe_bfly_lazy(x0, x1, x1);  // (y0, y1)
-      fe_bfly_lazy(x2, x3, x3);  // (y2, y3)
-      fe t3;
-      if (DB::on) {
-        t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_4^1 = w_R^(R/4), wave-uniform: SGPRs
-      } else {
-        const uint32_t ic = 2 * (1u << (LOG_R - 2));  // w_4^1
-        t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
-      }
-      fe_csub2p(x2);
-      fe_bfly_lazy(x0, x2, x2);
-      fe_bfly_lazy(x1, x3, t3);
-      XI.st((base << log_b) + b, x0);
-      XI.st(((base + 2) << log_b) + b, x2);
-      XI.st(((base + 1) << log_b) + b, x1);
-      XI.st(((base + 3) << log_b) + b, x3);
-    }
-    __syncthreads();
-    s = 2;
-  }
+  // A dense pass did its first stage in registers before the scatter (radix-4 step s = 0 for an
+  // even radix, the radix-2 stage 0 for an odd one); a sparse pass starts after its copy stages.
+  int s = sp.skip ? (int)sp.skip : (LOG_R & 1) ? 1 : 2;
   // The first radix-4 step with twiddles (s0 = 2, m = 4 for an even radix; s0 = 1, m = 2 after the
   // radix-2 stage of an odd one) with a jj-major thread mapping: each 1/m of the threads takes one
   // jj, so with B R >= 1024 every wave has a single jj and the jj = 0 waves skip the products by
