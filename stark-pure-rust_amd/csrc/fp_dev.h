@@ -220,8 +220,13 @@ __device__ __forceinline__ void fe_csub2p(fe& t) {
 // Radix-2 butterfly in the lazy representation (Harvey):
 //   X in [0, 4p), T in [0, 2p)  ->  X' = X mod 2p in [0, 2p),
 //   x <- X' + T in [0, 4p),  y <- X' - T + 2p in (0, 4p).
+__device__ __forceinline__ void fe_bfly_lazy_reduced(fe& x, fe& y, const fe& t);
 __device__ __forceinline__ void fe_bfly_lazy(fe& x, fe& y, const fe& t) {
   fe_csub2p(x);
+  fe_bfly_lazy_reduced(x, y, t);
+}
+// The same for X already in [0, 2p).
+__device__ __forceinline__ void fe_bfly_lazy_reduced(fe& x, fe& y, const fe& t) {
   const P2Limbs q = p2_vgprs();
   // s = X' + T and d = (X' + 2p) - T written to fresh registers (an in-place form would copy X'
   // into both first: 16 v_mov_b32 per butterfly).  X' + 2p < 4p < 2^256 and >= T, so neither

@@ -46,6 +46,11 @@ __device__ __forceinline__ void mul2(fe& r, fe& s, const fe& a, const fe& b, con
   fe_mul_lazy2(r, s, a, b, c, d);
 }
 
+// fe_bfly_lazy for an X input already below 2p (a product or a canonical load): no reduction of X.
+__device__ __forceinline__ void bfly_lt2p(fe& x, fe& y, const fe& t) {
+  fe_bfly_lazy_reduced(x, y, t);
+}
+
 // The digit-basis table of constant k in LDS: 72 u32 per constant, 16-B aligned.  Constants 8 apart
 // would share banks (72 * 8 = 0 mod 64 banks) and a radix-4 step reads k, k + 8, k + 16, k + 24 in
 // one ds_read_b128 lane group, so each group of 8 constants starts 4 banks after the previous one.
@@ -211,11 +216,11 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       // The first stage in registers: the thread holds rows r0 + t R/4 of column eb, whose image rows
       // are 4 rev(r0) + {0, 2, 1, 3}[t], i.e. exactly one group of the first radix-4 step (w_4 only)
       // or two pairs of the odd radices' radix-2 stage 0.  No LDS round trip, one barrier less.
+      // Its inputs are below 2p (canonical loads, or column-twiddle products in [0, 2p)), so the first
+      // butterflies need no reductions.
       if ((LOG_R & 1) == 0) {  // x0..x3 = v[0], v[2], v[1], v[3]
-        fe_csub2p(v[2]);
-        fe_csub2p(v[3]);
-        fe_bfly_lazy(v[0], v[2], v[2]);
-        fe_bfly_lazy(v[1], v[3], v[3]);
+        bfly_lt2p(v[0], v[2], v[2]);
+        bfly_lt2p(v[1], v[3], v[3]);
         fe t3;
         if (DB::on) {
           t3 = fe_mul_db(v[3], db + 72u * (1u << (LOG_R - 2)));  // w_4^1 = w_R^(R/4), wave-uniform: SGPRs
@@ -227,10 +232,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         fe_bfly_lazy(v[0], v[1], v[1]);
         fe_bfly_lazy(v[2], v[3], t3);
       } else {
-        fe_csub2p(v[2]);
-        fe_bfly_lazy(v[0], v[2], v[2]);
-        fe_csub2p(v[3]);
-        fe_bfly_lazy(v[1], v[3], v[3]);
+        bfly_lt2p(v[0], v[2], v[2]);
+        bfly_lt2p(v[1], v[3], v[3]);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -354,9 +357,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         const uint32_t e = (__builtin_bitreverse32((a << 2) + k) >> 28) * t;  // rev4(g) k1, < 256
         x[k] = fe_mul_shoup(v, sm[2 * e], sm[2 * e + 1]);                      // [0, 2p)
       }
-      // 16-point DFT across the groups, first radix-4 step (stride 16 rows): only w_4 (SGPRs)
-      fe_bfly_lazy(x[0], x[1], x[1]);
-      fe_bfly_lazy(x[2], x[3], x[3]);
+      // 16-point DFT across the groups, first radix-4 step (stride 16 rows): only w_4 (SGPRs); the
+      // twiddled inputs are below 2p
+      bfly_lt2p(x[0], x[1], x[1]);
+      bfly_lt2p(x[2], x[3], x[3]);
       const fe t3 = fe_mul_db(x[3], db + 72u * (1u << (LOG_R - 2)));
       fe_csub2p(x[2]);
       fe_bfly_lazy(x[0], x[2], x[2]);
