@@ -143,16 +143,6 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
   const uint32_t tile = blockIdx.x;
   if (tile >= total_tiles) return;  // (uniform per workgroup)
 
-  if (DB::shoup_fe)
-    for (uint32_t k = tid; k < DB::shoup_fe; k += blockDim.x) sm[k] = small[k];
-  // The global table holds every w_R^k, k < R/2; the LDS copy every stride-th one.
-  if (DB::on)
-    for (uint32_t k = tid; k < DB::entries * 18; k += blockDim.x) {
-      const uint32_t e = k / 18;
-      reinterpret_cast<uint4*>(sdb)[k + (e >> 3)] =
-          reinterpret_cast<const uint4*>(db)[(e * DB::stride) * 18 + (k - e * 18)];
-    }
-
   // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row) as stored and loaded.
   uint32_t eb[4], er[4];
 #pragma unroll
@@ -175,6 +165,41 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
+  }
+
+  // Stage the pass's LDS tables once the tile's loads are in flight, every staging load before any
+  // store, so a wave waits for one memory latency instead of one per staging round.  (The global
+  // digit-basis table holds every w_R^k, k < R/2; the LDS copy every stride-th one.)
+  {
+    constexpr uint32_t kSm = 2 * DB::shoup_fe, kDb = DB::on ? DB::entries * 18 : 0;  // 16-B units
+    const uint4* db4 = reinterpret_cast<const uint4*>(db);
+    const uint4* small4 = reinterpret_cast<const uint4*>(small);
+    uint4* sm4 = reinterpret_cast<uint4*>(sm);
+    uint4* sdb4 = reinterpret_cast<uint4*>(sdb);
+    auto db_src = [&](uint32_t k) { const uint32_t e = k / 18; return (e * DB::stride) * 18 + (k - e * 18); };
+    auto db_dst = [&](uint32_t k) { return k + ((k / 18) >> 3); };
+    if (blockDim.x == kPassThreads) {
+      constexpr uint32_t nSm = (kSm + kPassThreads - 1) / kPassThreads, nDb = (kDb + kPassThreads - 1) / kPassThreads;
+      // (full rounds need no bounds test: tid < kPassThreads here)
+      auto in_sm = [&](uint32_t i) { return (i + 1) * kPassThreads <= kSm || tid + i * kPassThreads < kSm; };
+      auto in_db = [&](uint32_t i) { return (i + 1) * kPassThreads <= kDb || tid + i * kPassThreads < kDb; };
+      uint4 ts[nSm ? nSm : 1], td[nDb ? nDb : 1];
+#pragma unroll
+      for (uint32_t i = 0; i < nSm; ++i)
+        if (in_sm(i)) ts[i] = small4[tid + i * kPassThreads];
+#pragma unroll
+      for (uint32_t i = 0; i < nDb; ++i)
+        if (in_db(i)) td[i] = db4[db_src(tid + i * kPassThreads)];
+#pragma unroll
+      for (uint32_t i = 0; i < nSm; ++i)
+        if (in_sm(i)) sm4[tid + i * kPassThreads] = ts[i];
+#pragma unroll
+      for (uint32_t i = 0; i < nDb; ++i)
+        if (in_db(i)) sdb4[db_dst(tid + i * kPassThreads)] = td[i];
+    } else {
+      for (uint32_t k = tid; k < kSm; k += blockDim.x) sm4[k] = small4[k];
+      for (uint32_t k = tid; k < kDb; k += blockDim.x) sdb4[db_dst(k)] = db4[db_src(k)];
+    }
   }
   const size_t boff = (size_t)(tile >> log_tiles) << log_n;
   const size_t j0 = (size_t)(tile & tile_mask) << log_b;
