@@ -61,7 +61,8 @@ __device__ __forceinline__ const uint32_t* dbt(const uint32_t* sdb, uint32_t k) 
 // COL: the pass's column-twiddle source, fixed per launch so each instance carries one product
 // form (kColNone: first pass; kColFull: last-pass full table, Montgomery; kColT16: Shoup pairs;
 // kColTwoLevel: lo * hi, Montgomery).
-enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3 };
+enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3, kColSparse = 4 };
+// (kColSparse: a first pass over a zero-padded input (Sparse::skip > 0); no column twiddle either.)
 
 // Elements per workgroup tile: 2^10 (B = 1024 / R columns, 256 threads).  4096- and 2048-element
 // tiles measured slower (one or two workgroups per CU leave the barriers uncovered).
@@ -73,26 +74,26 @@ constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
 //     LDS, staged once per workgroup).  Where a wave's constant is uniform (the first step's w_4 and
 //     the jj-major first twiddled step) its table is read from the global one into SGPRs instead
 //     (scalar loads; the column sums take it as the SGPR operand of v_mad_u64_u32): no LDS reads;
-//   * the last step too for radices <= 2^7: once the step has read its inputs, all R/2 constants
-//     (L2-resident, <= 18 KB) are staged over the data image (two more barriers per tile).  For R = 2^8
-//     (36 KB) that measured slower, so its last step multiplies by Shoup pairs staged in LDS (8 KB).
+//   * the last step too for radices 2^4..2^7 (2^7 outside sparse passes): once the step has read its inputs, all R/2 constants
+//     (L2-resident, <= 18 KB) are staged over the data image (two more barriers per tile).
 // (Measured and dropped, DESIGN.md section 5: no digit basis, the R/2-constant table resident (2
 // workgroups per CU), the m <= 4 steps only with global Shoup pairs, the tables read through L1.)
-// Radix 2^8 runs as 16 x 16 inside the tile (`four`): after the first two radix-4 steps (a 16-point
-// DFT over each group of 16 image rows) every element is multiplied by its twiddle w_R^(r1 k1), and the
-// last two steps are a 16-point DFT across the groups, whose constants (w_4, and w_16^a for the wave's
-// a) are wave-uniform.  Every digit-basis constant of the pass then comes from SGPRs; the only
-// per-lane constants are the twiddles, Shoup pairs of w_R^e, e < R, staged in LDS (16 KB).
+// Radix 2^8, and radix 2^7 in a sparse first pass, run as T x 16 inside the tile (`four`, T = R/16): after the first stages (a
+// T-point DFT over each group of T image rows) every element is multiplied by its twiddle w_R^(r1 k1),
+// and the last two radix-4 steps are a 16-point DFT across the groups, whose constants (w_4, and
+// w_16^a for the wave's a) are wave-uniform.  Every digit-basis constant of the pass then comes from
+// SGPRs; the only per-lane constants are the twiddles, Shoup pairs of w_R^e, e < R, staged in LDS
+// (16 / 8 KB).  The LDE's sparse first pass (radix 2^7, three copy stages) enters at the twiddles.
 template <int LOG_R, int COL>
 struct DbPlan {
   static constexpr bool on = LOG_R >= 4 && LOG_R <= 8;
-  static constexpr bool four = LOG_R == 8;
+  static constexpr bool four = LOG_R == 8 || (LOG_R == 7 && COL == kColSparse);
   static constexpr int s_end = on ? LOG_R - 2 : 0;  // DB for steps s < s_end
   static constexpr uint32_t stride = 4;             // the table holds w_R^(4 k), k < R / 8
   static constexpr uint32_t entries = (on && !four) ? (1u << LOG_R) / (2 * stride) : 0;
   // 72 u32 per constant, plus 4 u32 of bank rotation per 8 constants (dbt)
   static constexpr uint32_t lds_fe = entries * 9 + entries / 16;
-  static constexpr bool last = on && LOG_R <= 7;
+  static constexpr bool last = on && !four && LOG_R <= 7;
   static constexpr uint32_t full_entries = last ? (1u << LOG_R) / 2 : 0;
   static constexpr uint32_t full_fe = full_entries * 9 + full_entries / 16;
   // staged Shoup pairs: the last step's w_R^k, k < R/2, or the twiddles' w_R^e, e < R (four)
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
 
   // ---- column twiddle, scatter into the bit-reversed LDS image ----
   if (active) {
-    if (COL != kColNone) {
+    if (COL != kColNone && COL != kColSparse) {
       const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
       fe tw[4];
       if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
@@ -363,23 +364,24 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     __syncthreads();
     s = kS0 + 2;
   }
-  // ---- radix 2^8 as 16 x 16 (DbPlan::four): twiddles, then a 16-point DFT across the groups ----
-  // Image row 16 g + t now holds Z[r1][k1 = t], the 16-point DFT of the natural inputs r1 + 16 r2
-  // with r1 = rev4(g); Y[k1 + 16 k2] = sum_r1 w_16^(r1 k2) (w_R^(r1 k1) Z[r1][k1]).  Both steps below
-  // keep the generic steps' thread mapping (s = 4: rows 64 a + t + 16 k; s = 6: rows q + 64 k), so the
-  // last one still ends in the store's registers.  (A sparse pass that skips more than the first 4
-  // stages arrives here with s > 4 and runs the generic last step: its copies span the twiddles.)
+  // ---- radix 2^8 / 2^7 as T x 16 (DbPlan::four): twiddles, then a 16-point DFT across the groups ----
+  // Image row T g + t now holds Z[r1][k1 = t], the T-point DFT of the natural inputs r1 + 16 r2
+  // with r1 = rev4(g); Y[k1 + T k2] = sum_r1 w_16^(r1 k2) (w_R^(r1 k1) Z[r1][k1]).  Both steps below
+  // keep the generic steps' thread mapping (s = LT: rows 4 T a + t + T k; then rows q + (R/4) k), so
+  // the last one still ends in the store's registers.  (A sparse pass that skips more than the first
+  // LT stages arrives here with s > LT and runs the generic last steps: its copies span the twiddles.)
   bool kept = false;  // the pass's last step left its outputs in yl (the store's mapping)
   fe yl[4];
-  if (DB::four && s == 4) {
+  constexpr uint32_t LT = LOG_R >= 4 ? LOG_R - 4 : 0;  // log2 of T = R / 16, the rows of a group
+  if (DB::four && s == (int)LT) {
     if (active) {
-      const uint32_t t = q & 15, a = q >> 4;
-      const uint32_t i0 = (((a << 6) + t) << log_b) + b, st = 16u << log_b;
+      const uint32_t t = q & ((1u << LT) - 1), a = q >> LT;
+      const uint32_t i0 = (((a << (LT + 2)) + t) << log_b) + b, st = (1u << LT) << log_b;
       fe x[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const fe v = XI.ld(i0 + k * st);
-        const uint32_t e = (__builtin_bitreverse32((a << 2) + k) >> 28) * t;  // rev4(g) k1, < 256
+        const uint32_t e = (__builtin_bitreverse32((a << 2) + k) >> 28) * t;  // rev4(g) k1, < R
         x[k] = fe_mul_shoup(v, sm[2 * e], sm[2 * e + 1]);                      // [0, 2p)
       }
       // 16-point DFT across the groups, first radix-4 step (stride 16 rows): only w_4 (SGPRs); the
@@ -395,8 +397,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     }
     __syncthreads();
     if (active) {
-      // second radix-4 step (stride 64 rows, jj = a = q >> 4): w_8^a, w_16^a, w_16^(a + 4)
-      const uint32_t i0 = (q << log_b) + b, st = 64u << log_b;
+      // second radix-4 step (stride R/4 rows, jj = a = q >> LT): w_8^a, w_16^a, w_16^(a + 4)
+      const uint32_t i0 = (q << log_b) + b, st = (R / 4) << log_b;
       fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
       auto step = [&](const uint32_t a) {
         if (a == 0) {
@@ -409,23 +411,23 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           fe_bfly_lazy(x0, x2, x2);
           fe_bfly_lazy(x1, x3, t3);
         } else {
-          const uint32_t* wa = db + 72u * (a << 5);  // w_8^a = w_R^(32 a)
+          const uint32_t* wa = db + 72u * (a << (LOG_R - 3));  // w_8^a = w_R^(a R/8)
           const fe t1 = fe_mul_db(x1, wa);
           fe t3 = fe_mul_db(x3, wa);
           fe_bfly_lazy(x0, x1, t1);
           fe_bfly_lazy(x2, x3, t3);
-          const fe t2 = fe_mul_db(x2, db + 72u * (a << 4));  // w_16^a
-          t3 = fe_mul_db(x3, db + 72u * ((a + 4) << 4));     // w_16^(a + 4)
+          const fe t2 = fe_mul_db(x2, db + 72u * (a << LT));  // w_16^a = w_R^(a R/16)
+          t3 = fe_mul_db(x3, db + 72u * ((a + 4) << LT));     // w_16^(a + 4)
           fe_bfly_lazy(x0, x2, t2);
           fe_bfly_lazy(x1, x3, t3);
         }
       };
-      // a wave holds 16 consecutive q when B = 4 (the 1024-element tile): a is uniform, its constants
-      // come from SGPRs; smaller tiles read them per lane
-      if (log_b == 2)
-        step(__builtin_amdgcn_readfirstlane(q >> 4));
+      // a wave holds 64 / B consecutive q, all with one a when 64 / B <= T (the 1024-element tile): a is
+      // uniform, its constants come from SGPRs; smaller tiles read them per lane
+      if ((64u >> log_b) <= (1u << LT))
+        step(__builtin_amdgcn_readfirstlane(q >> LT));
       else
-        step(q >> 4);
+        step(q >> LT);
       yl[0] = x0;
       yl[1] = x1;
       yl[2] = x2;
@@ -665,6 +667,7 @@ size_t db_full_fe_c(uint32_t log_r) {
 size_t db_full_fe(uint32_t log_r, int col) {
   switch (col) {
     case kColNone: return db_full_fe_c<kColNone>(log_r);
+    case kColSparse: return db_full_fe_c<kColSparse>(log_r);
     case kColFull: return db_full_fe_c<kColFull>(log_r);
     case kColT16: return db_full_fe_c<kColT16>(log_r);
     default: return db_full_fe_c<kColTwoLevel>(log_r);
@@ -687,6 +690,7 @@ size_t db_lds_fe_c(uint32_t log_r) {
 size_t db_lds_fe(uint32_t log_r, int col) {
   switch (col) {
     case kColNone: return db_lds_fe_c<kColNone>(log_r);
+    case kColSparse: return db_lds_fe_c<kColSparse>(log_r);
     case kColFull: return db_lds_fe_c<kColFull>(log_r);
     case kColT16: return db_lds_fe_c<kColT16>(log_r);
     default: return db_lds_fe_c<kColTwoLevel>(log_r);
@@ -697,6 +701,7 @@ template <int LOG_R>
 pass_fn pass_kernel_r(int col) {
   switch (col) {
     case kColNone: return ntt_pass_kernel<LOG_R, kColNone>;
+    case kColSparse: return ntt_pass_kernel<LOG_R, kColSparse>;
     case kColFull: return ntt_pass_kernel<LOG_R, kColFull>;
     case kColT16: return ntt_pass_kernel<LOG_R, kColT16>;
     default: return ntt_pass_kernel<LOG_R, kColTwoLevel>;
@@ -763,7 +768,7 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
     tw->small_off[l] = (uint32_t)h_small.size();
     const HostFp wr = F.pow_u64(w, (uint64_t)1 << (log_n - l));
     HostFp a = F.one();
-    for (uint32_t k = 0; k < (l == 8 ? 256u : (1u << (l - 1))); ++k) {
+    for (uint32_t k = 0; k < ((l == 7 || l == 8) ? (1u << l) : (1u << (l - 1))); ++k) {
       fe pr[2];
       shoup_pair(a, pr);
       h_small.push_back(pr[0]);
@@ -955,7 +960,8 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
       if (st != STARK_OK) return st;
     }
     ColTw ct{fold ? tw.d_t16_s : tw.d_t16, tw.d_lo, fold ? tw.d_hi_s : tw.d_hi, full, tw.l16, tw.kb};
-    const int col = log_ns == 0 ? kColNone : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
+    const int col = log_ns == 0 ? (sp.skip ? kColSparse : kColNone)
+                    : full ? kColFull : log_ns + lr <= tw.l16 ? kColT16 : kColTwoLevel;
     // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
     const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
     const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
