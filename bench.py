@@ -159,6 +159,37 @@ def steady_ms(fn, stream, target_ms=60.0):
     return timed_events(fn, stream, max(5, int(target_ms / one)))
 
 
+def median_ms(fn, stream, reps=25, warm=3):
+    """BASELINE.md's timing: the median of `reps` (>= 20) timed calls after `warm` untimed ones, each
+    call bracketed by its own HIP event pair on `stream` (the launch stream), after ~30 ms of untimed
+    calls so the clock has ramped (steady_ms).  Returns (median ms, [every call's ms])."""
+    fn()
+    one = max(timed_events(fn, stream, 1), 1e-3)
+    for _ in range(max(warm, int(30.0 / one))):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    ev[-1][1].synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
+    return ts[len(ts) // 2] if len(ts) % 2 else 0.5 * (ts[len(ts) // 2 - 1] + ts[len(ts) // 2]), ts
+
+
+def median_host_ms(fn, reps=21, warm=3):
+    """Host-to-host median of `reps` calls of a synchronous fn (host buffers in and out)."""
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t0) * 1000.0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def _smi_power():
     """(socket power W, power cap W, sclk MHz) from rocm-smi, or None (a child process, never exec)."""
     import re
@@ -360,6 +391,7 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
 
 
 MERKLE_SQ = os.path.join(ROOT, "profiles", "r03_pmc_merkle32.json")
+CPU_PROVE_2_20 = os.path.join(ROOT, "profiles", "r04_cpu_prove_synth_2_20.json")
 
 
 def merkle_valu_roofline(n: int, ms: float) -> dict:
@@ -593,19 +625,25 @@ def main():
             ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=False, stream=sptr)
             ctx.ntt_dev(b20.data_ptr(), 20, 1, w20, inverse=True, stream=sptr)
         pair()
-        pair_ms = steady_ms(pair, stream)
+        pair_ms, _ = median_ms(pair, stream, reps=25)
         stream.synchronize()
         ok = bool(np.array_equal(b20.cpu().numpy().view(np.uint64).reshape(-1, 4), h20))
         extras["ntt_2^20_fwd_inv_ms"] = round(pair_ms, 4)
+        extras["ntt_2^20_fwd_inv_timing"] = "median of 25 event-timed pairs after warm-up"
         extras["ntt_2^20_fwd_inv_roundtrip_exact"] = ok
         # The host-buffer entry point (best_fft on a host Vec: H2D + NTT + D2H), PCIe-inclusive;
         # reported beside `value`, never as it.
         hc = host.copy()
-        ctx.best_fft(hc, w, log_n)
-        t_h = time.perf_counter()
-        ctx.best_fft(hc, w, log_n)
-        extras["best_fft_host_2^24_ms_pcie_inclusive"] = round((time.perf_counter() - t_h) * 1000.0, 2)
+        extras["best_fft_host_2^24_ms_pcie_inclusive"] = round(
+            median_host_ms(lambda: ctx.best_fft(hc, w, log_n), reps=21, warm=2), 2)
+        extras["best_fft_host_2^24_timing"] = "host-to-host median of 21 calls (H2D + NTT + D2H)"
         del hc
+        # BASELINE.md's timing of the headline transform: the median of 25 event-timed calls after
+        # warm-up (`value` above is the contract's mean over the K barrier-bracketed steps).
+        med, ts = median_ms(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=False, stream=sptr), stream, reps=25)
+        extras[f"ntt_2^{log_n}_median_ms"] = round(med, 4)
+        extras[f"ntt_2^{log_n}_median_elems_per_s"] = n / (med / 1000.0)
+        extras[f"ntt_2^{log_n}_min_max_ms"] = [round(ts[0], 4), round(ts[-1], 4)]
         # Size sweep 2^20..2^26 (north star: synthetic traces of 2^20-2^26 field elements), forward NTT,
         # HBM-resident; elements uniform below 2^252 (< p), generated on the device.
         sweep = {}
@@ -616,29 +654,35 @@ def main():
             t[:, 3] &= 0x0FFFFFFFFFFFFFFF
             ws = O.root_of_unity(ls)
             ctx.ntt_dev(t.data_ptr(), ls, 1, ws, inverse=False, stream=sptr)
-            ms = steady_ms(lambda: ctx.ntt_dev(t.data_ptr(), ls, 1, ws, inverse=False, stream=sptr), stream)
+            ms, _ = median_ms(lambda: ctx.ntt_dev(t.data_ptr(), ls, 1, ws, inverse=False, stream=sptr), stream,
+                              reps=25)
             sweep[f"2^{ls}"] = {"ms": round(ms, 4), "elems_per_s": (1 << ls) / (ms / 1000.0),
                                 "hbm_frac": round(64.0 * (1 << ls) / (ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)}
             del t
         torch.cuda.empty_cache()
         extras["ntt_sweep"] = sweep
+        extras["ntt_sweep_timing"] = "median of 25 event-timed transforms per size after warm-up"
         # inverse 2^24 throughput
         ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr)   # warm: builds the w^-1 tables
-        inv_ms = steady_ms(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream)
+        inv_ms, _ = median_ms(lambda: ctx.ntt_dev(dptr, log_n, 1, w, inverse=True, stream=sptr), stream, reps=25)
         extras["intt_2^24_elems_per_s"] = n / (inv_ms / 1000.0)
         # Merkle: 2^24 leaves of 32 B (canonical Fp, the FRI / L-tree leaves)
         tree = S.MerkleProofInPlace(ctx)
         tree.update_dev(dptr, n, 32, stream=sptr)
-        mk_ms = steady_ms(lambda: tree.update_dev(dptr, n, 32, stream=sptr), stream)
+        stream.synchronize()
+        tree.gen_proofs([])
+        merkle_root = tree.get_root()  # the CPU baseline below rebuilds this tree and compares roots
+        mk_ms, _ = median_ms(lambda: tree.update_dev(dptr, n, 32, stream=sptr), stream, reps=25)
         extras["merkle_2^24x32B_leaves_per_s"] = n / (mk_ms / 1000.0)
         extras["merkle_2^24x32B_ms"] = round(mk_ms, 4)
+        extras["merkle_timing"] = "median of 25 event-timed builds after warm-up"
         extras["merkle_roofline_frac"] = round(96.0 * n / (mk_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
         extras["merkle_valu_roofline"] = merkle_valu_roofline(n, mk_ms)
         # Secondary leaf shapes: 256-B leaves (the main tree's P|A|S|D1..B3 rows; the same
         # 512 MiB buffer read as 2^21 rows) and 2^20 x 40-B accumulator leaves.
         for cnt, ll, key in ((n // 8, 256, "merkle_2^21x256B"), (1 << 20, 40, "merkle_2^20x40B")):
             tree.update_dev(dptr, cnt, ll, stream=sptr)
-            t_ms = steady_ms(lambda: tree.update_dev(dptr, cnt, ll, stream=sptr), stream)
+            t_ms, _ = median_ms(lambda: tree.update_dev(dptr, cnt, ll, stream=sptr), stream, reps=25)
             extras[f"{key}_leaves_per_s"] = cnt / (t_ms / 1000.0)
             extras[f"{key}_ms"] = round(t_ms, 4)
         del tree
@@ -655,12 +699,14 @@ def main():
         ctx.ntt_dev(bf.data_ptr(), lf, 1, wf, stream=sptr)
         stream.synchronize()
         proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
+        fri_json_sha = sha256(proof.to_json())
         if big.get("fri_2^23"):
-            extras["fri_2^23_bitexact_vs_oracle_digest"] = sha256(proof.to_json()) == big["fri_2^23"]["json_sha256"]
-        t1 = time.perf_counter()
-        proof = ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8)
-        extras["fri_prove_2^23_ms"] = round((time.perf_counter() - t1) * 1000.0, 3)
+            extras["fri_2^23_bitexact_vs_oracle_digest"] = fri_json_sha == big["fri_2^23"]["json_sha256"]
+        extras["fri_prove_2^23_ms"] = round(median_host_ms(
+            lambda: ctx.prove_low_degree_dev(bf.data_ptr(), nf, wf, nf // 4, 8), reps=21, warm=2), 3)
+        extras["fri_prove_timing"] = "host-to-host median of 21 proofs (device-resident input, proof on the host)"
         extras["fri_layers"] = len(proof)
+        fri_vals = bf.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()  # the CPU baseline's input
         del bf, proof
         # End-to-end proof wall-clock (config 3: pedersen_test full prove on 1 GPU):
         # prove_with_witness = .r1cs/.wtns bytes -> trace -> mk_r1cs_proof -> StarkProof JSON.
@@ -821,13 +867,51 @@ def main():
         extras[f"ntt_2^{log_n}_bitexact_vs_cpu_baseline"] = cpu["gpu_output_bitexact"]
         del cpu_out
         if not args.no_extras:
-            # End-to-end CPU baseline: the oracle's restatement of mk_r1cs_proof on pedersen_test.
+            # The metric's other legs beside their GPU numbers, same inputs, each CPU output compared with
+            # the GPU's (one timed run each: ~10-40 s of CPU work).
+            legs = {}
+            # Merkle: gen_multi_proofs_multi_core (merkle_proof_in_place.rs:106-206) over the same 2^24
+            # x 32-B leaves.  The reference hashes every leaf and layer on one thread (it never calls
+            # worker.scope); its 2^floor(log2 cpus) subtrees run one after another.
+            leaves = host.tobytes()
+            t3 = time.perf_counter()
+            cpu_root, _ = o.merkle(leaves, n, 32, chunks=threads)
+            tm = time.perf_counter() - t3
+            del leaves
+            legs["merkle_2^24x32B"] = {
+                "value": n / tm, "unit": "leaves/s", "ms": round(tm * 1000.0, 1), "cores": 1, "threads": 1,
+                "kind": "port", "sample": f"one build of the bench's 2^24 x 32-B tree, {threads} subtrees hashed "
+                                          "in sequence on one thread (oracle C restatement)",
+                "gpu_root_bitexact": bool(cpu_root == merkle_root)}
+            # FRI: prove_low_degree (fri.rs:46-224) on the bench's precision-2^23 input, single-threaded
+            # like the reference (its Merkle builds are sequential and its fold is a serial loop).
+            t3 = time.perf_counter()
+            cpu_fri = o.prove_low_degree_json(fri_vals, wf, nf // 4, 8, chunks=threads)
+            tf = time.perf_counter() - t3
+            legs["fri_prove_2^23"] = {
+                "value": round(tf * 1000.0, 1), "unit": "ms", "cores": 1, "threads": 1, "kind": "port",
+                "sample": "one prove_low_degree at precision 2^23 (maxdeg 2^21, exclude 8) on the bench's input "
+                          "(oracle C restatement)",
+                "gpu_json_bitexact": bool(sha256(cpu_fri) == fri_json_sha)}
+            del cpu_fri
+            # End-to-end: the oracle's restatement of mk_r1cs_proof on pedersen_test.
             import r1cs as R
             tr = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "pedersen_test"))
             t3 = time.perf_counter()
             R.mk_r1cs_proof_json(o, tr, cpus=threads)
             extras["prove_pedersen_cpu_port_ms"] = round((time.perf_counter() - t3) * 1000.0, 1)
             extras["prove_pedersen_cpu_port_threads"] = threads
+            legs["prove_pedersen"] = {"value": extras["prove_pedersen_cpu_port_ms"], "unit": "ms", "cores": threads,
+                                      "threads": threads, "kind": "port",
+                                      "sample": "one mk_r1cs_proof of pedersen_test (oracle C restatement)"}
+            # The 2^20-step proof on the CPU port takes minutes, so it is timed once by
+            # tools/cpu_prove_baseline.py on the GPU box and committed; reported here with its source.
+            try:
+                rec = json.load(open(CPU_PROVE_2_20))
+                legs["prove_synth_2^20_steps"] = rec
+            except (OSError, ValueError):
+                pass
+            extras["cpu_baselines"] = legs
 
     if rank == 0:
         line = {"metric": "2^24-pt NTT field-elems/sec", "value": value, "unit": "field-elems/s",

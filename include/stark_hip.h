@@ -61,6 +61,19 @@ const char* stark_status_str(stark_status s);
 const char* stark_ctx_last_error(const stark_ctx* ctx);
 /* Returns the HIP stream the context launches on (as void* = hipStream_t). */
 void* stark_ctx_stream(stark_ctx* ctx);
+/* Memory bound of the context's caches (no reference counterpart: the reference recomputes its
+ * twiddles per call, fft.rs:173).  The context caches the last NTT pass's full twiddle table per
+ * (root, size, direction) -- 2^log_n x 32 B, 512 MB at 2^24 -- and the extension of the index
+ * column per trace size (precision x 32 B).  Together they stay at or below `bytes` (default 4 GiB):
+ * least recently used entries are freed first (after a device synchronisation), a table that does
+ * not fit is not cached (the NTT's last pass then forms its twiddles from the two-level tables, same
+ * outputs).  Setting a lower cap frees down to it at once. */
+stark_status stark_ctx_set_cache_limit(stark_ctx* ctx, size_t bytes);
+/* Device bytes the context holds: cached tables (<= *cache_limit), and everything resident
+ * (cached tables, the small per-root twiddle tables, working arenas, context-owned trees).  Any
+ * pointer may be NULL. */
+stark_status stark_ctx_memory(const stark_ctx* ctx, size_t* cached_bytes, size_t* cache_limit,
+                              size_t* resident_bytes);
 
 /* ---- NTT (packages/fri/src/fft.rs) --------------------------------------- */
 /* best_fft<T>(coefficients: Vec<T>, root_of_unity: &T, log_order_of_root: u32) -> Vec<T>
@@ -197,10 +210,14 @@ stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, 
 /* Layer i's bytes (any pointer may be NULL): n_column 32-B column leaves and n_column x column_depth
  * 32-B siblings (leaf to root), the same for the n_poly poly openings, and n_last 32-B values of the
  * Last entry -- everything a caller needs to build FriProof<H> values itself (fri.rs:16-26) without
- * going through serde. */
+ * going through serde.  Each non-NULL output comes with its capacity in bytes; the sizes it needs are
+ * (from stark_fri_proof_layer_info) column_leaves 32 n_column, column_nodes 32 n_column column_depth,
+ * poly_leaves 32 n_poly, poly_nodes 32 n_poly poly_depth, last_values 32 n_last.  A capacity below
+ * that is STARK_ERR_BAD_LENGTH, and then no output is written. */
 stark_status stark_fri_proof_layer_data(const stark_fri_proof* proof, size_t i, uint8_t* column_leaves,
-                                        uint8_t* column_nodes, uint8_t* poly_leaves, uint8_t* poly_nodes,
-                                        uint8_t* last_values);
+                                        size_t column_leaves_cap, uint8_t* column_nodes, size_t column_nodes_cap,
+                                        uint8_t* poly_leaves, size_t poly_leaves_cap, uint8_t* poly_nodes,
+                                        size_t poly_nodes_cap, uint8_t* last_values, size_t last_values_cap);
 
 /* ---- R1CS STARK prover (packages/r1cs-stark) -------------------------------- */
 /* mk_r1cs_proof<Fp, BlakeDigest>(witness_trace, computational_trace, public_wires,
@@ -224,9 +241,12 @@ stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_roo
                                     uint8_t a_root[32]);
 /* StarkProof's openings (utils.rs:122-130): which = 0 main_branches (k = 320, 256-B leaves),
  * 1 linear_comb_branches (k = 80, 32-B leaves); leaves k x leaf_len bytes, nodes k x depth x 32 bytes
- * (siblings leaf to root).  Any output pointer may be NULL (query the sizes first). */
+ * (siblings leaf to root).  Any output pointer may be NULL (query the sizes first); leaves_cap and
+ * nodes_cap are the byte capacities of the two buffers, and one below k x leaf_len (resp.
+ * k x depth x 32) is STARK_ERR_BAD_LENGTH with neither buffer written. */
 stark_status stark_r1cs_proof_branches(const stark_r1cs_proof* proof, int which, size_t* k, size_t* leaf_len,
-                                       size_t* depth, uint8_t* leaves, uint8_t* nodes);
+                                       size_t* depth, uint8_t* leaves, size_t leaves_cap, uint8_t* nodes,
+                                       size_t nodes_cap);
 /* StarkProof's fri_proof, borrowed (valid until stark_r1cs_proof_free); read it with the
  * stark_fri_proof_* accessors. */
 const stark_fri_proof* stark_r1cs_proof_fri(const stark_r1cs_proof* proof);

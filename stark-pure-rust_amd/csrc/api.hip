@@ -37,6 +37,65 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   return STARK_OK;
 }
 
+size_t cache_bytes(const stark_ctx* ctx) {
+  size_t b = 0;
+  for (const auto& kv : ctx->tw) {
+    const size_t full = ((size_t)1 << kv.second->log_n) * sizeof(fe);
+    if (kv.second->d_full) b += full;
+    if (kv.second->d_full_s) b += full;
+  }
+  for (const auto& kv : ctx->ext_idx) b += kv.second.bytes;
+  return b;
+}
+
+bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext) {
+  if (need > ctx->cache_limit) return false;
+  bool synced = false;
+  for (size_t have = cache_bytes(ctx); have + need > ctx->cache_limit;) {
+    // the least recently used candidate
+    fe** full_slot = nullptr;
+    size_t full_bytes = 0;
+    auto ext_it = ctx->ext_idx.end();
+    uint64_t oldest = UINT64_MAX;
+    for (auto& kv : ctx->tw) {
+      Twiddles& t = *kv.second;
+      const size_t bytes = ((size_t)1 << t.log_n) * sizeof(fe);
+      if (t.d_full && t.full_used < oldest) {
+        oldest = t.full_used;
+        full_slot = &t.d_full;
+        full_bytes = bytes;
+      }
+      if (t.d_full_s && t.full_s_used < oldest) {
+        oldest = t.full_s_used;
+        full_slot = &t.d_full_s;
+        full_bytes = bytes;
+      }
+    }
+    if (evict_ext)
+      for (auto it = ctx->ext_idx.begin(); it != ctx->ext_idx.end(); ++it)
+        if (it->second.used < oldest) {
+          oldest = it->second.used;
+          ext_it = it;
+          full_slot = nullptr;
+        }
+    if (!full_slot && ext_it == ctx->ext_idx.end()) return false;
+    if (!synced) {
+      hipDeviceSynchronize();
+      synced = true;
+    }
+    if (full_slot) {
+      hipFree(*full_slot);
+      *full_slot = nullptr;
+      have -= full_bytes;
+    } else {
+      hipFree(ext_it->second.ptr);
+      have -= ext_it->second.bytes;
+      ctx->ext_idx.erase(ext_it);
+    }
+  }
+  return true;
+}
+
 namespace {
 
 class HostWorkers {
@@ -249,13 +308,39 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   if (ctx->staged) hipEventDestroy(ctx->staged);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
-                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde})
+                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
 const char* stark_ctx_last_error(const stark_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+stark_status stark_ctx_set_cache_limit(stark_ctx* ctx, size_t bytes) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->cache_limit = bytes;
+  cache_reserve(ctx, 0, true);  // down to the new cap at once (every cached entry is a candidate here)
+  return STARK_OK;
+}
+
+stark_status stark_ctx_memory(const stark_ctx* ctx, size_t* cached_bytes, size_t* cache_limit,
+                              size_t* resident_bytes) {
+  if (!ctx) return STARK_ERR_BAD_ARG;
+  const size_t cached = cache_bytes(ctx);
+  size_t total = cached;
+  for (const auto& kv : ctx->tw) total += kv.second->base_bytes;
+  for (const DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena,
+                          &ctx->trace_raw, &ctx->fri_misc, &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde,
+                          &ctx->ext_idx_tmp})
+    total += b->ptr ? b->bytes : 0;
+  for (const stark_merkle_tree* t : ctx->trees) total += merkle_device_bytes(t);
+  for (const stark_merkle_tree* t : ctx->fri_trees) total += merkle_device_bytes(t);
+  if (cached_bytes) *cached_bytes = cached;
+  if (cache_limit) *cache_limit = ctx->cache_limit;
+  if (resident_bytes) *resident_bytes = total;
+  return STARK_OK;
+}
 void* stark_ctx_stream(stark_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 stark_status stark_best_fft(stark_ctx* ctx, const uint64_t* coeffs, size_t len, const uint64_t root[4], uint32_t log_n,

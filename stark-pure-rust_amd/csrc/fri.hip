@@ -575,18 +575,23 @@ stark_status stark_fri_proof_layer_info(const stark_fri_proof* proof, size_t i, 
 }
 
 stark_status stark_fri_proof_layer_data(const stark_fri_proof* proof, size_t i, uint8_t* column_leaves,
-                                        uint8_t* column_nodes, uint8_t* poly_leaves, uint8_t* poly_nodes,
-                                        uint8_t* last_values) {
+                                        size_t column_leaves_cap, uint8_t* column_nodes, size_t column_nodes_cap,
+                                        uint8_t* poly_leaves, size_t poly_leaves_cap, uint8_t* poly_nodes,
+                                        size_t poly_nodes_cap, uint8_t* last_values, size_t last_values_cap) {
   if (!proof || i >= proof->layers.size()) return STARK_ERR_BAD_ARG;
   const stark_fri_layer& L = proof->layers[i];
-  auto put = [](uint8_t* dst, const std::vector<uint8_t>& v) {
-    if (dst && !v.empty()) memcpy(dst, v.data(), v.size());
-  };
-  put(column_leaves, L.col_leaves);
-  put(column_nodes, L.col_nodes);
-  put(poly_leaves, L.poly_leaves);
-  put(poly_nodes, L.poly_nodes);
-  put(last_values, L.last_values);
+  // Every capacity is checked before anything is written: a short buffer is STARK_ERR_BAD_LENGTH
+  // and leaves all five outputs untouched.
+  const std::pair<const std::vector<uint8_t>*, std::pair<uint8_t*, size_t>> outs[5] = {
+      {&L.col_leaves, {column_leaves, column_leaves_cap}},
+      {&L.col_nodes, {column_nodes, column_nodes_cap}},
+      {&L.poly_leaves, {poly_leaves, poly_leaves_cap}},
+      {&L.poly_nodes, {poly_nodes, poly_nodes_cap}},
+      {&L.last_values, {last_values, last_values_cap}}};
+  for (const auto& o : outs)
+    if (o.second.first && o.second.second < o.first->size()) return STARK_ERR_BAD_LENGTH;
+  for (const auto& o : outs)
+    if (o.second.first && !o.first->empty()) memcpy(o.second.first, o.first->data(), o.first->size());
   return STARK_OK;
 }
 

@@ -76,6 +76,8 @@ struct Twiddles {
   // the two of lo * hi, for one 32-B coalesced read.
   fe* d_full = nullptr;
   fe* d_full_s = nullptr;
+  uint64_t full_used = 0, full_s_used = 0;  // cache clock of their last use (LRU eviction, cache_reserve)
+  size_t base_bytes = 0;         // device bytes of the tables above d_full (one allocation at d_lo)
   size_t n_small_pairs = 0;      // Shoup pairs in d_small
   // Digit-basis tables (fe_db.h) of w_R^k, k < R/2, for every radix R = 2^l >= 16: the constants of the
   // radix-4 steps (ntt.hip DbPlan).  db_off[l] = offset in u32 into d_db (72 u32 per root).
@@ -84,6 +86,17 @@ struct Twiddles {
   HostFp root;      // the root these tables were built for (Montgomery)
   HostFp inv_n;     // n^-1 (Montgomery)
 };
+
+// A cached device buffer with the cache clock of its last use.
+struct CacheBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  uint64_t used = 0;
+};
+
+// Default cap on a context's cached tables (the last-pass full twiddle tables, 2^log_n x 32 B per
+// direction, and the shared IDX extensions): both directions of a 2^26 transform.
+constexpr size_t kDefaultCacheLimit = (size_t)4 << 30;
 
 }  // namespace stark
 
@@ -100,6 +113,7 @@ struct stark_ctx {
   stark::DevBuf trace_raw;    // the raw constraint section and witness bytes it reads
   stark::DevBuf lde_tmp;      // circuit_lde's step columns and Zb values
   stark::DevBuf verify_arena, verify_lde;  // the verifier's circuit, kept for the next call
+  stark::DevBuf ext_idx_tmp;  // an IDX extension too large for the cache cap (this proof only)
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -113,7 +127,11 @@ struct stark_ctx {
   // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
   // (prove.rs:160-163) at that rank's points: it depends on the trace length only, so every
   // proof of that size shares it (r1cs.hip ext_index_column).
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, stark::DevBuf> ext_idx;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, stark::CacheBuf> ext_idx;
+  // Cached tables (full twiddle tables + ext_idx) stay under cache_limit bytes: least recently used
+  // ones are freed first (stark::cache_reserve).  stark_ctx_set_cache_limit changes it.
+  size_t cache_limit = stark::kDefaultCacheLimit;
+  uint64_t cache_clock = 0;
 };
 
 namespace stark {
@@ -126,6 +144,13 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
   } while (0)
 
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
+// Bytes held by the context's cached tables (full twiddle tables and IDX extensions).
+size_t cache_bytes(const stark_ctx* ctx);
+// Makes room for `need` more cached bytes under ctx->cache_limit by freeing least recently used
+// entries (after a device synchronisation: a kernel of any stream may still read them).  Full
+// twiddle tables are always candidates; IDX extensions only with evict_ext (a proof's start, where
+// no pointer into one is held).  False when the bytes cannot fit (the caller then does not cache).
+bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext);
 // Context-owned pinned host scratch of at least `bytes` (async copy target).
 // Slot 0: gather batches; slot 1: transcript values and roots; slot 2: the device trace builder's
 // record-walk tables; slot 3: its upload staging (the raw .r1cs constraint section and witness).
@@ -167,6 +192,7 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
                           hipStream_t stream, size_t plane_stride = 0);
 stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t);
+size_t merkle_device_bytes(const stark_merkle_tree* t);  // device memory the tree owns (0 for null)
 stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* indices, size_t k,
                            uint8_t* leaves_out, uint8_t* nodes_out, hipStream_t stream, bool sync = true);
 

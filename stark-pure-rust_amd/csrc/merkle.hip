@@ -473,6 +473,13 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
 }
 
 // Device address of the root digest (valid after merkle_build).
+size_t merkle_device_bytes(const stark_merkle_tree* t) {
+  if (!t) return 0;
+  size_t b = 0;
+  for (const DevBuf* d : {&t->nodes, &t->own_leaves, &t->gather}) b += d->ptr ? d->bytes : 0;
+  return b;
+}
+
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t) {
   return (const uint8_t*)t->nodes.ptr + (2 * t->n - 2) * sizeof(Digest);
 }

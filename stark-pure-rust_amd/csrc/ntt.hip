@@ -839,6 +839,7 @@ stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n
   tw->d_hi_s = tw->d_t16 + 2 * n16;
   tw->d_t16_s = tw->d_hi_s + n_hi;
   tw->d_db = reinterpret_cast<uint32_t*>(tw->d_t16_s + 2 * n16);
+  tw->base_bytes = bytes;
   STARK_HIP(ctx, hipMemcpy(tw->d_lo, h_lo.data(), n_lo * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_hi, h_hi.data(), n_hi * sizeof(fe), hipMemcpyHostToDevice));
   STARK_HIP(ctx, hipMemcpy(tw->d_small, h_small.data(), h_small.size() * sizeof(fe), hipMemcpyHostToDevice));
@@ -862,16 +863,20 @@ __global__ void full_tw_kernel(const fe* __restrict__ lo, const fe* __restrict__
   fe_store(out + g, t);
 }
 
-// The last pass's full twiddle table, built once per (root, n, direction).
+// The last pass's full twiddle table, built once per (root, n, direction) and kept in the context's
+// size-capped cache (cache_reserve: least recently used tables go first).  When it cannot be cached
+// (larger than the cap, or no device memory) *out is null and the pass takes the two-level form.
 static stark_status full_table(stark_ctx* ctx, const Twiddles& tw_c, uint32_t log_r, bool scaled, hipStream_t stream,
                                const fe** out) {
   Twiddles& tw = const_cast<Twiddles&>(tw_c);  // lazily filled cache entry
   fe*& slot = scaled ? tw.d_full_s : tw.d_full;
+  (scaled ? tw.full_s_used : tw.full_used) = ++ctx->cache_clock;
   if (!slot) {
     const uint64_t n = (uint64_t)1 << tw.log_n;
     void* d = nullptr;
-    if (hipMalloc(&d, n * sizeof(fe)) != hipSuccess) {
-      *out = nullptr;  // no room: fall back to the two-level form
+    if (!cache_reserve(ctx, n * sizeof(fe), false) || hipMalloc(&d, n * sizeof(fe)) != hipSuccess) {
+      hipGetLastError();  // (a failed allocation is not an error here)
+      *out = nullptr;     // no room: fall back to the two-level form
       return STARK_OK;
     }
     hipLaunchKernelGGL(full_tw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, tw.d_lo, tw.d_hi,

@@ -220,13 +220,12 @@ __device__ __forceinline__ fe pow_tab(const fe* __restrict__ lo, const fe* __res
 // IDX / PIDX step columns (prove.rs:160-167 with the identity tail of
 // prove.rs:55-56) and the accumulator leaves u64 LE index || to_bytes_le(w)
 // (utils.rs:254-263).
+// (IDX itself is not written: its extension is the context's shared ext_index_column.)
 __global__ void r1cs_index_kernel(const uint64_t* __restrict__ perm, uint64_t os, uint64_t steps,
-                                  const fe* __restrict__ w, fe* __restrict__ idx, fe* __restrict__ pidx,
-                                  uint64_t* __restrict__ acc_leaves) {
+                                  const fe* __restrict__ w, fe* __restrict__ pidx, uint64_t* __restrict__ acc_leaves) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= steps) return;
   const uint64_t p = i < os ? perm[i] : i;
-  fe_store(idx + i, fe_from_u64(i));
   fe_store(pidx + i, fe_from_u64(p));
   const fe x = fe_load(w + i);
   uint64_t* leaf = acc_leaves + 5 * i;
@@ -723,14 +722,30 @@ static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_
   const auto key = std::make_tuple(log_steps, log_prec, log_g, r);
   auto it = ctx->ext_idx.find(key);
   if (it != ctx->ext_idx.end()) {
+    it->second.used = ++ctx->cache_clock;
     *out = (const fe*)it->second.ptr;
     return STARK_OK;
   }
   const uint64_t steps = (uint64_t)1 << log_steps, P = (uint64_t)1 << (log_prec - log_g);
+  // Counted in the context's capped cache (stark_ctx_set_cache_limit).  An extension larger than the
+  // cap lives in a per-context buffer for this proof only and is recomputed by the next one.
+  const bool cached = cache_reserve(ctx, P * sizeof(fe), true);
   void *col = nullptr, *coef = nullptr;
-  if (hipMalloc(&col, P * sizeof(fe)) != hipSuccess) return STARK_ERR_OOM;
+  if (cached) {
+    if (hipMalloc(&col, P * sizeof(fe)) != hipSuccess) return STARK_ERR_OOM;
+    ctx->ext_idx[key] = CacheBuf{col, P * sizeof(fe), ++ctx->cache_clock};  // counted while it is built
+  } else {
+    STARK_TRY(ensure_buf(ctx, ctx->ext_idx_tmp, P * sizeof(fe)));
+    col = ctx->ext_idx_tmp.ptr;
+  }
+  auto drop = [&] {
+    if (cached) {
+      ctx->ext_idx.erase(key);
+      hipFree(col);
+    }
+  };
   if (hipMalloc(&coef, steps * sizeof(fe)) != hipSuccess) {
-    hipFree(col);
+    drop();
     return STARK_ERR_OOM;
   }
   hipLaunchKernelGGL(iota_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (fe*)coef, steps);
@@ -740,10 +755,9 @@ static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_
   if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
   hipFree(coef);
   if (st != STARK_OK) {
-    hipFree(col);
+    drop();
     return st;
   }
-  ctx->ext_idx[key] = DevBuf{col, P * sizeof(fe)};
   *out = (const fe*)col;
   return STARK_OK;
 }
@@ -854,11 +868,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   Transcript* d_tr;
   const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
   Carve cv;
-  cv.add(&raw, 8 * steps);  // K F0 F1 F2 S P PIDX IDX (then A's coefficients reuse K's slot)
+  cv.add(&raw, 7 * steps);  // K F0 F1 F2 S P PIDX (then A's coefficients reuse K's slot)
   cv.add(&wcopy, steps);
   cv.add(&perm, steps);
   cv.add(&acc_leaves, 5 * steps);
-  cv.add(&cols, 9 * prec);
+  cv.add(&cols, 8 * prec);  // the extensions of K F0 F1 F2 S P PIDX A (IDX's is shared: idx_ext)
   cv.add(&nmr, steps);
   cv.add(&dnm, steps);
   cv.add(&tot, 2 * (size_t)nb);
@@ -897,9 +911,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   clk.mark("setup + uploads enqueued");
   STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
-  // (IDX lands in slot 7 and is not extended: idx_ext is the shared extension.)
+  // (IDX is not materialised: idx_ext is the shared extension.)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 7 * steps, raw + 6 * steps, acc_leaves);
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves);
   STARK_HIP(ctx, hipGetLastError());
 
   auto proof = std::make_unique<stark_r1cs_proof>();
@@ -929,7 +943,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
                      (const fe*)inv_dnm, steps, raw);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(lde(ctx, raw, 1, cols + 8 * prec, log_steps, log_prec, *tw1i, *tw2, s));
+  STARK_TRY(lde(ctx, raw, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
 
   if (!pre) {  // prepared circuits carry these (they depend on the public wires' positions only)
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
@@ -941,8 +955,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
 
   // Constraint kernel.
   ConstraintArgs ca;
-  for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * prec;
+  for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * prec;
   ca.col[6] = ext_idx;
+  ca.col[8] = cols + 7 * prec;  // A
   ca.col[7] = ext_pidx;
   if (pre)
     for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * prec;
@@ -1281,11 +1296,11 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   uint64_t* acc_leaves;
   const uint32_t nb = (uint32_t)((steps + kScanBlock - 1) / kScanBlock);
   Carve cv;
-  cv.add(&raw, 8 * steps);
+  cv.add(&raw, 7 * steps);  // K F0 F1 F2 S P PIDX
   cv.add(&wcopy, steps);
   cv.add(&perm, steps);
   cv.add(&acc_leaves, 5 * steps);
-  cv.add(&cols, 9 * P);
+  cv.add(&cols, 8 * P);  // K F0 F1 F2 S P PIDX A (IDX's extension is shared: idx_ext)
   cv.add(&nmr, steps);
   cv.add(&dnm, steps);
   cv.add(&tot, 2 * (size_t)nb);
@@ -1320,9 +1335,9 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(d.d_tr, 0, sizeof(Transcript), s));
-  // (PIDX in slot 6, IDX in slot 7, not extended: idx_ext)
+  // (PIDX in slot 6; IDX is not materialised: idx_ext)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 7 * steps, raw + 6 * steps, acc_leaves);
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves);
   STARK_HIP(ctx, hipGetLastError());
   // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
   STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
@@ -1345,7 +1360,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
                      (const fe*)inv_dnm, steps, raw);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(lde_coset(d, raw, 1, cols + 8 * P, *tw1i, *tw2, *twh));
+  STARK_TRY(lde_coset(d, raw, 1, cols + 7 * P, *tw1i, *tw2, *twh));  // A in slot 7
   if (!pre) {  // Zb2 / Zb3 at this rank's points and their inverses
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                        (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
@@ -1354,7 +1369,8 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
     STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
   }
   ConstraintArgs ca;
-  for (int c = 0; c < 9; ++c) ca.col[c] = cols + (size_t)c * P;
+  for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * P;
+  ca.col[8] = cols + 7 * P;  // A
   ca.inv_zb = pre ? pre + 6 * P : inv_zb;
   ca.col[6] = pre ? pre + 4 * P : idx_ext;
   ca.col[7] = pre ? pre + 5 * P : cols + 6 * P;
@@ -1451,7 +1467,8 @@ stark_status stark_r1cs_proof_roots(const stark_r1cs_proof* proof, uint8_t m_roo
 }
 
 stark_status stark_r1cs_proof_branches(const stark_r1cs_proof* proof, int which, size_t* k, size_t* leaf_len,
-                                       size_t* depth, uint8_t* leaves, uint8_t* nodes) {
+                                       size_t* depth, uint8_t* leaves, size_t leaves_cap, uint8_t* nodes,
+                                       size_t nodes_cap) {
   if (!proof || (which != 0 && which != 1)) return STARK_ERR_BAD_ARG;
   const size_t ll = which == 0 ? 256 : 32;
   const std::vector<uint8_t>& lv = which == 0 ? proof->m_leaves : proof->l_leaves;
@@ -1459,6 +1476,8 @@ stark_status stark_r1cs_proof_branches(const stark_r1cs_proof* proof, int which,
   if (k) *k = lv.size() / ll;
   if (leaf_len) *leaf_len = ll;
   if (depth) *depth = proof->depth;
+  // capacities checked before either buffer is written
+  if ((leaves && leaves_cap < lv.size()) || (nodes && nodes_cap < nd.size())) return STARK_ERR_BAD_LENGTH;
   if (leaves) memcpy(leaves, lv.data(), lv.size());
   if (nodes) memcpy(nodes, nd.data(), nd.size());
   return STARK_OK;

@@ -254,7 +254,9 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
       at += len;
     }
   std::atomic<size_t> next{0};
-  std::atomic<int> failed{0};
+  // The first failing copy's error, recorded by the worker that saw it (HIP's last-error state is
+  // per thread, so the caller could not read it back with hipGetLastError).
+  std::atomic<int> failed{(int)hipSuccess};
   // thread 1 runs `beside` (the record walk); every other thread stages chunks in order of claim
   host_parallel(workers + 1, [&](unsigned t) {
     if (t == 1) {
@@ -262,13 +264,22 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
       return;
     }
     for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+      if (failed.load(std::memory_order_relaxed) != (int)hipSuccess) break;
       const Piece& p = pieces[i];
       memcpy(p.stage, p.src, p.len);
-      if (hipMemcpyAsync(p.dst, p.stage, p.len, hipMemcpyHostToDevice, s) != hipSuccess) failed = 1;
+      const hipError_t e = hipMemcpyAsync(p.dst, p.stage, p.len, hipMemcpyHostToDevice, s);
+      int ok = (int)hipSuccess;
+      if (e != hipSuccess) failed.compare_exchange_strong(ok, (int)e);
     }
   });
-  if (failed) return hip_fail(ctx, hipGetLastError(), "r1cs/wtns upload");
-  STARK_HIP(ctx, hipEventRecord(ctx->staged, s));
+  // Recorded on the error path too: DMAs already enqueued from the staging buffer must be covered by
+  // the event the next call waits on before it writes that buffer again.
+  const hipError_t rec = hipEventRecord(ctx->staged, s);
+  if (failed.load() != (int)hipSuccess) {
+    if (rec != hipSuccess) hipStreamSynchronize(s);  // no event: drain the stream instead
+    return hip_fail(ctx, (hipError_t)failed.load(), "r1cs/wtns upload");
+  }
+  if (rec != hipSuccess) return hip_fail(ctx, rec, "hipEventRecord(staged)");
   return STARK_OK;
 }
 

@@ -50,6 +50,8 @@ _SIGNATURES = {
     "stark_status_str": ([ctypes.c_int], ctypes.c_char_p),
     "stark_ctx_last_error": ([_vp], ctypes.c_char_p),
     "stark_ctx_stream": ([_vp], _vp),
+    "stark_ctx_set_cache_limit": ([_vp, ctypes.c_size_t], ctypes.c_int),
+    "stark_ctx_memory": ([_vp, _szp, _szp, _szp], ctypes.c_int),
     "stark_best_fft": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p], ctypes.c_int),
     "stark_inv_best_fft": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p], ctypes.c_int),
     "stark_fft_in_place": ([_vp, _u64p, _u64p, ctypes.c_uint32, ctypes.c_int], ctypes.c_int),
@@ -80,14 +82,15 @@ _SIGNATURES = {
     "stark_fri_proof_num_layers": ([_vp], ctypes.c_size_t),
     "stark_fri_proof_layer_info": ([_vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), _u8p, _szp, _szp, _szp,
                                     _szp, _szp], ctypes.c_int),
-    "stark_fri_proof_layer_data": ([_vp, ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p], ctypes.c_int),
+    "stark_fri_proof_layer_data": ([_vp, ctypes.c_size_t] + [_u8p, ctypes.c_size_t] * 5, ctypes.c_int),
     "stark_mk_r1cs_proof": ([_vp, _u64p, _u64p, ctypes.c_size_t, _u64p, ctypes.c_size_t, _szp, ctypes.c_size_t,
                              _szp, _u64p, _u64p, _u64p, _u64p, ctypes.c_size_t, ctypes.c_size_t,
                              ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_proof_json": ([_vp, ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
     "stark_r1cs_proof_json_view": ([_vp, ctypes.POINTER(ctypes.c_void_p), _szp], ctypes.c_int),
     "stark_r1cs_proof_roots": ([_vp, _u8p, _u8p, _u8p], ctypes.c_int),
-    "stark_r1cs_proof_branches": ([_vp, ctypes.c_int, _szp, _szp, _szp, _u8p, _u8p], ctypes.c_int),
+    "stark_r1cs_proof_branches": ([_vp, ctypes.c_int, _szp, _szp, _szp, _u8p, ctypes.c_size_t, _u8p,
+                                   ctypes.c_size_t], ctypes.c_int),
     "stark_r1cs_proof_fri": ([_vp], _vp),
     "stark_r1cs_proof_free": ([_vp], None),
     "stark_r1cs_trace_build": ([_u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
@@ -225,6 +228,16 @@ class Context:
 
     def synchronize(self):
         self.check(self.lib.stark_ctx_synchronize(self.h), "synchronize")
+
+    def set_cache_limit(self, nbytes: int):
+        """Cap on the context's cached tables (full last-pass twiddle tables, IDX extensions)."""
+        self.check(self.lib.stark_ctx_set_cache_limit(self.h, int(nbytes)), "set_cache_limit")
+
+    def memory(self) -> dict:
+        """{'cached': bytes of cached tables, 'cache_limit': their cap, 'resident': all device bytes held}."""
+        c, l, r = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        self.check(self.lib.stark_ctx_memory(self.h, ctypes.byref(c), ctypes.byref(l), ctypes.byref(r)), "memory")
+        return {"cached": c.value, "cache_limit": l.value, "resident": r.value}
 
     # ---- fri::fft ----------------------------------------------------------
     def best_fft(self, coefficients, root_of_unity, log_order_of_root: int) -> np.ndarray:

@@ -88,7 +88,15 @@ static void fri_proof(std::string& o, const stark_fri_proof* p) {
     size_t nc = 0, cd = 0, np = 0, pd = 0, nl = 0;
     check(stark_fri_proof_layer_info(p, i, &is_last, root2, &nc, &cd, &np, &pd, &nl), "fri layer info");
     std::vector<uint8_t> cl(32 * nc), cn(32 * nc * cd), pl(32 * np), pn(32 * np * pd), last(32 * nl);
-    check(stark_fri_proof_layer_data(p, i, cl.data(), cn.data(), pl.data(), pn.data(), last.data()), "fri layer data");
+    // a buffer one byte short must be refused untouched (capacity check), the exact sizes accepted
+    if (!cl.empty() && stark_fri_proof_layer_data(p, i, cl.data(), cl.size() - 1, nullptr, 0, nullptr, 0, nullptr, 0,
+                                                  nullptr, 0) != STARK_ERR_BAD_LENGTH) {
+      fprintf(stderr, "stark_fri_proof_layer_data: short buffer accepted\n");
+      exit(1);
+    }
+    check(stark_fri_proof_layer_data(p, i, cl.data(), cl.size(), cn.data(), cn.size(), pl.data(), pl.size(),
+                                     pn.data(), pn.size(), last.data(), last.size()),
+          "fri layer data");
     if (i) o += ',';
     if (is_last) {
       o += "{\"Last\":{\"last\":[";
@@ -122,9 +130,16 @@ static std::string from_parts(const stark_r1cs_proof* p) {
   bytes(o, a, 32);
   for (int which = 0; which < 2; ++which) {
     size_t k = 0, ll = 0, depth = 0;
-    check(stark_r1cs_proof_branches(p, which, &k, &ll, &depth, nullptr, nullptr), "branches (sizes)");
+    check(stark_r1cs_proof_branches(p, which, &k, &ll, &depth, nullptr, 0, nullptr, 0), "branches (sizes)");
     std::vector<uint8_t> leaves(k * ll), nodes(k * depth * 32);
-    check(stark_r1cs_proof_branches(p, which, &k, &ll, &depth, leaves.data(), nodes.data()), "branches");
+    if (stark_r1cs_proof_branches(p, which, &k, &ll, &depth, leaves.data(), leaves.size(), nodes.data(),
+                                  nodes.size() - 1) != STARK_ERR_BAD_LENGTH) {
+      fprintf(stderr, "stark_r1cs_proof_branches: short buffer accepted\n");
+      exit(1);
+    }
+    check(stark_r1cs_proof_branches(p, which, &k, &ll, &depth, leaves.data(), leaves.size(), nodes.data(),
+                                    nodes.size()),
+          "branches");
     o += which == 0 ? ",\"main_branches\":" : ",\"linear_comb_branches\":";
     branches(o, leaves, ll, nodes, k, depth);
   }

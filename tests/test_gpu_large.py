@@ -131,3 +131,40 @@ def test_fft_in_place_vs_oracle(ctx, oracle, log_n):
     u = c.copy()
     ctx.inv_serial_fft(u, w, log_n)
     assert np.array_equal(u, oracle.inv_best_fft(c, w, log_n, cpus=8))
+
+
+def test_twiddle_cache_stays_under_cap(oracle):
+    """The context's cached tables (the last pass's full twiddle table per size and direction, 2^log_n x
+    32 B: 1 GiB at 2^25, 2 GiB at 2^26) stay under a 1 GiB cap while one context transforms 2^20 .. 2^27
+    forward and inverse, and every transform still equals the oracle's digest (2^21 - 2^23: the round
+    trip).  2^26's table does not fit the cap, so its last pass forms the twiddles from the two-level
+    tables instead; 2^25's fits only after the others are evicted (least recently used first)."""
+    import stark_amd as S
+    cap = 1 << 30
+    c = S.Context(0)
+    try:
+        c.set_cache_limit(cap)
+        for log_n in range(20, 28):
+            n = 1 << log_n
+            x = O.random_elements(n, 0x5EED0000 + log_n)
+            w = O.root_of_unity(log_n)
+            fwd = _ntt_dev(c, x, log_n, w, inverse=False)
+            m = c.memory()
+            assert m["cache_limit"] == cap and m["cached"] <= cap, (log_n, m)
+            rec = BIG.get(f"ntt_2^{log_n}")
+            if rec:
+                assert _sha(x) == rec["input_sha256"]
+                assert _sha(fwd) == rec["forward_sha256"], log_n
+                assert _sha(_ntt_dev(c, x, log_n, w, inverse=True)) == rec["inverse_sha256"], log_n
+            else:
+                assert np.array_equal(_ntt_dev(c, fwd, log_n, w, inverse=True), x), log_n
+            assert c.memory()["cached"] <= cap, log_n
+            del x, fwd
+        assert c.memory()["resident"] >= c.memory()["cached"]
+        c.set_cache_limit(0)  # frees every cached table at once
+        assert c.memory()["cached"] == 0
+        x = O.random_elements(1 << 24, 0x5EED0000 + 24)
+        assert _sha(_ntt_dev(c, x, 24, O.root_of_unity(24), inverse=False)) == BIG["ntt_2^24"]["forward_sha256"]
+        assert c.memory()["cached"] == 0
+    finally:
+        c.close()
