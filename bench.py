@@ -378,6 +378,13 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
     if rank == 0:
         out["prove_synth_2^20_steps_distributed_bitexact_vs_oracle_digest"] = sha256(js20) == want
     out["prove_synth_2^20_steps_distributed_ms"] = timed(rs, ws, 3)
+    # One more proof with this rank's per-phase times (host wall-clock and the device time line from
+    # HIP events on the proof's stream) and its count of host-synchronising steps (stark_amd/dprove.py).
+    st = {}
+    dist.barrier()
+    prove_distributed(ops, rs, ws, stats=st)
+    if rank == 0:
+        out["prove_synth_2^20_steps_distributed_phases_rank0"] = st
     # Prepared circuit per rank (DistCircuit: the .r1cs-only work outside the timed region), labelled.
     from stark_amd.dprove import DistCircuit
     circ = DistCircuit(ctx, rs)

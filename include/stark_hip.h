@@ -328,6 +328,15 @@ stark_status stark_merkle_leaf_digests_dev(stark_ctx* ctx, const uint8_t* d_leav
  * digest as the leaf bytes. */
 stark_status stark_merkle_update_digests_dev(stark_merkle_tree* tree, const uint8_t* d_digests, size_t n,
                                              uint32_t interleave, void* stream);
+/* The tree's root digest copied to device memory d_out (32 B), asynchronously on `stream`: the
+ * distributed prover all-gathers subtree roots without a host round trip. */
+stark_status stark_merkle_root_dev(const stark_merkle_tree* tree, uint8_t* d_out, void* stream);
+/* The top of a tree split into g subtrees (merkle_proof_in_place.rs:176-180, the chunk roots hashed as
+ * a tree of their own), on the device: d_roots holds the g subtree roots (g a power of two <= 1024,
+ * 32 B each), d_levels receives the g - 1 digests above them level by level (the g/2 parents of the
+ * roots first, the root last).  Both 16-B aligned.  Asynchronous on `stream`. */
+stark_status stark_merkle_top_dev(stark_ctx* ctx, const uint8_t* d_roots, size_t g, uint8_t* d_levels,
+                                  void* stream);
 /* Many openings in one launch: request i gathers, for its k indices, the leaves
  * (leaf_len bytes each) and log2(n) sibling digests of `tree`, or, when tree is
  * NULL, only the rows (row_bytes each) of the device buffer d_rows (n_rows rows).
@@ -349,6 +358,11 @@ stark_status stark_open_batch(stark_ctx* ctx, const stark_open_req* reqs, size_t
 stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
                                 const uint64_t root[4], const uint8_t m_root[32], uint32_t world, uint32_t rank,
                                 void* stream);
+/* Same with the layer's Merkle root in device memory (d_m_root, 32 B, 4-B aligned): special_x is
+ * derived on the device and nothing waits for the host (asynchronous on `stream`). */
+stark_status stark_fri_fold_dev_root(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                                     const uint64_t root[4], const uint8_t* d_m_root, uint32_t world, uint32_t rank,
+                                     void* stream);
 /* serde_json of StarkProof (utils.rs:122-130) from its parts. */
 typedef struct stark_branches {
   const uint8_t* leaves; /* k * leaf_len bytes */
@@ -396,6 +410,8 @@ stark_status stark_dprove_info(stark_dprove* h, size_t* precision, size_t* n_loc
 stark_status stark_dprove_rows(stark_dprove* h, uint8_t** rows_dev);
 /* k from m_root (prove.rs:274-283) and L at this rank's points (prove.rs:287-322). */
 stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uint64_t** l_dev);
+/* Same with m_root in device memory (4-B aligned): asynchronous on the stream given at begin. */
+stark_status stark_dprove_lincomb_dev(stark_dprove* h, const uint8_t* d_m_root, uint64_t** l_dev);
 void stark_dprove_free(stark_dprove* h);
 
 /* ---- device memory helpers (for callers without their own allocator) ------ */

@@ -452,10 +452,12 @@ void stark_fri_proof_free(stark_fri_proof* proof) { delete proof; }
 // `values` holds the layer's values at the points rank + world*j (n/world of
 // them), `column` receives the folded column at the same residue class of the
 // n/4 rows; special_x = from_bytes_le(m_root) (fri.rs:135).
-stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
-                                const uint64_t root[4], const uint8_t m_root[32], uint32_t world, uint32_t rank,
-                                void* stream) {
-  if (!ctx || !values || !column || !root || !m_root) return STARK_ERR_BAD_ARG;
+// special_x from a host root (m_root) or a device-resident one (d_m_root: the fold reads it on the stream,
+// no host round trip).
+static stark_status fri_fold(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                             const uint64_t root[4], const uint8_t* m_root, const uint8_t* d_m_root, uint32_t world,
+                             uint32_t rank, void* stream) {
+  if (!ctx || !values || !column || !root || (!m_root && !d_m_root)) return STARK_ERR_BAD_ARG;
   if (world == 0 || (world & (world - 1)) || rank >= world) return STARK_ERR_BAD_ARG;
   if (n < 4 || (n & (n - 1)) || (n / 4) % world != 0) return STARK_ERR_BAD_LENGTH;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
@@ -472,16 +474,37 @@ stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t
   st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
   if (st != STARK_OK) return st;
   fe* d_sx = (fe*)ctx->fri_misc.ptr + 15;  // slot 15: unused by prove_low_degree's <= 15 layers
-  const fe sx = to_dev(F.from_bytes_le(m_root, 32));
-  STARK_HIP(ctx, hipMemcpyAsync(d_sx, &sx, sizeof(fe), hipMemcpyHostToDevice, s));
+  fe sx;
+  if (m_root) {
+    sx = to_dev(F.from_bytes_le(m_root, 32));
+    STARK_HIP(ctx, hipMemcpyAsync(d_sx, &sx, sizeof(fe), hipMemcpyHostToDevice, s));
+  } else {  // fri.rs:135 on the device: the root read as LE words, reduced mod p, Montgomery image
+    hipLaunchKernelGGL(fri_special_x_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)d_m_root, d_sx,
+                       to_dev(F.from_canonical(F.one().v)));
+    STARK_HIP(ctx, hipGetLastError());
+  }
   const HostFp zeta = F.pow_u64(F.from_canonical(root), n / 4);
   const size_t q = n / 4 / world;
   hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, (const fe*)values,
                      (fe*)column, (uint64_t)q, (uint32_t)0, (uint64_t)rank, log_g, tw->d_lo, tw->d_hi, tw->kb,
                      (const fe*)d_sx, to_dev(zeta), to_dev(F.inv(F.from_u64(4))));
   STARK_HIP(ctx, hipGetLastError());
-  STARK_HIP(ctx, hipStreamSynchronize(s));  // sx lives on this stack frame
+  if (m_root) STARK_HIP(ctx, hipStreamSynchronize(s));  // sx lives on this stack frame
   return STARK_OK;
+}
+
+stark_status stark_fri_fold_dev(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                                const uint64_t root[4], const uint8_t m_root[32], uint32_t world, uint32_t rank,
+                                void* stream) {
+  if (!m_root) return STARK_ERR_BAD_ARG;
+  return fri_fold(ctx, values, column, n, root, m_root, nullptr, world, rank, stream);
+}
+
+stark_status stark_fri_fold_dev_root(stark_ctx* ctx, const uint64_t* values, uint64_t* column, size_t n,
+                                     const uint64_t root[4], const uint8_t* d_m_root, uint32_t world, uint32_t rank,
+                                     void* stream) {
+  if (!d_m_root || (((uintptr_t)d_m_root) & 3)) return STARK_ERR_BAD_ARG;
+  return fri_fold(ctx, values, column, n, root, nullptr, d_m_root, world, rank, stream);
 }
 
 // serde_json of a StarkProof (r1cs-stark/src/utils.rs:122-130) from its parts

@@ -401,6 +401,30 @@ __global__ void merkle_interleave_kernel(const Digest* __restrict__ chunks, uint
   store_digest(level0 + o, load_digest(chunks + r * (n >> log_g) + m));
 }
 
+// The top of a tree split into g subtrees (merkle_proof_in_place.rs:176-180): the g subtree roots
+// hashed pairwise level by level in LDS by one workgroup; out = the g - 1 digests above them, level
+// by level (the root last).
+constexpr uint32_t kTopMax = 1024;
+__global__ __launch_bounds__(kTopMax / 2) void merkle_top_kernel(const Digest* __restrict__ roots, uint32_t g,
+                                                                 Digest* __restrict__ out) {
+  __shared__ Digest lv[kTopMax];
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < g; i += blockDim.x) lv[i] = load_digest(roots + i);
+  __syncthreads();
+  uint32_t off = 0;
+  for (uint32_t w = g >> 1; w >= 1; w >>= 1) {
+    Digest d;
+    if (t < w) d = hash_pair(lv[2 * t], lv[2 * t + 1]);
+    __syncthreads();
+    if (t < w) {
+      lv[t] = d;
+      store_digest(out + off + t, d);
+    }
+    __syncthreads();
+    off += w;
+  }
+}
+
 // Builds every level of the tree over d_leaves (n leaves of leaf_len bytes);
 // with d_leaves == nullptr level 0 (the leaf digests) is already in place.
 // plane_stride != 0: leaf i's bytes [32 c, 32 c + 32) are at d_leaves + c * plane_stride + 32 i
@@ -472,7 +496,6 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   return STARK_OK;
 }
 
-// Device address of the root digest (valid after merkle_build).
 size_t merkle_device_bytes(const stark_merkle_tree* t) {
   if (!t) return 0;
   size_t b = 0;
@@ -480,6 +503,7 @@ size_t merkle_device_bytes(const stark_merkle_tree* t) {
   return b;
 }
 
+// Device address of the root digest (valid after merkle_build).
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t) {
   return (const uint8_t*)t->nodes.ptr + (2 * t->n - 2) * sizeof(Digest);
 }
@@ -715,6 +739,27 @@ stark_status stark_merkle_update_digests_dev(stark_merkle_tree* t, const uint8_t
                      (const Digest*)d_digests, (uint64_t)n, log_g, (Digest*)t->nodes.ptr);
   STARK_HIP(ctx, hipGetLastError());
   return merkle_build(ctx, t, nullptr, n, 32, s);
+}
+
+stark_status stark_merkle_root_dev(const stark_merkle_tree* t, uint8_t* d_out, void* stream) {
+  if (!t || !d_out) return STARK_ERR_BAD_ARG;
+  if (!t->built) return STARK_ERR_STATE;
+  stark_ctx* ctx = t->ctx;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  STARK_HIP(ctx, hipMemcpyAsync(d_out, merkle_root_dev(t), 32, hipMemcpyDeviceToDevice, pick_stream(ctx, stream)));
+  return STARK_OK;
+}
+
+stark_status stark_merkle_top_dev(stark_ctx* ctx, const uint8_t* d_roots, size_t g, uint8_t* d_levels, void* stream) {
+  if (!ctx || (g > 1 && (!d_roots || !d_levels))) return STARK_ERR_BAD_ARG;
+  if (g == 0 || (g & (g - 1)) || g > kTopMax) return STARK_ERR_BAD_LENGTH;
+  if ((((uintptr_t)d_roots) | ((uintptr_t)d_levels)) & 15) return STARK_ERR_BAD_ARG;  // 16-B digest loads
+  if (g == 1) return STARK_OK;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(merkle_top_kernel, dim3(1), dim3((unsigned)(g / 2)), 0, pick_stream(ctx, stream),
+                     (const Digest*)d_roots, (uint32_t)g, (Digest*)d_levels);
+  STARK_HIP(ctx, hipGetLastError());
+  return STARK_OK;
 }
 
 // Every opening of a distributed proof on this rank in one zero-copy gather launch:

@@ -1589,14 +1589,17 @@ stark_status stark_dprove_rows(stark_dprove* h, uint8_t** rows_dev) {
   return STARK_OK;
 }
 
-stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uint64_t** l_dev) {
-  if (!h || !m_root || !l_dev) return STARK_ERR_BAD_ARG;
+// k from the main tree's root (prove.rs:274-283) on the device, then L at this rank's points; the root
+// is host memory (m_root) or device memory (d_m_root, no host round trip).
+static stark_status dprove_lincomb(stark_dprove* h, const uint8_t* m_root, const uint8_t* d_m_root, uint64_t** l_dev) {
   DProveState& d = h->st;
   const Mont mc = mont();
   STARK_HIP(d.ctx, hipSetDevice(d.ctx->device));
-  // k from m_root (prove.rs:274-283) on the device, then L at this rank's points.
-  uint32_t* d_root = d.d_tr->roots[1];
-  STARK_HIP(d.ctx, hipMemcpyAsync(d_root, m_root, 32, hipMemcpyHostToDevice, d.s));
+  const uint32_t* d_root = (const uint32_t*)d_m_root;
+  if (m_root) {
+    STARK_HIP(d.ctx, hipMemcpyAsync(d.d_tr->roots[1], m_root, 32, hipMemcpyHostToDevice, d.s));
+    d_root = d.d_tr->roots[1];
+  }
   XsPowers xs;
   for (int t = 0; t < 8; ++t) xs.v[t] = d.xs_m[t];
   hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs,
@@ -1612,9 +1615,19 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
   la.tr = d.d_tr;
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(d.P)), dim3(256), 0, d.s, la);
   STARK_HIP(d.ctx, hipGetLastError());
-  STARK_HIP(d.ctx, hipStreamSynchronize(d.s));  // m_root is the caller's (pageable) buffer
+  if (m_root) STARK_HIP(d.ctx, hipStreamSynchronize(d.s));  // m_root is the caller's (pageable) buffer
   *l_dev = (uint64_t*)d.lvals;
   return STARK_OK;
+}
+
+stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uint64_t** l_dev) {
+  if (!h || !m_root || !l_dev) return STARK_ERR_BAD_ARG;
+  return dprove_lincomb(h, m_root, nullptr, l_dev);
+}
+
+stark_status stark_dprove_lincomb_dev(stark_dprove* h, const uint8_t* d_m_root, uint64_t** l_dev) {
+  if (!h || !d_m_root || !l_dev || (((uintptr_t)d_m_root) & 3)) return STARK_ERR_BAD_ARG;
+  return dprove_lincomb(h, nullptr, d_m_root, l_dev);
 }
 
 void stark_dprove_free(stark_dprove* h) { delete h; }

@@ -130,6 +130,11 @@ _SIGNATURES = {
                                    ctypes.c_int),
     "stark_fri_fold_dev": ([_vp, _vp, _vp, ctypes.c_size_t, _u64p, _u8p, ctypes.c_uint32, ctypes.c_uint32, _vp],
                            ctypes.c_int),
+    "stark_fri_fold_dev_root": ([_vp, _vp, _vp, ctypes.c_size_t, _u64p, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp],
+                                ctypes.c_int),
+    "stark_merkle_root_dev": ([_vp, _vp, _vp], ctypes.c_int),
+    "stark_merkle_top_dev": ([_vp, _vp, ctypes.c_size_t, _vp, _vp], ctypes.c_int),
+    "stark_dprove_lincomb_dev": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_proof_json_from_parts": ([_u8p, _u8p, _u8p, _vp, _vp, _vp, ctypes.c_size_t, _u8p, ctypes.c_size_t,
                                           ctypes.c_char_p, ctypes.c_size_t, _szp], ctypes.c_int),
     "stark_dprove_begin": ([_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, ctypes.c_size_t, _u64p,

@@ -15,16 +15,23 @@ almost the whole proof local (csrc/r1cs.hip `dprove_begin`):
 Only the Merkle commitments mix classes.  DistTree hashes the local leaves,
 exchanges the 32-B leaf digests with one all-to-all (RCCL over xGMI with
 backend "nccl"), builds the rank's contiguous subtree, all-gathers the G
-subtree roots and hashes the top log2(G) levels: the reference's own
-subtree + top-tree split (merkle_proof_in_place.rs:106-206), so the root is
-the single tree's.  Small trees (fewer than G leaves per rank) are all-gathered
-and built whole on every rank.  Openings: a leaf comes from its class owner,
-the lower path from the subtree owner, the top path from the roots; one
-all_gather_object collects every opening of the proof, rank 0 renders the
-StarkProof JSON (utils.rs:122-130).
+subtree roots as one (G, 32) device tensor and hashes the top log2(G) levels on
+the device: the reference's own subtree + top-tree split
+(merkle_proof_in_place.rs:106-206), so the root is the single tree's.  Small
+trees (fewer than G leaves per rank) are all-gathered and built whole on every
+rank.
 
-The transcript (m_root -> k, l_root -> positions, FRI roots -> special_x, ys)
-is recomputed identically on every rank from the all-gathered roots.
+Nothing in the commit phase waits for the host: each root stays in HBM and
+feeds the next step on the stream (k and L from the main root, special_x and
+the fold from each FRI layer's root), and every collective is stream-ordered
+under RCCL.  The roots come down in ONE batched copy after the last FRI layer;
+the host then derives the transcript's indices (l_root -> positions, each
+root2 -> ys; the same transcript on every rank), every rank gathers the
+openings it holds in one zero-copy launch, and one tensor all-gather (sizes
+known on every rank from the layout) brings them to rank 0, which renders the
+StarkProof JSON (utils.rs:122-130).  Host-synchronising steps per proof: the
+begin call, the status reduction, the roots download, the opening gather and
+its collective (`stats["host_syncs"]`).
 
 `ops` abstracts the per-rank device work: GpuProverOps runs it in
 libstark_hip on this rank's GPU; tests/test_dprove_cpu.py runs the same
@@ -80,7 +87,8 @@ class DistTree:
         self.G = dist.get_world_size(group)
         self.r = dist.get_rank(group)
 
-    def commit(self, leaves, n_local: int, leaf_len: int) -> bytes:
+    def commit(self, leaves, n_local: int, leaf_len: int) -> None:
+        """Enqueues the commitment; the root is `d_root()` (device) until `set_host` brings the levels."""
         G = self.G
         self.leaves, self.n_local, self.leaf_len = leaves, n_local, leaf_len
         self.n = n_local * G
@@ -90,20 +98,30 @@ class DistTree:
             # Few leaves: every rank builds the whole tree from all the digests.
             self.blocked = False
             alld = _all_gather_tensor(dig, G, self.group).reshape(-1)
-            self.root = self.tree.build(alld, self.n, G)
-            self.top = []
-            return self.root
+            self.tree.build(alld, self.n, G)
+            self.d_levels = self.tree.root_tensor()
+            return
         self.blocked = True
         recv = torch.empty_like(dig)
         _exchange(recv, dig, self.group)          # chunk s of class r -> rank s; rank s gets G chunks
-        sub = self.tree.build(recv, n_local, G)   # leaves [r n_local, (r+1) n_local)
-        roots = _all_gather_object(sub, G, self.group)
-        self.top = [roots]
-        while len(self.top[-1]) > 1:
-            lv = self.top[-1]
-            self.top.append([blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)])
-        self.root = self.top[-1][0]
-        return self.root
+        self.tree.build(recv, n_local, G)         # leaves [r n_local, (r+1) n_local)
+        roots = _all_gather_tensor(self.tree.root_tensor(), G, self.group).reshape(-1)   # (G * 32,)
+        # subtree roots, then the G - 1 digests above them (the root last), all on the device
+        self.d_levels = torch.cat([roots, self.ops.merkle_top(roots, G)])
+
+    def d_root(self) -> torch.Tensor:
+        return self.d_levels[-32:]
+
+    def set_host(self, levels: bytes) -> None:
+        """The downloaded levels: self.root and (blocked) self.top, the subtree roots and the levels above."""
+        self.root = levels[-32:]
+        self.top = []
+        if self.blocked:
+            at, w = 0, self.G
+            while w >= 1:
+                self.top.append([levels[at + 32 * i:at + 32 * (i + 1)] for i in range(w)])
+                at += 32 * w
+                w //= 2
 
     def open_plan(self, idx: np.ndarray) -> list:
         """This rank's gathers for opening leaves idx: (rows request, path request).
@@ -117,13 +135,24 @@ class DistTree:
             path_local = idx if r == 0 else idx[:0]
         return [("rows", self.leaves, self.leaf_len, m, leaf_local), ("tree", self.tree, path_local)]
 
+    def _low(self) -> int:
+        depth = self.n.bit_length() - 1
+        return (self.n_local.bit_length() - 1) if self.blocked else depth
+
+    def blob_sizes(self, idx: np.ndarray, p: int) -> tuple:
+        """Bytes of rank p's (leaf blob, node blob) for opening idx (what its open_plan gathers)."""
+        G, m = self.G, self.n_local
+        leaves = int(np.count_nonzero(idx % G == p)) * self.leaf_len
+        paths = int(np.count_nonzero(idx // m == p)) if self.blocked else (len(idx) if p == 0 else 0)
+        return leaves, paths * self._low() * 32
+
     def assemble(self, idx: np.ndarray, parts: list) -> tuple:
         """(k x leaf_len leaves, k x depth x 32 nodes) from every rank's (leaf blob, node blob)."""
         G, m, k = self.G, self.n_local, len(idx)
         depth = self.n.bit_length() - 1
         leaves = np.empty((k, self.leaf_len), dtype=np.uint8)
         nodes = np.empty((k, depth, 32), dtype=np.uint8)
-        low = (m.bit_length() - 1) if self.blocked else depth
+        low = self._low()
         for p, (lb, nb) in enumerate(parts):
             sel = idx % G == p
             leaves[sel] = np.frombuffer(lb, dtype=np.uint8).reshape(-1, self.leaf_len)
@@ -175,22 +204,51 @@ def render_json(lib, m_root, l_root, a_root, main, lcomb, layers, last: bytes) -
 
 
 class _Phases:
-    """STARK_PROFILE=1: wall-clock of each phase on this rank (stderr)."""
+    """Per-phase time of one proof on this rank: host wall-clock at each mark and, on a GPU, a HIP event
+    on the proof's stream (the device time line, read after the proof's last synchronisation).
+    STARK_PROFILE=1 also prints the host marks (stderr).  host_syncs counts the steps that wait for
+    the device or for another rank."""
 
-    def __init__(self, rank: int):
+    def __init__(self, rank: int, device: bool):
         import os
         import time
         self.on = os.environ.get("STARK_PROFILE", "0") not in ("", "0")
-        self.rank, self.time = rank, time.perf_counter
+        self.rank, self.time, self.device = rank, time.perf_counter, device
         self.t0 = self.last = self.time()
+        self.marks = []   # (name, host seconds since the previous mark, device event or None)
+        self.ev0 = self._event()
+        self.host_syncs = 0
+
+    def _event(self):
+        if not self.device:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
 
     def mark(self, what: str):
+        now = self.time()
+        self.marks.append((what, now - self.last, self._event()))
         if self.on:
             import sys
-            now = self.time()
             print(f"[dprove r{self.rank}] {what}: {1e3 * (now - self.last):.3f} ms (total {1e3 * (now - self.t0):.3f})",
                   file=sys.stderr)
-            self.last = now
+        self.last = now
+
+    def sync(self, n: int = 1):
+        self.host_syncs += n
+
+    def report(self) -> dict:
+        """{phase: {"host_ms", "device_ms"}} (device_ms from the events, after everything completed)."""
+        out, prev = {}, self.ev0
+        for what, dt, ev in self.marks:
+            rec = {"host_ms": round(1e3 * dt, 3)}
+            if ev is not None and prev is not None:
+                ev.synchronize()
+                rec["device_ms"] = round(prev.elapsed_time(ev), 3)
+            out[what] = rec
+            prev = ev
+        return {"phases": out, "host_syncs": self.host_syncs, "total_ms": round(1e3 * (self.last - self.t0), 3)}
 
 
 # FRI layers of at most 2^FRI_TAIL_LOG values are not worth a collective each: their
@@ -200,73 +258,129 @@ FRI_TAIL_LOG = 16
 _EMPTY_LAST = '{"Last":{"last":[]}}]}'
 
 
-def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: int = FRI_TAIL_LOG, circuit=None):
+def _status_max(code: int, group=None, dev=None) -> int:
+    """The largest status code over the ranks (0 = every rank ok): one small all-reduce."""
+    t = torch.tensor([int(code)], dtype=torch.int64,
+                     device=dev if dev is not None and dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.cpu()[0])
+
+
+def _gather_to_rank0(blobs: list, sizes: list, G: int, r: int, group=None, dev=None):
+    """Rank 0 gets every rank's blobs (blobs[i] bytes, rank p's sizes in sizes[p][i], known on every
+    rank): one padded tensor all-gather (device memory under RCCL).  Returns [per rank [bytes...]] on
+    rank 0, None elsewhere."""
+    totals = [sum(sz) for sz in sizes]
+    width = max(max(totals), 1)
+    mine = np.zeros(width, dtype=np.uint8)
+    flat = b"".join(blobs)
+    assert len(flat) == totals[r], (len(flat), totals[r])
+    mine[:len(flat)] = np.frombuffer(flat, dtype=np.uint8)
+    t = torch.from_numpy(mine)
+    if dev is not None and dist.get_backend(group) == "nccl":
+        t = t.to(dev)
+    allt = _all_gather_tensor(t, G, group).cpu().numpy()   # (G, width)
+    if r != 0:
+        return None
+    out = []
+    for p in range(G):
+        row, at, parts = allt[p].tobytes(), 0, []
+        for n in sizes[p]:
+            parts.append(row[at:at + n])
+            at += n
+        out.append(parts)
+    return out
+
+
+def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: int = FRI_TAIL_LOG, circuit=None,
+                      stats: dict | None = None):
     """prove_with_witness (run.rs:310-452) over the G ranks of `group`.
     Every rank calls it; rank 0 returns the StarkProof JSON, the others None.
-    circuit: this rank's DistCircuit (the .r1cs-only work done once; r1cs is then unused)."""
+    circuit: this rank's DistCircuit (the .r1cs-only work done once; r1cs is then unused).
+    stats: filled (when given) with this rank's per-phase times and host-synchronising step count."""
     G = dist.get_world_size(group)
     r = dist.get_rank(group)
-    ph = _Phases(r)
+    dev = getattr(ops, "dev", None)
+    ph = _Phases(r, dev is not None and dev.type == "cuda")
     if G & (G - 1) or G > EXTENSION_FACTOR:
         raise ValueError(f"prove_distributed: world size must be a power of two <= 8 (got {G})")
     # A rank that fails must not leave the others blocked in a collective: every rank
     # reports its status first and all of them raise together.
     h, status, info = None, 0, None
     try:
-        h = ops.begin(r1cs, wtns, G, r, circuit)
+        h = ops.begin(r1cs, wtns, G, r, circuit)   # trace, LDE, constraints (ends with a stream sync)
         status, info = ops.info(h)
     except Exception as e:  # noqa: BLE001 - re-raised below on every rank
         status = getattr(e, "code", -1) or -1
+        if status < 0:
+            status = 1 << 20
+    ph.sync(2)   # begin ends with a stream synchronisation; info reads the transcript back
     try:
-        codes = _all_gather_object(status, G, group)
-        if any(codes):
-            ops.raise_status(next(c for c in codes if c), "prove_distributed")
+        worst = _status_max(status, group, dev)
+        ph.sync()
+        if worst:
+            ops.raise_status(worst, "prove_distributed")
         prec, n_local, os_, g2, a_root = info
-        ph.mark("trace + LDE + constraints (begin)")
+        ph.mark("begin: trace + LDE + constraints")
         skips = EXTENSION_FACTOR
-        log_prec = prec.bit_length() - 1
-        # Main tree over the 256-B rows (prove.rs:235-264) -> k -> L (prove.rs:274-322) -> L tree.
+        # Main tree over the 256-B rows (prove.rs:235-264) -> k -> L (prove.rs:274-322) -> L tree, each
+        # root consumed on the device.
         main = DistTree(ops, group)
-        m_root = main.commit(ops.rows(h), n_local, 256)
+        main.commit(ops.rows(h), n_local, 256)
         ph.mark("main tree")
-        lvals = ops.lincomb(h, m_root, _k_values(m_root))
+        lvals = ops.lincomb(h, main.d_root())
         ltree = DistTree(ops, group)
-        l_root = ltree.commit(lvals, n_local, 32)
+        ltree.commit(lvals, n_local, 32)
         ph.mark("L + L tree")
-        # prove_low_degree(L, g2, precision/4, skips) (prove.rs:367, fri.rs:46-224), layer by layer.
+        # prove_low_degree(L, g2, precision/4, skips) (prove.rs:367, fri.rs:46-224), layer by layer; the
+        # fold's special_x comes from the previous tree's root on the device.
         layers = []
-        vals, n, w, deg, mtree, mroot = lvals, prec, g2, prec // 4, ltree, l_root
+        vals, n, w, deg, mtree = lvals, prec, g2, prec // 4, ltree
         while deg > 16 and n > (1 << fri_tail_log):
             q = n // 4
-            col = ops.fold(vals, n, w, mroot, G, r)
+            col = ops.fold(vals, n, w, mtree.d_root(), G, r)
             t2 = DistTree(ops, group)
-            root2 = t2.commit(col, q // G, 32)
-            ys = get_pseudorandom_indices(root2, q, 40, skips)              # fri.rs:181-189
-            poly_idx = [y + q * j for y in ys for j in range(4)]           # fri.rs:193-204
-            layers.append((root2, t2, ys, mtree, poly_idx, (q.bit_length() - 1)))
-            vals, n, w, deg, mtree, mroot = col, q, pow(w, 4, P), deg // 4, t2, root2
-        last_local = ops.to_host(vals, n // G)
-        ph.mark(f"FRI ({len(layers)} layers)")
-        # Spot checks (prove.rs:337-362).
+            t2.commit(col, q // G, 32)
+            layers.append((t2, mtree, q))
+            vals, n, w, deg, mtree = col, q, pow(w, 4, P), deg // 4, t2
+        ph.mark(f"FRI folds + trees ({len(layers)} layers)")
+        # Every root and top level, and this rank's share of the last layer, in one download.
+        trees = [main, ltree] + [t2 for t2, _, _ in layers]
+        host = ops.to_host_many([t.d_levels for t in trees] + [(vals, n // G * 32)])
+        ph.sync()
+        for t, b in zip(trees, host):
+            t.set_host(b)
+        last_local = host[-1]
+        m_root, l_root = main.root, ltree.root
+        # Spot checks (prove.rs:337-362) and the FRI openings (fri.rs:181-205), from the roots.
         positions = get_pseudorandom_indices(l_root, prec, SPOT_CHECK_SECURITY_FACTOR, skips)
         aug = []
         for j in positions:
             aug += [j, (j + prec - skips) % prec, (j + os_ // 3 * skips) % prec, (j + os_ // 3 * 2 * skips) % prec]
         reqs = [(main, aug), (ltree, positions)]
-        for (_, t2, ys, mt, poly_idx, _) in layers:
-            reqs += [(t2, ys), (mt, poly_idx)]
+        for (t2, mt, q) in layers:
+            ys = get_pseudorandom_indices(t2.root, q, 40, skips)             # fri.rs:181-189
+            reqs += [(t2, ys), (mt, [y + q * j for y in ys for j in range(4)])]   # fri.rs:193-204
         reqs = [(t, np.asarray(idx, dtype=np.uint64)) for t, idx in reqs]
+        ph.mark("roots download + transcript")
         plan = [g for t, idx in reqs for g in t.open_plan(idx)]
         got = ops.open_batch(plan)        # one gather launch for every opening held here
-        mine = [(got[2 * i][0], got[2 * i + 1][1]) for i in range(len(reqs))]
-        allparts = _all_gather_object((mine, last_local), G, group)
-        ph.mark("openings")
+        ph.sync(2)   # the stream (trees built) and the gather's own completion
+        blobs = []
+        for i in range(len(reqs)):
+            blobs += [got[2 * i][0], got[2 * i + 1][1]]
+        blobs.append(last_local)
+        sizes = [[x for t, idx in reqs for x in t.blob_sizes(idx, p)] + [len(last_local)] for p in range(G)]
+        allparts = _gather_to_rank0(blobs, sizes, G, r, group, dev)
+        ph.sync()
+        ph.mark("openings gathered")
         if r != 0:
             return None
-        opened = [t.assemble(idx, [p[0][i] for p in allparts]) for i, (t, idx) in enumerate(reqs)]
-        chunks = np.stack([np.frombuffer(p[1], dtype=np.uint8).reshape(-1, 32) for p in allparts], axis=1)
+        opened = [t.assemble(idx, [(allparts[p][2 * i], allparts[p][2 * i + 1]) for p in range(G)])
+                  for i, (t, idx) in enumerate(reqs)]
+        chunks = np.stack([np.frombuffer(allparts[p][-1], dtype=np.uint8).reshape(-1, 32) for p in range(G)], axis=1)
         values = chunks.reshape(-1, 32).tobytes()   # value r + G j is rank r's j-th
-        fri_parts = [(root2, opened[2 + 2 * li], opened[3 + 2 * li]) for li, (root2, *_rest) in enumerate(layers)]
+        fri_parts = [(t2.root, opened[2 + 2 * li], opened[3 + 2 * li]) for li, (t2, _, _) in enumerate(layers)]
         if deg <= 16:
             js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, values)
         else:
@@ -276,9 +390,11 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
             js = render_json(ops.lib, m_root, l_root, a_root, opened[0], opened[1], fri_parts, b"")
             assert js.endswith(_EMPTY_LAST) and tail.startswith("[") and tail.endswith("]")
             js = js[:-len(_EMPTY_LAST)] + tail[1:] + "}"
-        ph.mark("assembly + JSON")
+        ph.mark("assembly + JSON (rank 0)")
         return js
     finally:
+        if stats is not None:
+            stats.update(ph.report())
         if h is not None:
             ops.end(h)
 
@@ -363,11 +479,41 @@ class GpuProverOps:
         self.ctx.check(self.lib.stark_dprove_rows(h, ctypes.byref(p)), "dprove_rows")
         return p.value
 
-    def lincomb(self, h, m_root: bytes, k: list) -> int:
+    def lincomb(self, h, d_m_root: torch.Tensor) -> int:
+        """k from the main tree's root (in HBM) and L at this rank's points, asynchronously."""
         from . import _vp
         p = _vp()
-        self.ctx.check(self.lib.stark_dprove_lincomb(h, m_root, ctypes.byref(p)), "dprove_lincomb")
+        self.ctx.check(self.lib.stark_dprove_lincomb_dev(h, d_m_root.data_ptr(), ctypes.byref(p)), "dprove_lincomb")
         return p.value
+
+    def merkle_top(self, roots: torch.Tensor, G: int) -> torch.Tensor:
+        """The G - 1 digests above G subtree roots (device), level by level, the root last."""
+        out = torch.empty((G - 1) * 32, dtype=torch.uint8, device=self.dev)
+        self.ctx.check(self.lib.stark_merkle_top_dev(self.ctx.h, roots.data_ptr(), G, out.data_ptr(), self._stream()),
+                       "merkle_top")
+        return out
+
+    def to_host_many(self, items: list) -> list:
+        """Bytes of each item (a uint8 tensor, or (buffer, nbytes)) in one device-to-host copy."""
+        parts = []
+        for it in items:
+            if isinstance(it, tuple):
+                buf, nb = it
+                if not isinstance(buf, torch.Tensor):   # a raw device pointer (no FRI layer ran)
+                    parts.append(self.to_host(buf, nb // 32))
+                    continue
+                it = buf.reshape(-1)[:nb]
+            parts.append(it.reshape(-1))
+        dev = [x for x in parts if isinstance(x, torch.Tensor)]
+        flat = torch.cat(dev).cpu().numpy().tobytes() if dev else b""
+        out, at = [], 0
+        for x in parts:
+            if isinstance(x, torch.Tensor):
+                out.append(flat[at:at + x.numel()])
+                at += x.numel()
+            else:
+                out.append(x)
+        return out
 
     def leaf_digests(self, leaves, n: int, leaf_len: int) -> torch.Tensor:
         out = torch.empty(n * 32, dtype=torch.uint8, device=self.dev)
@@ -409,12 +555,13 @@ class GpuProverOps:
         v = np.frombuffer(values, dtype=np.uint64).reshape(-1, 4)
         return self.ctx.prove_low_degree(v, root, max_deg_plus_1, excl).to_json()
 
-    def fold(self, vals, n: int, root: int, m_root: bytes, G: int, r: int) -> torch.Tensor:
+    def fold(self, vals, n: int, root: int, d_m_root: torch.Tensor, G: int, r: int) -> torch.Tensor:
+        """The layer's fold with special_x from its Merkle root in HBM (no host round trip)."""
         from . import _limbs, _p64
         col = torch.empty(n // 4 // G * 32, dtype=torch.uint8, device=self.dev)
         rl = _limbs(root)
-        self.ctx.check(self.lib.stark_fri_fold_dev(self.ctx.h, self._ptr(vals), col.data_ptr(), n, _p64(rl), m_root,
-                                                   G, r, self._stream()), "fri_fold")
+        self.ctx.check(self.lib.stark_fri_fold_dev_root(self.ctx.h, self._ptr(vals), col.data_ptr(), n, _p64(rl),
+                                                        d_m_root.data_ptr(), G, r, self._stream()), "fri_fold")
         return col
 
     def to_host(self, buf, count: int) -> bytes:
@@ -430,8 +577,13 @@ class _GpuTree:
         self.ops = ops
         self.t = MerkleProofInPlace(ops.ctx)
 
-    def build(self, digests: torch.Tensor, n: int, interleave: int) -> bytes:
+    def build(self, digests: torch.Tensor, n: int, interleave: int) -> None:
+        self.keep = digests       # read by the build's kernels on the stream
         self.t.update_digests_dev(digests.data_ptr(), n, interleave, stream=self.ops._stream())
-        torch.cuda.current_stream().synchronize()
-        self.t.gen_proofs([])      # sets the root (MerkleProofInPlace::get_root semantics)
-        return self.t.get_root()
+
+    def root_tensor(self) -> torch.Tensor:
+        """The root digest copied into a (32,) device tensor on the stream."""
+        out = torch.empty(32, dtype=torch.uint8, device=self.ops.dev)
+        self.ops.ctx.check(self.ops.lib.stark_merkle_root_dev(self.t.h, out.data_ptr(), self.ops._stream()),
+                           "merkle_root_dev")
+        return out

@@ -25,18 +25,25 @@ def _u8(b: bytes) -> torch.Tensor:
     return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy())
 
 
+def _levels(lv: list) -> list:
+    out = [lv]
+    while len(lv) > 1:
+        lv = [O.py_blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)]
+        out.append(lv)
+    return out
+
+
 class _PyTree:
     """Blake2s tree over given leaf digests (interleaved residue-class chunks)."""
 
-    def build(self, digests: torch.Tensor, n: int, interleave: int) -> bytes:
+    def build(self, digests: torch.Tensor, n: int, interleave: int) -> None:
         raw = bytes(digests.numpy())
         chunk = n // interleave
-        lv = [raw[32 * (r * chunk + m):32 * (r * chunk + m + 1)] for m in range(chunk) for r in range(interleave)]
-        self.levels = [lv]
-        while len(lv) > 1:
-            lv = [O.py_blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)]
-            self.levels.append(lv)
-        return lv[0]
+        self.levels = _levels([raw[32 * (r * chunk + m):32 * (r * chunk + m + 1)]
+                               for m in range(chunk) for r in range(interleave)])
+
+    def root_tensor(self) -> torch.Tensor:
+        return _u8(self.levels[-1][0])
 
     def open(self, idx) -> list:
         out = []
@@ -80,8 +87,10 @@ class OracleProverOps:
     def rows(self, h):
         return h["rows"]
 
-    def lincomb(self, h, m_root, k):
-        """L = k0 D1 + ... + k10 S at this rank's points (prove.rs:287-322)."""
+    def lincomb(self, h, m_root_t):
+        """L = k0 D1 + ... + k10 S at this rank's points (prove.rs:287-322), k from m_root (prove.rs:274-283)."""
+        from stark_amd.dprove import _k_values
+        k = _k_values(bytes(m_root_t.numpy()))
         G, r, prec, rows = h["G"], h["r"], h["prec"], h["rows"]
         steps = prec // 8
         g2s = pow(h["g2"], steps, P)
@@ -101,6 +110,21 @@ class OracleProverOps:
     def new_tree(self):
         return _PyTree()
 
+    def merkle_top(self, roots_t, G):
+        raw = bytes(roots_t.numpy())
+        lv = _levels([raw[32 * i:32 * (i + 1)] for i in range(G)])
+        return _u8(b"".join(b"".join(x) for x in lv[1:]))
+
+    def to_host_many(self, items):
+        out = []
+        for it in items:
+            if isinstance(it, tuple):
+                buf, nb = it
+                out.append(bytes(buf.numpy()[:nb]) if isinstance(buf, torch.Tensor) else bytes(buf[:nb]))
+            else:
+                out.append(bytes(it.numpy()))
+        return out
+
     def open_batch(self, plan):
         out = []
         for g in plan:
@@ -112,9 +136,9 @@ class OracleProverOps:
                 out.append((b"", b"".join(b"".join(nodes) for nodes in tree.open([int(i) for i in idx]))))
         return out
 
-    def fold(self, vals, n, root, m_root, G, r):
+    def fold(self, vals, n, root, m_root_t, G, r):
         """Column rows r + G j: the cubic through (w^(i + t n/4), v[i + t n/4]) at special_x (fri.rs:135-164)."""
-        sx = int.from_bytes(m_root, "little") % P
+        sx = int.from_bytes(bytes(m_root_t.numpy()), "little") % P
         q = n // 4
         ql = q // G
         v = [int.from_bytes(vals[32 * i:32 * (i + 1)], "little") for i in range(n // G)]

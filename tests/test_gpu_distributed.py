@@ -243,3 +243,57 @@ def test_rccl_world1_pipelined_and_merkle():
     assert np.array_equal(res["cyclic"], o.best_fft(ins[0], w, log_n, cpus=8))
     root, _ = o.merkle(ins[1].tobytes(), 1 << log_n, 32)
     assert res["merkle_root"] == root
+
+
+@pytest.mark.parametrize("g", [1, 2, 8, 64])
+def test_merkle_top_and_root_dev(ctx, oracle, g):
+    """stark_merkle_root_dev + stark_merkle_top_dev (the distributed commit's device-side top tree,
+    merkle_proof_in_place.rs:176-180) against the single tree's root and the host Blake2s."""
+    import stark_amd as S
+    m = 16
+    leaves = O.random_elements(g * m, 0x5EED0500 + g).tobytes()
+    want_root, _ = oracle.merkle(leaves, g * m, 32)
+    roots = torch.empty(g * 32, dtype=torch.uint8, device="cuda")
+    trees = []
+    for c in range(g):
+        t = S.MerkleProofInPlace(ctx)
+        blob = torch.from_numpy(np.frombuffer(leaves[c * m * 32:(c + 1) * m * 32], dtype=np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        t.update_dev(blob.data_ptr(), m, 32, stream=ctx.stream)
+        ctx.check(ctx.lib.stark_merkle_root_dev(t.h, roots[32 * c:].data_ptr(), ctx.stream), "root_dev")
+        trees.append((t, blob))
+    levels = torch.zeros(max(g - 1, 1) * 32, dtype=torch.uint8, device="cuda")
+    ctx.check(ctx.lib.stark_merkle_top_dev(ctx.h, roots.data_ptr(), g, levels.data_ptr(), ctx.stream), "top_dev")
+    ctx.synchronize()
+    got = (levels if g > 1 else roots).cpu().numpy().tobytes()[-32:]
+    assert got == want_root
+    # every level equals pairwise host hashing of the level below
+    lv = [roots.cpu().numpy().tobytes()[32 * i:32 * (i + 1)] for i in range(g)]
+    flat, at = levels.cpu().numpy().tobytes(), 0
+    while len(lv) > 1:
+        lv = [O.py_blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)]
+        assert flat[at:at + 32 * len(lv)] == b"".join(lv)
+        at += 32 * len(lv)
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (4, 3)])
+def test_fri_fold_dev_root_equals_host_root(ctx, world, rank):
+    """stark_fri_fold_dev_root (special_x from a device-resident root, fri.rs:135) = stark_fri_fold_dev
+    (the same root from the host), including a root >= p (reduced mod p)."""
+    from stark_amd import _limbs, _p64
+    log_n = 12
+    n = 1 << log_n
+    w = O.root_of_unity(log_n)
+    vals = torch.from_numpy(O.random_elements(n // world, 0x5EED0600 + world).view(np.int64).copy()).cuda()
+    for root in (bytes(range(32)), b"\xff" * 32):
+        d_root = torch.from_numpy(np.frombuffer(root, dtype=np.uint8).copy()).cuda()
+        a = torch.empty(n // 4 // world * 32, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        torch.cuda.synchronize()
+        rl = _limbs(w)
+        ctx.check(ctx.lib.stark_fri_fold_dev(ctx.h, vals.data_ptr(), a.data_ptr(), n, _p64(rl), root, world, rank,
+                                             ctx.stream), "fold")
+        ctx.check(ctx.lib.stark_fri_fold_dev_root(ctx.h, vals.data_ptr(), b.data_ptr(), n, _p64(rl), d_root.data_ptr(),
+                                                  world, rank, ctx.stream), "fold_root")
+        ctx.synchronize()
+        assert torch.equal(a, b)
