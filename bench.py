@@ -903,8 +903,24 @@ def main():
                           "(oracle C restatement)",
                 "gpu_json_bitexact": bool(sha256(cpu_fri) == fri_json_sha)}
             del cpu_fri
-            # End-to-end: the oracle's restatement of mk_r1cs_proof on pedersen_test.
+            # Config 2's pair on the CPU: best_fft then inv_best_fft of the 2^20 input (fft.rs:327-379).
+            t3 = time.perf_counter()
+            f20c = o.best_fft(h20, w20, 20, cpus=threads)
+            b20c = o.inv_best_fft(f20c, w20, 20, cpus=threads)
+            t20 = time.perf_counter() - t3
+            legs["ntt_2^20_fwd_inv"] = {
+                "value": round(t20 * 1000.0, 1), "unit": "ms", "cores": threads, "threads": threads, "kind": "port",
+                "sample": "best_fft + inv_best_fft of the bench's 2^20 input (oracle C restatement of parallel_fft)",
+                "roundtrip_exact": bool(np.array_equal(b20c, h20))}
+            del f20c, b20c
+            # End-to-end: the oracle's restatement of mk_r1cs_proof on compute (config 1) and pedersen_test.
             import r1cs as R
+            trc = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "compute"))
+            t3 = time.perf_counter()
+            R.mk_r1cs_proof_json(o, trc, cpus=threads)
+            legs["prove_compute"] = {"value": round((time.perf_counter() - t3) * 1000.0, 2), "unit": "ms",
+                                     "cores": threads, "threads": threads, "kind": "port",
+                                     "sample": "one mk_r1cs_proof of compute (oracle C restatement)"}
             tr = R.build_trace(*R.load_fixture(os.path.join(ROOT, "tests", "golden", "r1cs"), "pedersen_test"))
             t3 = time.perf_counter()
             R.mk_r1cs_proof_json(o, tr, cpus=threads)

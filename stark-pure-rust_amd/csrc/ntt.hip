@@ -68,11 +68,6 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3, kColSpar
 // tiles measured slower (one or two workgroups per CU leave the barriers uncovered).
 constexpr uint32_t kTileLog = 10;
 constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
-// L2 prefetch of the tile the next round of workgroups on this XCD takes (tile + kCUs x occupancy: the
-// dispatcher deals workgroup k to XCD k mod 8, and kCUs x occupancy is a multiple of 8), one dword
-// load per 128-B run, issued behind the tile's own loads.
-constexpr bool kPrefetch = false;
-constexpr uint32_t kCUs = 256;  // MI355X
 
 // Which radix-4 steps multiply by the digit-basis product (fe_db.h), radices 2^4..2^8:
 //   * every step before the pass's last one: constants w_R^(4k), k < R/8 (32 for R = 256, 9 KB of
@@ -171,18 +166,6 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
-  }
-  uint32_t pf = 0;
-  if (kPrefetch && COL != kColSparse && B == 4 && tid < R) {
-    const uint32_t nt = tile + kCUs * DB::occupancy;
-    if (nt < total_tiles) {
-      const fe* nsrc = in + ((size_t)(nt >> log_tiles) << log_in) + ((size_t)(nt & tile_mask) << log_b);
-      pf = *reinterpret_cast<const uint32_t*>(nsrc + ((size_t)tid << log_cols));  // row tid's 128-B run
-      if (COL == kColFull) {
-        const size_t j1 = ((size_t)(nt & tile_mask) << log_b) & ns_mask;
-        pf += *reinterpret_cast<const uint32_t*>(ct.full + (j1 << LOG_R) + 4 * tid);  // its 32-KB table slice
-      }
-    }
   }
 
   // Stage the pass's LDS tables once the tile's loads are in flight, every staging load before any
@@ -589,7 +572,6 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         if (do_scale) val = fe_mul(val, scale);
         fe_store(dst + o, val);
       }
-      if (kPrefetch) asm volatile("" ::"v"(pf));  // keeps the prefetch load (its value is never needed)
     } else {
       // Ns < B: the tile's output is the contiguous run [j0 R, (j0 + B) R).
 #pragma unroll

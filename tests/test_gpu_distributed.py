@@ -227,6 +227,17 @@ def _worker_rccl_world1(rank, world, port, out_q):
     leaves = torch.from_numpy(ins[1].view(np.int64).copy()).cuda()
     res["merkle_root"] = DistributedMerkle(ops).commit(leaves, n, 32)
     torch.cuda.synchronize()
+    # prove_distributed over RCCL: the status all-reduce, the device-tensor all-gathers of the tree
+    # digests and of the openings, the device roots (k, special_x) -- at world 1
+    import hashlib
+    from stark_amd.dprove import GpuProverOps, prove_distributed
+    fix = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "r1cs")
+    r1 = open(os.path.join(fix, "pedersen_test.r1cs"), "rb").read()
+    wt = open(os.path.join(fix, "pedersen_test.wtns"), "rb").read()
+    st = {}
+    js = prove_distributed(GpuProverOps(ctx), r1, wt, stats=st)
+    res["pedersen_sha"] = hashlib.sha256(js.encode()).hexdigest()
+    res["host_syncs"] = st["host_syncs"]
     out_q.put(res)
     ctx.close()
     dist.destroy_process_group()
@@ -243,6 +254,10 @@ def test_rccl_world1_pipelined_and_merkle():
     assert np.array_equal(res["cyclic"], o.best_fft(ins[0], w, log_n, cpus=8))
     root, _ = o.merkle(ins[1].tobytes(), 1 << log_n, 32)
     assert res["merkle_root"] == root
+    import json
+    golden = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "r1cs_proofs.json")))
+    assert res["pedersen_sha"] == golden["pedersen_test"]["json_sha256"]
+    assert res["host_syncs"] <= 7
 
 
 @pytest.mark.parametrize("g", [1, 2, 8, 64])
