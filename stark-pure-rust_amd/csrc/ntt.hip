@@ -632,6 +632,16 @@ inline uint32_t max_log_r(uint32_t log_n) { return (log_n == 25 || log_n >= 27) 
 // which the cached full last-pass twiddle table depends on.)
 PassPlan plan_passes(uint32_t log_n) {
   PassPlan p;
+  if (log_n == 20) {
+    // 2^20 (config 2): the two radix-2^8 passes run 16 x 16 (ntt.hip DbPlan::four), the radix-4 pass
+    // is short; 0.104-0.105 vs 0.107-0.108 ms for (6, 7, 7), and the 2^17 -> 2^20 LDE 0.768-0.777 vs
+    // 0.786-0.790 ms (profiles/r04_plan_2_20_22_ab.txt).  (8, 8, 4) measured the same, (8, 6, 6) slower.
+    p.n_pass = 3;
+    p.log_r[0] = 8;
+    p.log_r[1] = 4;
+    p.log_r[2] = 8;
+    return p;
+  }
   const uint32_t cap = max_log_r(log_n);
   p.n_pass = (int)((log_n + cap - 1) / cap);
   const uint32_t base = log_n / p.n_pass, extra = log_n % p.n_pass;

@@ -50,10 +50,10 @@ def test_lincomb(ctx, n_cols, n):
 
 # (13, 3), (12, 4), (10, 6), (8, 8): a radix-2^8 first pass (the 16 x 16 split) skipping 2, 4, 6 and all 8
 # copy stages of the zero-padded input
-# (12, 2), (9, 5), (19, 2): radix-2^7 sparse first passes (plans (7, 7) and (7, 7, 7), the 8 x 16
+# (17, 3): the 2^20 plan (8, 4, 8); (12, 2), (9, 5), (19, 2): radix-2^7 sparse first passes (plans (7, 7) and (7, 7, 7), the 8 x 16
 # kColSparse instance) that skip 1 and 5 copy stages
 @pytest.mark.parametrize("log_steps,log_blowup", [(4, 3), (7, 3), (13, 3), (15, 3), (10, 1), (4, 8), (12, 6),
-                                                  (12, 4), (10, 6), (8, 8), (12, 2), (9, 5), (19, 2)])
+                                                  (12, 4), (10, 6), (8, 8), (12, 2), (9, 5), (19, 2), (17, 3)])
 def test_lde(ctx, oracle, log_steps, log_blowup):
     log_prec = log_steps + log_blowup
     g2 = O.root_of_unity(log_prec)
