@@ -306,6 +306,15 @@ stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, 
  * the cross-rank DFT of the one-exchange distributed NTT. */
 stark_status stark_ntt_strided_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, size_t stride,
                                    const uint64_t root[4], int inverse, void* stream);
+/* The one-exchange distributed NTT's first step on rank `rank` of G = 2^log_g (stark_amd/distributed.py
+ * cyclic_ntt; no reference counterpart: the reference's only parallelism is parallel_fft's threads,
+ * fft.rs:195-251): the rank's cyclic shard of M = 2^(log_n - log_g) points (x[rank + G j]) is
+ * transformed in place with root w^G, w = root of order 2^log_n, and output k is multiplied by
+ * w^(rank k) in the same last pass (w^-1, and the 1/M scale, with inverse != 0).  What the all-to-all
+ * then sends; stark_ntt_strided_dev finishes the transform on the receiving rank.  The twiddle table
+ * (M x 32 B per rank and direction) is cached under the context's cap.  Asynchronous on `stream`. */
+stark_status stark_cyclic_ntt_local_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t log_g,
+                                        uint32_t rank, const uint64_t root[4], int inverse, void* stream);
 /* The same, after first scaling d[i + stride*j] by tw_root^(j*(tw_base + i))
  * (tw_root a primitive 2^log_order-th root): the receiver-side twiddle of the
  * one-exchange distributed NTT, fused into its cross-rank DFT. */

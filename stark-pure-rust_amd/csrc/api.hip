@@ -45,6 +45,7 @@ size_t cache_bytes(const stark_ctx* ctx) {
     if (kv.second->d_full_s) b += full;
   }
   for (const auto& kv : ctx->ext_idx) b += kv.second.bytes;
+  for (const auto& kv : ctx->post_tw) b += kv.second.bytes;
   return b;
 }
 
@@ -78,7 +79,15 @@ bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext) {
           ext_it = it;
           full_slot = nullptr;
         }
-    if (!full_slot && ext_it == ctx->ext_idx.end()) return false;
+    auto post_it = ctx->post_tw.end();  // (only read inside a launch: always a candidate)
+    for (auto it = ctx->post_tw.begin(); it != ctx->post_tw.end(); ++it)
+      if (it->second.used < oldest) {
+        oldest = it->second.used;
+        post_it = it;
+        full_slot = nullptr;
+        ext_it = ctx->ext_idx.end();
+      }
+    if (!full_slot && ext_it == ctx->ext_idx.end() && post_it == ctx->post_tw.end()) return false;
     if (!synced) {
       hipDeviceSynchronize();
       synced = true;
@@ -87,6 +96,10 @@ bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext) {
       hipFree(*full_slot);
       *full_slot = nullptr;
       have -= full_bytes;
+    } else if (post_it != ctx->post_tw.end()) {
+      hipFree(post_it->second.ptr);
+      have -= post_it->second.bytes;
+      ctx->post_tw.erase(post_it);
     } else {
       hipFree(ext_it->second.ptr);
       have -= ext_it->second.bytes;
@@ -304,6 +317,8 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (void* p : ctx->pinned)
     if (p) hipHostFree(p);
   for (auto& kv : ctx->ext_idx)
+    if (kv.second.ptr) hipFree(kv.second.ptr);
+  for (auto& kv : ctx->post_tw)
     if (kv.second.ptr) hipFree(kv.second.ptr);
   if (ctx->staged) hipEventDestroy(ctx->staged);
   ctx->fri_trees.clear();

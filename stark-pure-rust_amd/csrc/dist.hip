@@ -2,6 +2,7 @@
 // a tiled transpose of 32-B field elements and the four-step twiddle
 // data[i][j] *= w^((row_base + i) * (col_base + j)).  The exchange steps are
 // RCCL all-to-alls issued by the caller (torch.distributed, backend "nccl").
+#include "fe_db.h"
 #include "internal.h"
 
 namespace stark {
@@ -40,6 +41,16 @@ __global__ void twiddle2d_kernel(fe* __restrict__ data, uint64_t rows, uint64_t 
   fe_store(data + idx, fe_mul(fe_load(data + idx), t));
 }
 
+// post[k] = w^(rank k mod n), k < m (Montgomery images of the two-level tables' product): the
+// one-exchange distributed NTT's twiddle, multiplied into the rank's local transform's last store.
+__global__ void post_tw_kernel(fe* __restrict__ out, uint64_t m, uint64_t rank, uint32_t log_n,
+                               const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  const uint64_t e = (rank * k) & (((uint64_t)1 << log_n) - 1);
+  fe_store(out + k, fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]));
+}
+
 // Small DFTs across a stride: for each i < stride, the G = 2^LOG_G points
 // d[i + stride j], j < G, are replaced by their DFT (root w_G), in place:
 //   out[i + stride k] = sum_j d[i + stride j] w_G^(j k)   [* G^-1 when scaling].
@@ -61,9 +72,13 @@ struct StridedTw {
   uint64_t base, mask;  // exponent (base + i) & mask, mask = order - 1
 };
 
+// db != nullptr: the DFT's constants w_G^k (k < G/2) as digit-basis tables (fe_db.h, 72 words each):
+// uniform across the grid, so the product takes them from SGPRs (140 VALU instead of a Montgomery
+// product's ~300); the result is reduced to canonical for the full-reduction butterflies.
 template <int LOG_G, bool TW>
 __global__ __launch_bounds__(256) void strided_ntt_kernel(fe* __restrict__ d, uint64_t stride, SmallRoots rt,
-                                                          fe scale, int do_scale, StridedTw tw) {
+                                                          fe scale, int do_scale, StridedTw tw,
+                                                          const uint32_t* __restrict__ db) {
   constexpr int G = 1 << LOG_G;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= stride) return;
@@ -96,7 +111,14 @@ __global__ __launch_bounds__(256) void strided_ntt_kernel(fe* __restrict__ d, ui
 #pragma unroll
       for (int jj = 0; jj < m; ++jj) {
         fe t = x[k + jj + m];
-        if (jj) t = fe_mul(t, rt.w[jj << (LOG_G - 1 - s)]);  // w_{2m}^jj
+        if (jj) {  // w_{2m}^jj
+          if (db) {
+            t = fe_mul_db(t, db + 72u * (jj << (LOG_G - 1 - s)));
+            fe_reduce_once(t);
+          } else {
+            t = fe_mul(t, rt.w[jj << (LOG_G - 1 - s)]);
+          }
+        }
         const fe u = x[k + jj];
         x[k + jj] = fe_add(u, t);
         x[k + jj + m] = fe_sub(u, t);
@@ -151,6 +173,16 @@ static stark_status strided(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, si
     tw = StridedTw{t->d_lo, t->d_hi, t->kb, tw_base, ((uint64_t)1 << log_order) - 1};
   }
   const fe scale = to_dev(F.inv(F.from_u64((uint64_t)1 << log_g)));
+  // the DFT's constants as digit-basis tables (the tables of the root w (or w^-1) of order G)
+  const uint32_t* db = nullptr;
+  {
+    uint64_t wc[4];
+    F.to_canonical(w, wc);
+    const Twiddles* tg = nullptr;
+    const stark_status st = get_twiddles(ctx, wc, log_g, &tg);
+    if (st != STARK_OK) return st;
+    db = tg->d_db + tg->db_off[log_g];
+  }
   const unsigned grid = (unsigned)((stride + 255) / 256);
   hipStream_t s = pick_stream(ctx, stream);
   fe* d = (fe*)d_data;
@@ -159,9 +191,11 @@ static stark_status strided(stark_ctx* ctx, uint64_t* d_data, uint32_t log_g, si
 #define STARK_STRIDED(LG)                                                                                      \
   do {                                                                                                        \
     if (tw_root)                                                                                              \
-      hipLaunchKernelGGL((strided_ntt_kernel<LG, true>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw);  \
+      hipLaunchKernelGGL((strided_ntt_kernel<LG, true>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw,   \
+                         db);                                                                                 \
     else                                                                                                      \
-      hipLaunchKernelGGL((strided_ntt_kernel<LG, false>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw); \
+      hipLaunchKernelGGL((strided_ntt_kernel<LG, false>), dim3(grid), dim3(256), 0, s, d, st, rt, scale, sc, tw,  \
+                         db);                                                                                 \
   } while (0)
   switch (log_g) {
     case 1: STARK_STRIDED(1); break;
@@ -184,6 +218,54 @@ stark_status stark_ntt_strided_tw_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t
                                       uint32_t log_order, uint64_t tw_base, void* stream) {
   if (!tw_root) return STARK_ERR_BAD_ARG;
   return strided(ctx, d_data, log_g, stride, root, inverse, tw_root, log_order, tw_base, stream);
+}
+
+stark_status stark_cyclic_ntt_local_dev(stark_ctx* ctx, uint64_t* d_data, uint32_t log_n, uint32_t log_g,
+                                       uint32_t rank, const uint64_t root[4], int inverse, void* stream) {
+  if (!ctx || !d_data || !root) return STARK_ERR_BAD_ARG;
+  // M = 2^(log_n - log_g) >= 4 points per rank, and G | M (the exchange's chunks)
+  if (log_n > 28 || log_g > 4 || log_n < log_g + 2 || log_n < 2 * log_g || rank >= (1u << log_g))
+    return STARK_ERR_BAD_LENGTH;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
+  const FieldHost& F = FieldHost::get();
+  const uint32_t log_m = log_n - log_g;
+  HostFp w = F.from_canonical(root);
+  {  // a primitive 2^log_n-th root: w^(n/2) = -1
+    const HostFp half = F.pow_u64(w, (uint64_t)1 << (log_n - 1));
+    if (!FieldHost::eq(F.add(half, F.one()), F.zero())) return STARK_ERR_BAD_ROOT;
+  }
+  if (inverse) w = F.inv(w);
+  // the local M-point transform's root w^G (its inverse tables for the inverse direction)
+  uint64_t wl[4];
+  F.to_canonical(F.pow_u64(w, (uint64_t)1 << log_g), wl);
+  const Twiddles* tl = nullptr;
+  STARK_TRY(get_twiddles(ctx, wl, log_m, &tl));
+  // post[k] = w^(rank k), k < M (cached per root, size and rank, in the capped table cache)
+  uint64_t wc[4];
+  F.to_canonical(w, wc);
+  const auto key = std::make_tuple(wc[0], wc[1], wc[2], wc[3], log_n, rank);
+  hipStream_t s = pick_stream(ctx, stream);
+  const fe* post = nullptr;
+  auto it = ctx->post_tw.find(key);
+  if (it != ctx->post_tw.end()) {
+    it->second.used = ++ctx->cache_clock;
+    post = (const fe*)it->second.ptr;
+  } else {
+    const Twiddles* tn = nullptr;
+    STARK_TRY(get_twiddles(ctx, wc, log_n, &tn));
+    const uint64_t M = (uint64_t)1 << log_m;
+    void* p = nullptr;
+    if (!cache_reserve(ctx, M * sizeof(fe), false) || hipMalloc(&p, M * sizeof(fe)) != hipSuccess) {
+      hipGetLastError();
+      return STARK_ERR_OOM;
+    }
+    hipLaunchKernelGGL(post_tw_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (fe*)p, M, (uint64_t)rank,
+                       log_n, tn->d_lo, tn->d_hi, tn->kb);
+    STARK_HIP(ctx, hipGetLastError());
+    ctx->post_tw[key] = CacheBuf{p, M * sizeof(fe), ++ctx->cache_clock};
+    post = (const fe*)p;
+  }
+  return ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, post);
 }
 
 stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, size_t cols, uint64_t row_base,

@@ -128,6 +128,9 @@ struct stark_ctx {
   // (prove.rs:160-163) at that rank's points: it depends on the trace length only, so every
   // proof of that size shares it (r1cs.hip ext_index_column).
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, stark::CacheBuf> ext_idx;
+  // (root canonical limbs, log_n, rank) -> post[k] = root^(rank k), k < n / world: the one-exchange
+  // distributed NTT's twiddle, applied in the rank's last local pass (dist.hip).
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t, uint32_t>, stark::CacheBuf> post_tw;
   // Cached tables (full twiddle tables + ext_idx) stay under cache_limit bytes: least recently used
   // ones are freed first (stark::cache_reserve).  stark_ctx_set_cache_limit changes it.
   size_t cache_limit = stark::kDefaultCacheLimit;
@@ -141,6 +144,12 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
   do {                                                        \
     hipError_t e_ = (call);                                   \
     if (e_ != hipSuccess) return ::stark::hip_fail(ctx, e_, #call); \
+  } while (0)
+
+#define STARK_TRY(expr)              \
+  do {                               \
+    stark_status st_ = (expr);       \
+    if (st_ != STARK_OK) return st_; \
   } while (0)
 
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
@@ -171,14 +180,17 @@ hipStream_t pick_stream(stark_ctx* ctx, void* stream);
 stark_status get_twiddles(stark_ctx* ctx, const uint64_t root[4], uint32_t log_n, const Twiddles** out);
 
 // Device NTT over `batch` contiguous transforms (in place, canonical values).
+// post != nullptr: output k of each transform is multiplied by post[k] (Montgomery images, n entries)
+// in the last pass's store (the one-exchange distributed NTT's twiddle, dist.hip).
 stark_status ntt_device(stark_ctx* ctx, fe* d_data, uint32_t log_n, uint32_t batch, const Twiddles& tw,
-                        bool inverse, hipStream_t stream);
+                        bool inverse, hipStream_t stream, const fe* post = nullptr);
 // Forward/inverse transform of src's batch columns of 2^(log_n - zero_log)
 // elements, zero-extended to 2^log_n, into d_data (zero_log <= the plan's
 // first radix); the zero tail is neither stored nor read.
 uint32_t ntt_first_log_r(uint32_t log_n);  // log2 of the first pass's radix
 stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
-                             uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream);
+                             uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream,
+                             const fe* post = nullptr);
 
 // First pass of a transform whose input is zero beyond its first n >> zero_log elements (best_fft's
 // zero padding): skip = the number of leading radix-2 stages that are plain copies (<= zero_log,

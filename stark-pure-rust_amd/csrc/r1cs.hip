@@ -653,11 +653,6 @@ struct Carve {
   }
 };
 
-#define STARK_TRY(expr)                 \
-  do {                                  \
-    stark_status st_ = (expr);          \
-    if (st_ != STARK_OK) return st_;    \
-  } while (0)
 
 static unsigned blocks_for(uint64_t n, unsigned t = 256) { return (unsigned)((n + t - 1) / t); }
 

@@ -133,6 +133,8 @@ _SIGNATURES = {
     "stark_fri_fold_dev_root": ([_vp, _vp, _vp, ctypes.c_size_t, _u64p, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp],
                                 ctypes.c_int),
     "stark_merkle_root_dev": ([_vp, _vp, _vp], ctypes.c_int),
+    "stark_cyclic_ntt_local_dev": ([_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u64p, ctypes.c_int,
+                                    _vp], ctypes.c_int),
     "stark_merkle_top_dev": ([_vp, _vp, ctypes.c_size_t, _vp, _vp], ctypes.c_int),
     "stark_dprove_lincomb_dev": ([_vp, _vp, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_r1cs_proof_json_from_parts": ([_u8p, _u8p, _u8p, _vp, _vp, _vp, ctypes.c_size_t, _u8p, ctypes.c_size_t,
@@ -288,6 +290,14 @@ class Context:
         r = _limbs(root)
         self.check(self.lib.stark_ntt_strided_dev(self.h, d_ptr, log_g, stride, _p64(r), 1 if inverse else 0,
                                                   stream or None), "ntt_strided")
+
+    def cyclic_ntt_local_dev(self, d_ptr: int, log_n: int, log_g: int, rank: int, root, inverse: bool = False,
+                             stream: int = 0) -> None:
+        """The rank's local M-point NTT of the one-exchange distributed NTT with its twiddle w^(rank k)
+        applied in the last pass (stark_cyclic_ntt_local_dev)."""
+        r = _limbs(root)
+        self.check(self.lib.stark_cyclic_ntt_local_dev(self.h, d_ptr, log_n, log_g, rank, _p64(r), 1 if inverse else 0,
+                                                       stream or None), "cyclic_ntt_local")
 
     def ntt_strided_tw_dev(self, d_ptr: int, log_g: int, stride: int, root, tw_root, log_order: int, tw_base: int,
                            inverse: bool = False, stream: int = 0) -> None:

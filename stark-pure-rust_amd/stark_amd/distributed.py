@@ -127,6 +127,10 @@ def cyclic_ntt_local(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool 
         ops.ntt(y, log_n, 1, w, inverse)
         return y
     log_m = M.bit_length() - 1
+    if hasattr(ops, "cyclic_local"):
+        # M-point NTT (root w^G) with the twiddle w^(+-r k2) in its last pass's store (one HBM pass)
+        ops.cyclic_local(y, log_n, G.bit_length() - 1, dist.get_rank(group), w, inverse)
+        return y
     ops.ntt(y, log_m, 1, pow(w, G, P), inverse)                     # M-point, root w^G
     if not hasattr(ops, "ntt_strided_tw"):
         ops.twiddle2d(y, 1, M, dist.get_rank(group), 0, pow(w, P - 2, P) if inverse else w, log_n)
@@ -144,9 +148,9 @@ def cyclic_ntt_finish(z: torch.Tensor, log_n: int, root: int, ops, inverse: bool
     c = M // G
     w = root % P
     log_g = G.bit_length() - 1
-    if hasattr(ops, "ntt_strided_tw"):
+    if hasattr(ops, "ntt_strided_tw") and not hasattr(ops, "cyclic_local"):
         ops.ntt_strided_tw(z, log_g, c, pow(w, M, P), inverse, pow(w, P - 2, P) if inverse else w, log_n, r * c)
-    else:
+    else:  # the twiddle was applied before the exchange (cyclic_ntt_local)
         ops.ntt_strided(z, log_g, c, pow(w, M, P), inverse)
 
 
@@ -185,6 +189,10 @@ class GpuOps:
 
     def ntt_strided(self, t: torch.Tensor, log_g: int, stride: int, root: int, inverse: bool) -> None:
         self.ctx.ntt_strided_dev(t.data_ptr(), log_g, stride, root, inverse=inverse, stream=self._stream())
+
+    def cyclic_local(self, t: torch.Tensor, log_n: int, log_g: int, rank: int, root: int, inverse: bool) -> None:
+        """The local M-point NTT with its twiddle fused into the last pass (stark_cyclic_ntt_local_dev)."""
+        self.ctx.cyclic_ntt_local_dev(t.data_ptr(), log_n, log_g, rank, root, inverse=inverse, stream=self._stream())
 
     def ntt_strided_tw(self, t: torch.Tensor, log_g: int, stride: int, root: int, inverse: bool, tw_root: int,
                        log_order: int, tw_base: int) -> None:

@@ -312,3 +312,29 @@ def test_fri_fold_dev_root_equals_host_root(ctx, world, rank):
                                                   world, rank, ctx.stream), "fold_root")
         ctx.synchronize()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("log_n,log_g,rank,inverse", [(15, 3, 5, False), (15, 3, 7, True), (12, 1, 1, False),
+                                                     (20, 2, 2, True), (8, 4, 9, False)])
+def test_cyclic_ntt_local_fused_twiddle(ctx, oracle, log_n, log_g, rank, inverse):
+    """stark_cyclic_ntt_local_dev = the rank's M-point best_fft (root w^G) followed by the twiddle
+    w^(rank k) (w^-1 and inv_best_fft for the inverse): the one-exchange distributed NTT's first step
+    with the twiddle in the last pass's store."""
+    G = 1 << log_g
+    M = 1 << (log_n - log_g)
+    w = O.root_of_unity(log_n)
+    x = O.random_elements(M, 0x5EED0700 + log_n + rank)
+    d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+    torch.cuda.synchronize()
+    ctx.cyclic_ntt_local_dev(d.data_ptr(), log_n, log_g, rank, w, inverse=inverse, stream=ctx.stream)
+    ctx.synchronize()
+    got = O.from_limbs(d.cpu().numpy().view(np.uint64).reshape(-1, 4))
+    wl = pow(w, G, O.P)
+    base = oracle.inv_best_fft(x, wl, log_n - log_g, cpus=8) if inverse else oracle.best_fft(x, wl, log_n - log_g, cpus=8)
+    wt = pow(w, O.P - 2, O.P) if inverse else w
+    step = pow(wt, rank, O.P)
+    want, t = [], 1
+    for v in O.from_limbs(base):
+        want.append(v * t % O.P)
+        t = t * step % O.P
+    assert got == want
