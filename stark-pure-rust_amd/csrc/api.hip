@@ -321,6 +321,8 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   for (auto& kv : ctx->post_tw)
     if (kv.second.ptr) hipFree(kv.second.ptr);
   if (ctx->staged) hipEventDestroy(ctx->staged);
+  if (ctx->ev_aux) hipEventDestroy(ctx->ev_aux);
+  if (ctx->aux) hipStreamDestroy(ctx->aux);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp})

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <iterator>
 #include <array>
 #include <string>
 
@@ -352,9 +353,22 @@ static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, s
   fns.clear();
 }
 
+static void prepend_done(std::vector<std::string>& done, std::vector<std::string>& out) {
+  if (done.empty()) return;
+  out.insert(out.begin(), std::make_move_iterator(done.begin()), std::make_move_iterator(done.end()));
+  done.clear();
+}
+
+void JsonPieces::prerender() {
+  std::vector<std::string> out;
+  render_pieces(fns, out);
+  for (std::string& x : out) done.push_back(std::move(x));
+}
+
 void JsonPieces::render(std::string& o) {
   std::vector<std::string> out;
   render_pieces(fns, out);
+  prepend_done(done, out);
   size_t total = o.size();
   for (const std::string& x : out) total += x.size();
   o.reserve(total);
@@ -364,6 +378,7 @@ void JsonPieces::render(std::string& o) {
 void JsonPieces::render(JsonText& o) {
   std::vector<std::string> out;
   render_pieces(fns, out);
+  prepend_done(done, out);
   std::vector<size_t> off(out.size() + 1, 0);
   for (size_t i = 0; i < out.size(); ++i) off[i + 1] = off[i] + out[i].size();
   o.n = off.back();

@@ -122,6 +122,10 @@ struct stark_ctx {
   void* pinned[4] = {nullptr, nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
   size_t pinned_bytes[4] = {0, 0, 0, 0};
   hipEvent_t staged = nullptr;  // the last DMA out of pinned slot 3 (r1cs_trace_dev.hip staged_upload)
+  // A second stream and an event for work the host overlaps with the main stream (the prover's spot-check
+  // openings gathered while its FRI layers still run, r1cs.hip); created on first use.
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_aux = nullptr;
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
   // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
@@ -231,12 +235,14 @@ struct JsonText {
 // concatenated in order (fri.hip).
 struct JsonPieces {
   std::vector<std::function<void(std::string&)>> fns;
+  std::vector<std::string> done;  // pieces already rendered (prerender), in order before fns
   void text(const std::string& s);
   void bytes(const uint8_t* p, size_t n);  // p must outlive render()
   void branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes, size_t k,
                 size_t depth);
   void render(std::string& o);
   void render(JsonText& o);  // pieces rendered and copied to their offsets on the host workers
+  void prerender();          // renders the pieces added so far now (e.g. while the GPU still works)
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
 

@@ -1007,19 +1007,25 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s));
   hipLaunchKernelGGL(r1cs_l_root_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(l_tree), d_tr);
   STARK_HIP(ctx, hipGetLastError());
-  // Roots and the constraint flags come back with the FRI prover's synchronisation.
+  // The roots and the constraint flags come down behind the L tree; an event marks them.
   Transcript* h_tr = nullptr;
   STARK_TRY(ctx_pinned(ctx, 1, sizeof(Transcript) + 1024, (void**)&h_tr));
   STARK_HIP(ctx, hipMemcpyAsync(h_tr, d_tr, sizeof(Transcript), hipMemcpyDeviceToHost, s));
+  if (!ctx->ev_aux) STARK_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_aux, hipEventDisableTiming));
+  if (!ctx->aux) STARK_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, s));
 
   // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367), enqueued behind the rest.
   FriPendingPtr fri_pending;
   clk.mark("prover kernels enqueued");
   STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending, l_tree));
   clk.mark("FRI kernels enqueued");
-  STARK_HIP(ctx, hipStreamSynchronize(s));  // the proof's one wait for the device
-  clk.mark("device wait");
+  // While the FRI layers run: the roots, the spot checks (prove.rs:337-362), their openings (gathered on
+  // the second stream) and the StarkProof JSON up to fri_proof.
+  STARK_HIP(ctx, hipEventSynchronize(ctx->ev_aux));
+  clk.mark("wait for the L root");
   if (h_tr->err) {
+    hipStreamSynchronize(s);  // (the enqueued FRI work finishes before the proof is dropped)
     ctx->last_error = (h_tr->err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
                                       : "invalid B: boundary value mismatch (utils.rs:477-524)";
     return STARK_ERR_CHECK;
@@ -1027,8 +1033,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   memcpy(proof->a_root, h_tr->roots[0], 32);
   memcpy(proof->m_root, h_tr->roots[1], 32);
   memcpy(proof->l_root, h_tr->roots[2], 32);
-
-  // Spot checks (prove.rs:337-362); their openings join the FRI openings in one gather batch.
   uint32_t pos32[kSpotChecks];
   STARK_TRY(stark_get_pseudorandom_indices(proof->l_root, 32, (uint32_t)prec, kSpotChecks, (uint32_t)skips, pos32));
   std::vector<size_t> positions(kSpotChecks), aug(4 * kSpotChecks);
@@ -1042,14 +1046,13 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   std::vector<uint8_t> l_leaves(32 * kSpotChecks), l_nodes(32 * kSpotChecks * log_prec);
   std::vector<uint8_t> m_leaves(256 * 4 * kSpotChecks), m_nodes(32 * 4 * kSpotChecks * log_prec);
-  std::vector<GatherReq> extra = {{l_tree, positions.data(), (size_t)kSpotChecks, l_leaves.data(), l_nodes.data()},
-                                  {m_tree, aug.data(), (size_t)4 * kSpotChecks, m_leaves.data(), m_nodes.data()}};
-  stark_fri_proof* fri = nullptr;
-  STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
-  clk.mark("indices + gather batch");
-  proof->fri = fri;  // owned by the proof from here on
-  // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string).
-  JsonText& o = proof->json;
+  {
+    // the trees are complete (behind the event); the gather runs beside the FRI kernels
+    std::vector<GatherReq> spot = {{l_tree, positions.data(), (size_t)kSpotChecks, l_leaves.data(), l_nodes.data()},
+                                   {m_tree, aug.data(), (size_t)4 * kSpotChecks, m_leaves.data(), m_nodes.data()}};
+    STARK_TRY(merkle_gather_batch(ctx, spot, ctx->aux));
+  }
+  // StarkProof JSON (utils.rs:122-130; run.rs:549 serde_json::to_string), its head rendered now.
   JsonPieces j;
   j.text("{\"m_root\":");
   j.bytes(proof->m_root, 32);
@@ -1062,9 +1065,18 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   j.text(",\"linear_comb_branches\":");
   j.branches(l_leaves, 32, l_nodes, kSpotChecks, log_prec);
   j.text(",\"fri_proof\":");
+  j.prerender();
+  clk.mark("spot checks + their JSON (beside FRI)");
+  STARK_HIP(ctx, hipStreamSynchronize(s));  // the FRI layers
+  clk.mark("device wait");
+  std::vector<GatherReq> extra;
+  stark_fri_proof* fri = nullptr;
+  STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
+  clk.mark("FRI indices + gather");
+  proof->fri = fri;  // owned by the proof from here on
   fri_proof_json_pieces(fri, j);
   j.text("}");
-  j.render(o);
+  j.render(proof->json);
   clk.mark("proof JSON");
   proof->depth = log_prec;
   proof->m_leaves = std::move(m_leaves);
