@@ -69,13 +69,6 @@ enum : int { kColNone = 0, kColFull = 1, kColT16 = 2, kColTwoLevel = 3, kColSpar
 // tiles measured slower (one or two workgroups per CU leave the barriers uncovered).
 constexpr uint32_t kTileLog = 10;
 constexpr uint32_t kPassThreads = (1u << kTileLog) / 4;
-// Persistent radix-2^8 passes: kPersistWGs workgroups per CU each loop over tiles (stride = grid), stage
-// the LDS tables once, and load the next tile's elements into registers right after the current
-// tile's scatter (2 waves per SIMD: 256 VGPRs leave room for them), so a tile's load latency hides
-// behind the previous tile's arithmetic.
-constexpr bool kPersist = false;
-constexpr uint32_t kPersistWGs = 2;
-constexpr uint32_t kCUs = 256;  // MI355X
 
 // Which radix-4 steps multiply by the digit-basis product (fe_db.h), radices 2^4..2^8:
 //   * every step before the pass's last one: constants w_R^(4k), k < R/8 (32 for R = 256, 9 KB of
@@ -130,13 +123,12 @@ struct XImage {
   }
 };
 
-template <int LOG_R, int COL, bool PERSIST = false>
-__global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(
+template <int LOG_R, int COL>
+__global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void ntt_pass_kernel(
     const fe* __restrict__ in, fe* __restrict__ out, uint32_t log_n, uint32_t log_ns, uint32_t log_b, ColTw ct,
-    const fe* __restrict__ small, const uint32_t* __restrict__ db_arg, fe scale, int do_scale, uint32_t log_tiles,
+    const fe* __restrict__ small, const uint32_t* __restrict__ db, fe scale, int do_scale, uint32_t log_tiles,
     uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
-  const uint32_t* db = db_arg;
   using DB = DbPlan<LOG_R, COL>;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
   fe* sm = lds;          // R/2 small roots w_R^k as Shoup pairs: sm[2k] = w_R^k, sm[2k + 1] = its quotient
@@ -145,24 +137,24 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
   const uint32_t B = 1u << log_b;
   const XImage XI{X, B << LOG_R};
   const uint32_t nthr = (B << LOG_R) >> 2;  // active threads
-  const uint32_t tid0 = threadIdx.x;
-  const bool active = tid0 < nthr;
+  const uint32_t tid = threadIdx.x;
+  const bool active = tid < nthr;
   const uint32_t log_cols = log_n - LOG_R;
   const size_t ns_mask = ((size_t)1 << log_ns) - 1;
   const uint32_t tile_mask = (1u << log_tiles) - 1;
-  uint32_t tile = blockIdx.x;
+  const uint32_t tile = blockIdx.x;
   if (tile >= total_tiles) return;  // (uniform per workgroup)
 
   // This thread's 4 elements of a tile: (eb[t], er[t]) = (column, row) as stored and loaded.
   uint32_t eb[4], er[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const uint32_t e = tid0 + (uint32_t)t * nthr;
+    const uint32_t e = tid + (uint32_t)t * nthr;
     eb[t] = e & (B - 1);
     er[t] = e >> log_b;
   }
-  const uint32_t b0 = tid0 & (B - 1);
-  const uint32_t q0 = tid0 >> log_b;  // radix-4 group within the column
+  const uint32_t b = tid & (B - 1);
+  const uint32_t q = tid >> log_b;  // radix-4 group within the column
 
   // Sparse first pass (sp.skip > 0): only rows < R >> sp.zero_log are
   // non-zero (read from a compact input of batch stride 2^sp.log_in), and the
@@ -170,22 +162,11 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
   const uint32_t live_rows = R >> sp.skip, nz_rows = R >> sp.zero_log;
   const uint32_t log_in = sp.zero_log ? sp.log_in : log_n;
   fe v[4];
-  auto load_tile = [&](uint32_t tl) {
-    const fe* src = in + ((size_t)(tl >> log_tiles) << log_in) + ((size_t)(tl & tile_mask) << log_b);
+  if (active) {
+    const fe* src = in + ((size_t)(tile >> log_tiles) << log_in) + ((size_t)(tile & tile_mask) << log_b);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       v[t] = er[t] < nz_rows ? fe_load(src + eb[t] + ((size_t)er[t] << log_cols)) : fe_zero();
-  };
-  // kColFull: the tile's full-table column twiddles, loaded with its elements (and prefetched with them)
-  fe twf[4];
-  auto load_tw = [&](uint32_t tl) {
-    const size_t jt = (size_t)(tl & tile_mask) << log_b;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) twf[t] = ct.full[(((jt + eb[t]) & ns_mask) << LOG_R) + er[t]];
-  };
-  if (active) {
-    load_tile(tile);
-    if (COL == kColFull) load_tw(tile);
   }
 
   // Stage the pass's LDS tables once the tile's loads are in flight, every staging load before any
@@ -201,35 +182,27 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
     auto db_dst = [&](uint32_t k) { return k + ((k / 18) >> 3); };
     if (blockDim.x == kPassThreads) {
       constexpr uint32_t nSm = (kSm + kPassThreads - 1) / kPassThreads, nDb = (kDb + kPassThreads - 1) / kPassThreads;
-      // (full rounds need no bounds test: tid0 < kPassThreads here)
-      auto in_sm = [&](uint32_t i) { return (i + 1) * kPassThreads <= kSm || tid0 + i * kPassThreads < kSm; };
-      auto in_db = [&](uint32_t i) { return (i + 1) * kPassThreads <= kDb || tid0 + i * kPassThreads < kDb; };
+      // (full rounds need no bounds test: tid < kPassThreads here)
+      auto in_sm = [&](uint32_t i) { return (i + 1) * kPassThreads <= kSm || tid + i * kPassThreads < kSm; };
+      auto in_db = [&](uint32_t i) { return (i + 1) * kPassThreads <= kDb || tid + i * kPassThreads < kDb; };
       uint4 ts[nSm ? nSm : 1], td[nDb ? nDb : 1];
 #pragma unroll
       for (uint32_t i = 0; i < nSm; ++i)
-        if (in_sm(i)) ts[i] = small4[tid0 + i * kPassThreads];
+        if (in_sm(i)) ts[i] = small4[tid + i * kPassThreads];
 #pragma unroll
       for (uint32_t i = 0; i < nDb; ++i)
-        if (in_db(i)) td[i] = db4[db_src(tid0 + i * kPassThreads)];
+        if (in_db(i)) td[i] = db4[db_src(tid + i * kPassThreads)];
 #pragma unroll
       for (uint32_t i = 0; i < nSm; ++i)
-        if (in_sm(i)) sm4[tid0 + i * kPassThreads] = ts[i];
+        if (in_sm(i)) sm4[tid + i * kPassThreads] = ts[i];
 #pragma unroll
       for (uint32_t i = 0; i < nDb; ++i)
-        if (in_db(i)) sdb4[db_dst(tid0 + i * kPassThreads)] = td[i];
+        if (in_db(i)) sdb4[db_dst(tid + i * kPassThreads)] = td[i];
     } else {
-      for (uint32_t k = tid0; k < kSm; k += blockDim.x) sm4[k] = small4[k];
-      for (uint32_t k = tid0; k < kDb; k += blockDim.x) sdb4[db_dst(k)] = db4[db_src(k)];
+      for (uint32_t k = tid; k < kSm; k += blockDim.x) sm4[k] = small4[k];
+      for (uint32_t k = tid; k < kDb; k += blockDim.x) sdb4[db_dst(k)] = db4[db_src(k)];
     }
   }
-  for (;;) {  // one tile per iteration (one iteration unless PERSIST)
-  // The wave-uniform digit-basis constants are reloaded (scalar loads) every tile: the opaque pointer keeps
-  // the compiler from hoisting their 72-SGPR tables out of the loop, which spills them into VGPRs.
-  if (PERSIST) asm volatile("" : "+s"(db));
-  // Likewise the thread's place in the tile: opaque per tile, so the per-lane table reads that depend on
-  // it (the twiddles' Shoup pairs) are not hoisted out of the loop into 64 live VGPRs.
-  uint32_t b = b0, q = q0, tid = tid0;
-  if (PERSIST) asm volatile("" : "+v"(b), "+v"(q), "+v"(tid));
   const size_t boff = (size_t)(tile >> log_tiles) << log_n;
   const size_t j0 = (size_t)(tile & tile_mask) << log_b;
 
@@ -238,11 +211,13 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
     if (COL != kColNone && COL != kColSparse) {
       const uint32_t lnr = log_ns + LOG_R;  // w_{Ns R} powers
       fe tw[4];
-      if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table (twf)
+      if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
+#pragma unroll
+        for (int t = 0; t < 4; ++t) tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
         // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
         // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
-        mul2(v[0], v[1], v[0], twf[0], v[1], twf[1]);
-        mul2(v[2], v[3], v[2], twf[2], v[3], twf[3]);
+        mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
+        mul2(v[2], v[3], v[2], tw[2], v[3], tw[3]);
       } else if (COL == kColT16) {
         // Shoup pairs from the L2-resident t16 table: v < 2^256 -> [0, 2p)
         const fe* e[4];
@@ -291,11 +266,6 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
       for (int t = 0; t < 4; ++t) {
         const uint32_t rr = __builtin_bitreverse32(er[t]) >> (32 - LOG_R);
         XI.st((rr << log_b) + eb[t], v[t]);
-      }
-      // The registers are free again: the next tile's loads, in flight through this tile's arithmetic.
-      if (PERSIST && tile + gridDim.x < total_tiles) {
-        load_tile(tile + gridDim.x);
-        if (COL == kColFull) load_tw(tile + gridDim.x);
       }
     } else {
       // Rows >= live_rows are zero, so after sp.skip DIT stages every
@@ -625,11 +595,6 @@ __global__ __launch_bounds__(kPassThreads, (PERSIST ? kPersistWGs : DbPlan<LOG_R
       }
     }
   }
-  if (!PERSIST) break;
-  tile += gridDim.x;
-  if (tile >= total_tiles) break;  // (uniform per workgroup)
-  __syncthreads();  // the next scatter rewrites the image this tile's last step read
-  }
 }
 
 // dst[c][i] = i < 2^log_m ? src[c][i] : 0 (best_fft's zero padding, fft.rs:327-357).
@@ -751,13 +716,12 @@ size_t db_lds_fe(uint32_t log_r, int col) {
 
 template <int LOG_R>
 pass_fn pass_kernel_r(int col) {
-  constexpr bool P = kPersist && LOG_R == 8;
   switch (col) {
-    case kColNone: return ntt_pass_kernel<LOG_R, kColNone, P>;
+    case kColNone: return ntt_pass_kernel<LOG_R, kColNone>;
     case kColSparse: return ntt_pass_kernel<LOG_R, kColSparse>;
-    case kColFull: return ntt_pass_kernel<LOG_R, kColFull, P>;
-    case kColT16: return ntt_pass_kernel<LOG_R, kColT16, P>;
-    default: return ntt_pass_kernel<LOG_R, kColTwoLevel, P>;
+    case kColFull: return ntt_pass_kernel<LOG_R, kColFull>;
+    case kColT16: return ntt_pass_kernel<LOG_R, kColT16>;
+    default: return ntt_pass_kernel<LOG_R, kColTwoLevel>;
   }
 }
 
@@ -1025,9 +989,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
     const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
     const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
-    const bool persist = kPersist && lr == 8 && col != kColSparse && threads == kPassThreads;
-    const uint64_t grid = persist ? std::min<uint64_t>(total, (uint64_t)kCUs * kPersistWGs) : total;
-    hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)grid), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
+    hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)total), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
                        tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
                        (inverse && last && !fold) ? 1 : 0, log_tiles,
                        (uint32_t)total, sp);

@@ -111,6 +111,15 @@ def cyclic_ntt(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = Fals
     return z
 
 
+def _fused_twiddle(ops, G: int) -> bool:
+    """Where the twiddle w^(r k2) goes: into the sender's last local pass (one product per element,
+    stark_cyclic_ntt_local_dev) from G = 8 on; below that the receiver's strided DFT applies it as a
+    chain of (G-1)/G products per element more cheaply.  One GPU, 2^24 per rank
+    (profiles/r04_distributed_local_step.txt): G = 2 1.685 vs 1.764 ms, G = 4 1.753 vs 1.779, G = 8
+    1.816 vs 1.792 (receiver vs sender)."""
+    return hasattr(ops, "cyclic_local") and G >= 8
+
+
 def cyclic_ntt_local(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool = False, group=None,
                      in_place: bool = False) -> torch.Tensor:
     """cyclic_ntt's first step: this rank's M-point NTT (root w^G), plus the twiddle w^(+-r k2) when
@@ -127,8 +136,8 @@ def cyclic_ntt_local(x: torch.Tensor, log_n: int, root: int, ops, inverse: bool 
         ops.ntt(y, log_n, 1, w, inverse)
         return y
     log_m = M.bit_length() - 1
-    if hasattr(ops, "cyclic_local"):
-        # M-point NTT (root w^G) with the twiddle w^(+-r k2) in its last pass's store (one HBM pass)
+    if _fused_twiddle(ops, G):
+        # M-point NTT (root w^G) with the twiddle w^(+-r k2) in its last pass's store
         ops.cyclic_local(y, log_n, G.bit_length() - 1, dist.get_rank(group), w, inverse)
         return y
     ops.ntt(y, log_m, 1, pow(w, G, P), inverse)                     # M-point, root w^G
@@ -148,7 +157,7 @@ def cyclic_ntt_finish(z: torch.Tensor, log_n: int, root: int, ops, inverse: bool
     c = M // G
     w = root % P
     log_g = G.bit_length() - 1
-    if hasattr(ops, "ntt_strided_tw") and not hasattr(ops, "cyclic_local"):
+    if hasattr(ops, "ntt_strided_tw") and not _fused_twiddle(ops, G):
         ops.ntt_strided_tw(z, log_g, c, pow(w, M, P), inverse, pow(w, P - 2, P) if inverse else w, log_n, r * c)
     else:  # the twiddle was applied before the exchange (cyclic_ntt_local)
         ops.ntt_strided(z, log_g, c, pow(w, M, P), inverse)
