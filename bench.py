@@ -46,8 +46,8 @@ SIMDS = 1024
 SHOUP_PRODUCT_PEAK = 138.71e9
 DB_PRODUCT_PEAK = 199.98e9
 LOG_N = 24
-PROFILE = os.path.join(ROOT, "profiles", "r03_summary.json")
-PMC = os.path.join(ROOT, "profiles", "r03_pmc_ntt.json")
+PROFILE = os.path.join(ROOT, "profiles", "r04_summary.json")
+PMC = os.path.join(ROOT, "profiles", "r04_pmc_ntt.json")
 LARGE = os.path.join(ROOT, "tests", "golden", "large_digests.json")
 
 
@@ -397,7 +397,7 @@ def distributed_prove(ctx, world, rank, on_gloo, local):
     return out
 
 
-MERKLE_SQ = os.path.join(ROOT, "profiles", "r03_pmc_merkle32.json")
+MERKLE_SQ = os.path.join(ROOT, "profiles", "r04_pmc_merkle32.json")
 CPU_PROVE_2_20 = os.path.join(ROOT, "profiles", "r04_cpu_prove_synth_2_20.json")
 
 
@@ -790,7 +790,7 @@ def main():
     # from the committed profile of this exact command line (tools/profile_round.sh), VALU issue from the
     # committed counter passes over 2^24 transforms alone (tools/pmc_round.sh ... ntt).
     traffic = prof_avg = prof_med = None
-    knames, sq = [], {}
+    knames, sq, timed = [], {}, None
     try:
         prof = json.load(open(PROFILE))
         knames = sorted(k for k in prof["kernels"] if "ntt_pass_kernel" in k)
@@ -800,6 +800,7 @@ def main():
             traffic = sum(prof["pmc_bytes_per_launch"][k]["hbm_bytes"] for k in knames)
             prof_avg = sum(prof["kernels"][k]["avg_ns"] for k in knames) / 1e6
             prof_med = sum(prof["kernels"][k]["steady_median_ns"] for k in knames) / 1e6
+            timed = prof.get("timed_region")
     except (OSError, KeyError, ValueError):
         pass
     try:
@@ -816,6 +817,9 @@ def main():
                 "rocprof_ms_per_transform_avg": round(prof_avg, 4) if prof_avg else None,
                 "rocprof_ms_per_transform_steady_median": round(prof_med, 4) if prof_med else None,
                 "rocprof_kernels": knames, "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
+    if timed:  # the profiled run's kernels over its own timed steps vs that run's ms_per_step
+        roofline["rocprof_timed_region_ms_per_transform"] = round(timed["kernel_ms_per_transform"], 4)
+        roofline["rocprof_run_ms_per_step"] = round(timed["bench_ms_per_step_same_run"], 4)
     modmuls, db_muls = ntt_products(log_n, plan)
     # The transform's products at the standalone rates of their two forms (the rest of the pass, the
     # butterflies, LDS traffic and the Montgomery full-table column twiddle, priced at nothing).

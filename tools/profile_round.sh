@@ -19,5 +19,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $B --steps 5 --warmup 1 > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $B --steps 5 --warmup 1 > "$OUT/bench_write.log" 2>&1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/full" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline > "$OUT/bench_full.log" 2>&1
-python3 "$ROOT/tools/profile_summary.py" "$OUT/stats" "$OUT/fetch" "$OUT/write" "$OUT/summary.json" > /dev/null
+python3 "$ROOT/tools/profile_summary.py" "$OUT/stats" "$OUT/fetch" "$OUT/write" "$OUT/summary.json" "$OUT/bench_stats.log" > /dev/null
 echo "profile $TAG done"

@@ -4,7 +4,12 @@ streaming reads on gfx950 and WRITE_SIZE taken as is
 (/opt/skills/guides/MI355X_MICROARCH.md, section HBM); both are reported in
 KiB by rocprofv3 and converted to bytes here.
 
-usage: profile_summary.py <stats_dir> <fetch_dir> <write_dir> <out.json>
+usage: profile_summary.py <stats_dir> <fetch_dir> <write_dir> <out.json> [bench_stats.log]
+
+With the profiled bench's own output (its JSON line), "timed_region" holds the NTT pass kernels'
+summed durations per transform over exactly the bench's timed steps (the last steps x passes
+launches of the trace) next to that same run's ms_per_step: the kernels of a step cannot take
+longer than the step, so the first is <= the second by construction of one run.
 """
 import collections
 import csv
@@ -38,6 +43,17 @@ def main():
         if k in summary["kernels"] and d:
             tail = sorted(d[len(d) // 2:])
             summary["kernels"][k]["steady_median_ns"] = float(tail[len(tail) // 2])
+    if len(sys.argv) > 5:
+        line = [l for l in open(sys.argv[5]) if l.startswith('{"metric"')][-1]
+        bench = json.loads(line)
+        passes = int(bench["roofline"]["kernel"].split()[0])
+        ntt = sorted((r for r in load(f"{stats_dir}/*kernel_trace.csv") if "ntt_pass_kernel" in r["Kernel_Name"]),
+                     key=lambda r: int(r["Start_Timestamp"]))[-bench["steps"] * passes:]
+        summary["timed_region"] = {
+            "steps": bench["steps"], "launches": len(ntt),
+            "kernel_ms_per_transform": sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in ntt)
+            / bench["steps"] / 1e6,
+            "bench_ms_per_step_same_run": bench["ms_per_step"]}
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in (fetch_dir, write_dir):
         for r in load(f"{d}/*counter_collection.csv"):
