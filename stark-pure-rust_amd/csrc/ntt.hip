@@ -630,8 +630,9 @@ struct PassPlan {
 
 constexpr uint32_t kMaxLogR = 9;  // largest radix with a kernel instance and small-root table
 // Radix cap of a size: 2^8 (three passes of 256 at the headline 2^24).  Radix 2^9 passes (three
-// passes instead of four) at 2^25 and from 2^27 on.  At 2^26 the four digit-basis passes (6, 6, 7, 7)
-// beat (8, 9, 9): 7.56 vs 7.73 ms; at 2^25 (8, 8, 9) beats (6, 6, 6, 7): 3.49-3.51 vs 3.55-3.56 ms.
+// passes instead of four) at 2^25 and from 2^27 on.  At 2^25 (8, 8, 9) beats (6, 6, 6, 7): 3.49-3.51 vs
+// 3.55-3.56 ms, and (9, 8, 8) measured within 0.7 % of it (profiles/r04_plan_2_25_26_ab.txt); 2^26 has its
+// own plan (plan_passes).
 inline uint32_t max_log_r(uint32_t log_n) { return (log_n == 25 || log_n >= 27) ? 9 : 8; }
 
 // The smaller radices lead: a sparse first pass of odd radix can skip 3 copy
@@ -647,6 +648,17 @@ PassPlan plan_passes(uint32_t log_n) {
     p.log_r[0] = 8;
     p.log_r[1] = 4;
     p.log_r[2] = 8;
+    return p;
+  }
+  if (log_n == 26) {
+    // 2^26: the last pass radix 2^8 (16 x 16, full table) after three digit-basis radix-2^6 passes:
+    // 6.76-6.77 / 6.98-7.00 vs 7.22 / 7.52-7.54 ms for (6, 6, 7, 7) on two boxes (profiles/r04_plan_2_25_26_ab.txt;
+    // (6, 4, 8, 8) 7.00-7.04, (5, 5, 8, 8) 6.88-6.89, (8, 4, 6, 8) 7.06-7.09, (8, 9, 9) 7.22-7.28)
+    p.n_pass = 4;
+    p.log_r[0] = 6;
+    p.log_r[1] = 6;
+    p.log_r[2] = 6;
+    p.log_r[3] = 8;
     return p;
   }
   const uint32_t cap = max_log_r(log_n);
