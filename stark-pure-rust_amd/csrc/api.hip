@@ -183,7 +183,60 @@ class HostWorkers {
   uint64_t gen_ = 0;
 };
 
+// One side thread for HostTask: one task at a time, tickets in submission order.
+class SideWorker {
+ public:
+  static SideWorker& get() {
+    static SideWorker* w = new SideWorker();  // never destroyed, like HostWorkers
+    return *w;
+  }
+  uint64_t submit(std::function<void()>& fn) {  // 0 when busy (the caller then runs fn itself)
+    std::lock_guard<std::mutex> g(m_);
+    if (task_) return 0;
+    task_ = std::move(fn);
+    const uint64_t t = ++submitted_;
+    cv_.notify_all();
+    return t;
+  }
+  void wait(uint64_t ticket) {
+    std::unique_lock<std::mutex> g(m_);
+    done_cv_.wait(g, [&] { return done_ >= ticket; });
+  }
+
+ private:
+  SideWorker() { std::thread([this] { loop(); }).detach(); }
+  void loop() {
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return (bool)task_; });
+        fn = task_;
+      }
+      fn();
+      std::lock_guard<std::mutex> g(m_);
+      task_ = nullptr;
+      ++done_;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void()> task_;
+  uint64_t submitted_ = 0, done_ = 0;
+};
+
 }  // namespace
+
+HostTask::HostTask(std::function<void()> fn) {
+  ticket_ = SideWorker::get().submit(fn);
+  if (!ticket_) fn();
+}
+
+void HostTask::wait() {
+  if (ticket_) SideWorker::get().wait(ticket_);
+  ticket_ = 0;
+}
 
 unsigned host_threads() { return HostWorkers::get().threads(); }
 void host_parallel(unsigned n, const std::function<void(unsigned)>& fn) { HostWorkers::get().run(n, fn); }
@@ -324,7 +377,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   if (ctx->ev_aux) hipEventDestroy(ctx->ev_aux);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   ctx->fri_trees.clear();
-  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
+  for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->inv_tmp, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
                      &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp})
     if (b->ptr) hipFree(b->ptr);
   hipStreamDestroy(ctx->stream);
@@ -347,7 +400,7 @@ stark_status stark_ctx_memory(const stark_ctx* ctx, size_t* cached_bytes, size_t
   const size_t cached = cache_bytes(ctx);
   size_t total = cached;
   for (const auto& kv : ctx->tw) total += kv.second->base_bytes;
-  for (const DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena,
+  for (const DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->inv_tmp, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena,
                           &ctx->trace_raw, &ctx->fri_misc, &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde,
                           &ctx->ext_idx_tmp})
     total += b->ptr ? b->bytes : 0;

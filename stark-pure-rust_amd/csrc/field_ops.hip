@@ -227,6 +227,7 @@ MontConsts mont_consts() {
 // so the dependent chain per level is ~10 products; large ones use up to 32
 // per thread so the scan costs < 1 product per element.
 constexpr uint64_t kInvTop = 16;
+static_assert(kInvTop * 32 <= 512, "one top array per 512 B of pinned slot 1");
 
 static uint32_t inv_chunk_for(uint64_t n) {
   uint32_t c = 1;
@@ -234,19 +235,18 @@ static uint32_t inv_chunk_for(uint64_t n) {
   return c;
 }
 
-stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s) {
+// Phase 1: the up kernels (scratch from `buf`; the top level's <= 16 products land in h_top, a pinned
+// coherent host array).  The caller synchronises, then multi_inv_top and multi_inv_down.
+stark_status multi_inv_up(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s, DevBuf& buf,
+                          fe* h_top, InvPlan& plan) {
+  plan.lv.clear();
+  plan.h_top = h_top;
   if (n == 0) return STARK_OK;
-  struct Level {
-    uint64_t n;
-    uint32_t chunk, wgs;
-    const fe* in;
-    fe *out, *pref, *others, *tot;
-  };
-  std::vector<Level> lv;
+  std::vector<InvPlan::Level>& lv = plan.lv;
   uint64_t m = n;
   size_t total = 0;
   while (m > kInvTop || lv.empty()) {
-    Level L{};
+    InvPlan::Level L{};
     L.n = m;
     L.chunk = inv_chunk_for(m);
     const uint64_t threads = (m + L.chunk - 1) / L.chunk;
@@ -255,11 +255,11 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
     lv.push_back(L);
     m = L.wgs;
   }
-  stark_status st = ensure_buf(ctx, ctx->io2, total * sizeof(fe));
+  stark_status st = ensure_buf(ctx, buf, total * sizeof(fe));
   if (st != STARK_OK) return st;
-  fe* at = (fe*)ctx->io2.ptr;
+  fe* at = (fe*)buf.ptr;
   for (size_t i = 0; i < lv.size(); ++i) {
-    Level& L = lv[i];
+    InvPlan::Level& L = lv[i];
     L.in = i ? lv[i - 1].tot : d_in;
     L.out = i ? nullptr : d_out;
     L.pref = at;
@@ -274,32 +274,38 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
     lv[i].out = at;
     at += lv[i].n;
   }
-  // Top: at most 16 non-zero Montgomery products, written by the last up
-  // kernel straight into the pinned (coherent) host slot, inverted there on
-  // the host and read back by the first down kernel, with no copies.
-  uint8_t* pinned = nullptr;
-  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
-  if (st != STARK_OK) return st;
-  fe* h_top = (fe*)(pinned + 2560);  // pinned slot 1 layout: [2560, 3072) batch-inverse top level
+  // Top: at most 16 non-zero Montgomery products, written by the last up kernel straight into the
+  // pinned (coherent) host array, inverted there on the host and read back by the first down kernel,
+  // with no copies.
   lv.back().tot = h_top;
   const MontConsts mc = mont_consts();
-  for (const Level& L : lv)
+  for (const InvPlan::Level& L : lv)
     hipLaunchKernelGGL(inv_up_kernel, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk, L.pref, L.others,
                        L.tot, mc);
   STARK_HIP(ctx, hipGetLastError());
-  const Level& T = lv.back();
-  STARK_HIP(ctx, hipStreamSynchronize(s));
-  {
-    const FieldHost& F = FieldHost::get();
-    for (uint32_t i = 0; i < T.wgs; ++i) {
-      HostFp x;
-      for (int k = 0; k < 4; ++k) x.v[k] = (uint64_t)h_top[i].w[2 * k] | ((uint64_t)h_top[i].w[2 * k + 1] << 32);
-      h_top[i] = to_dev(F.inv(x));  // Montgomery in, Montgomery out; products are never zero
-    }
+  return STARK_OK;
+}
+
+// Phase 2 (host, after the caller's synchronisation): the top level's inverses in place.
+void multi_inv_top(const InvPlan& plan) {
+  if (plan.lv.empty()) return;
+  const FieldHost& F = FieldHost::get();
+  for (uint32_t i = 0; i < plan.lv.back().wgs; ++i) {
+    HostFp x;
+    for (int k = 0; k < 4; ++k)
+      x.v[k] = (uint64_t)plan.h_top[i].w[2 * k] | ((uint64_t)plan.h_top[i].w[2 * k + 1] << 32);
+    plan.h_top[i] = to_dev(F.inv(x));  // Montgomery in, Montgomery out; products are never zero
   }
+}
+
+// Phase 3: the down kernels.
+stark_status multi_inv_down(stark_ctx* ctx, const InvPlan& plan, hipStream_t s) {
+  const std::vector<InvPlan::Level>& lv = plan.lv;
+  if (lv.empty()) return STARK_OK;
+  const MontConsts mc = mont_consts();
   for (size_t i = lv.size(); i-- > 0;) {
-    const Level& L = lv[i];
-    const fe* wg_inv = i + 1 < lv.size() ? lv[i + 1].out : h_top;
+    const InvPlan::Level& L = lv[i];
+    const fe* wg_inv = i + 1 < lv.size() ? lv[i + 1].out : plan.h_top;
     if (i == 0)
       hipLaunchKernelGGL(inv_down_kernel<true>, dim3(L.wgs), dim3(kInvThreads), 0, s, L.in, L.n, L.chunk,
                          (const fe*)L.pref, (const fe*)L.others, wg_inv, L.out, mc);
@@ -309,6 +315,23 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
   }
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
+}
+
+fe* multi_inv_h_top(stark_ctx* ctx, int k) {  // pinned slot 1: [2560 + 512 k, 3072 + 512 k), k < 2
+  uint8_t* pinned = nullptr;
+  if (ctx_pinned(ctx, 1, kPinned1Bytes, (void**)&pinned) != STARK_OK) return nullptr;
+  return (fe*)(pinned + kPinned1InvTopOff + 512 * (size_t)k);
+}
+
+stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s) {
+  if (n == 0) return STARK_OK;
+  fe* h_top = multi_inv_h_top(ctx, 0);
+  if (!h_top) return STARK_ERR_OOM;
+  InvPlan plan;
+  STARK_TRY(multi_inv_up(ctx, d_in, d_out, n, s, ctx->io2, h_top, plan));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  multi_inv_top(plan);
+  return multi_inv_down(ctx, plan, s);
 }
 
 }  // namespace stark

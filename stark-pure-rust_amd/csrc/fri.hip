@@ -157,7 +157,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
   if (st != STARK_OK) return st;
   uint8_t* pinned = nullptr;
-  st = ctx_pinned(ctx, 1, 4096, (void**)&pinned);
+  st = ctx_pinned(ctx, 1, kPinned1Bytes, (void**)&pinned);
   if (st != STARK_OK) return st;
   p->h_roots = pinned + kFriRootsOff;
   fe* d_sx = (fe*)ctx->fri_misc.ptr;
@@ -247,13 +247,23 @@ stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& e
     reqs.push_back({trees[layer + 1], L.col_idx.data(), 40, L.col_leaves.data(), L.col_nodes.data()});
     reqs.push_back({trees[layer], L.poly_idx.data(), 160, L.poly_leaves.data(), L.poly_nodes.data()});
   }
+  // The last layer's values come down with the gather (one synchronisation) when they fit the pinned slot.
+  const size_t last_bytes = p->last_len * 32;
+  uint8_t* h_last = const_cast<uint8_t*>(p->h_roots) - kFriRootsOff + kPinned1LastOff;
+  const bool last_pinned = last_bytes && last_bytes <= kPinned1Bytes - kPinned1LastOff;
+  if (last_pinned) STARK_HIP(ctx, hipMemcpyAsync(h_last, p->last_dev, last_bytes, hipMemcpyDeviceToHost, s));
   stark_status st = merkle_gather_batch(ctx, reqs, s);
   if (st != STARK_OK) return st;
+  size_t gathered = 0;
+  for (const GatherReq& q : reqs) gathered += q.k;
+  if (last_pinned && gathered == 0) STARK_HIP(ctx, hipStreamSynchronize(s));  // (no gather: no synchronisation)
   stark_fri_layer last;
   last.last = true;
-  last.last_values.resize(p->last_len * 32);
-  if (p->last_len)
-    STARK_HIP(ctx, hipMemcpy(last.last_values.data(), p->last_dev, p->last_len * 32, hipMemcpyDeviceToHost));
+  last.last_values.resize(last_bytes);
+  if (last_pinned)
+    memcpy(last.last_values.data(), h_last, last_bytes);
+  else if (last_bytes)
+    STARK_HIP(ctx, hipMemcpy(last.last_values.data(), p->last_dev, last_bytes, hipMemcpyDeviceToHost));
   proof->layers.push_back(std::move(last));
   *out = p->proof.release();
   return STARK_OK;
@@ -268,48 +278,67 @@ stark_status fri_prove_device(stark_ctx* ctx, const fe* d_values, size_t n, cons
   return fri_finish(ctx, p.get(), none, out);
 }
 
-// "[b0,b1,...]" for a byte string (serde_json of Vec<u8>), table driven.
+// "[b0,b1,...]" for a byte string (serde_json of Vec<u8>), table driven: each byte is one 4-byte store
+// of its digits and a comma and an advance by their count (no branch); the last comma becomes ']'.
 struct ByteText {
-  char s[256][4];
+  uint32_t s[256];  // the decimal digits of i then ',' (little-endian bytes)
   uint8_t len[256];
   ByteText() {
-    for (int i = 0; i < 256; ++i) len[i] = (uint8_t)snprintf(s[i], sizeof s[i], "%d", i);
+    for (int i = 0; i < 256; ++i) {
+      char t[8] = {0};
+      len[i] = (uint8_t)snprintf(t, sizeof t, "%d,", i);
+      memcpy(&s[i], t, 4);  // (4 bytes: the padding past the comma is overwritten by the next byte)
+    }
   }
 };
 
-void json_bytes(std::string& o, const uint8_t* p, size_t n) {
+// Writes "[b0,...]" at w (at most 2 + 4 n bytes; the 4-byte stores may touch 2 bytes past the
+// returned end, inside that bound) and returns the end.
+static char* json_bytes_at(char* w, const uint8_t* p, size_t n) {
   static const ByteText T;
-  const size_t at = o.size();
-  o.resize(at + 2 + 4 * n);  // upper bound: 3 digits + comma per byte
-  char* w = &o[at];
   *w++ = '[';
   for (size_t i = 0; i < n; ++i) {
-    if (i) *w++ = ',';
     const uint8_t b = p[i];
-    memcpy(w, T.s[b], 4);
+    memcpy(w, &T.s[b], 4);
     w += T.len[b];
   }
+  if (n) --w;  // the last comma
   *w++ = ']';
+  return w;
+}
+
+void json_bytes(std::string& o, const uint8_t* p, size_t n) {
+  const size_t at = o.size();
+  o.resize(at + 2 + 4 * n);  // upper bound: 3 digits + comma per byte
+  char* w = json_bytes_at(&o[at], p, n);
   o.resize((size_t)(w - &o[0]));
 }
 
 // Proofs [i0, i1) of a serde_json Vec<Proof<Vec<u8>, BlakeDigest>>
 // (commitment/src/merkle_tree.rs:14-18), each preceded by a comma unless it is
-// proof 0; the caller writes the brackets.
+// proof 0; the caller writes the brackets.  Rendered into one buffer sized for the worst case.
 static void json_branch_range(std::string& o, const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes,
                               size_t i0, size_t i1, size_t depth) {
-  o.reserve(o.size() + (i1 - i0) * (24 + 4 * leaf_len + depth * 130));
+  static const char kLeaf[] = "{\"leaf\":", kNodes[] = ",\"nodes\":[";
+  const size_t per = 1 + (sizeof kLeaf - 1) + (2 + 4 * leaf_len) + (sizeof kNodes - 1) + depth * (1 + 2 + 4 * 32) + 2;
+  const size_t at = o.size();
+  o.resize(at + (i1 - i0) * per + 8);
+  char* w = &o[at];
   for (size_t i = i0; i < i1; ++i) {
-    if (i) o.push_back(',');
-    o += "{\"leaf\":";
-    json_bytes(o, leaves + leaf_len * i, leaf_len);
-    o += ",\"nodes\":[";
+    if (i) *w++ = ',';
+    memcpy(w, kLeaf, sizeof kLeaf - 1);
+    w += sizeof kLeaf - 1;
+    w = json_bytes_at(w, leaves + leaf_len * i, leaf_len);
+    memcpy(w, kNodes, sizeof kNodes - 1);
+    w += sizeof kNodes - 1;
     for (size_t d = 0; d < depth; ++d) {
-      if (d) o.push_back(',');
-      json_bytes(o, nodes + (i * depth + d) * 32, 32);
+      if (d) *w++ = ',';
+      w = json_bytes_at(w, nodes + (i * depth + d) * 32, 32);
     }
-    o += "]}";
+    *w++ = ']';
+    *w++ = '}';
   }
+  o.resize((size_t)(w - &o[0]));
 }
 
 void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,

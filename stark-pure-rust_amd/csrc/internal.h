@@ -114,6 +114,7 @@ struct stark_ctx {
   stark::DevBuf lde_tmp;      // circuit_lde's step columns and Zb values
   stark::DevBuf verify_arena, verify_lde;  // the verifier's circuit, kept for the next call
   stark::DevBuf ext_idx_tmp;  // an IDX extension too large for the cache cap (this proof only)
+  stark::DevBuf inv_tmp;      // the scratch of a second batch inverse sharing a host round trip (r1cs.hip)
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -126,6 +127,8 @@ struct stark_ctx {
   // openings gathered while its FRI layers still run, r1cs.hip); created on first use.
   hipStream_t aux = nullptr;
   hipEvent_t ev_aux = nullptr;
+  // The device trace builder's deferred wire-id flag for the proof being built (stark_prove_r1cs_bytes).
+  const uint32_t* trace_err = nullptr;
   // (root canonical limbs, log_n) -> tables
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t>, std::unique_ptr<stark::Twiddles>> tw;
   // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
@@ -168,6 +171,33 @@ bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext);
 // Slot 0: gather batches; slot 1: transcript values and roots; slot 2: the device trace builder's
 // record-walk tables; slot 3: its upload staging (the raw .r1cs constraint section and witness).
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
+// Pinned slot 1 (always this size, so no caller's pointer into it moves): [0, 2048) the prover's
+// transcript head, [2048, 2560) FRI roots, [2560, 3584) two batch inverses' top levels, [3584, 3588) the
+// trace builder's deferred flag, [4096, 16384) the last FRI layer's values.
+constexpr size_t kPinned1Bytes = 16384;
+constexpr size_t kPinned1InvTopOff = 2560;
+constexpr size_t kPinned1TraceErrOff = 3584;
+constexpr size_t kPinned1LastOff = 4096;
+
+// Batch inverse (0 -> 0) in phases (field_ops.hip), so that one host round trip can serve two of them:
+// multi_inv_up enqueues the up kernels, the caller synchronises its stream, multi_inv_top inverts the
+// top level on the host, multi_inv_down enqueues the down kernels.  multi_inv_device does all four.
+struct InvPlan {
+  struct Level {
+    uint64_t n;
+    uint32_t chunk, wgs;
+    const fe* in;
+    fe *out, *pref, *others, *tot;
+  };
+  std::vector<Level> lv;
+  fe* h_top = nullptr;
+};
+stark_status multi_inv_up(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s, DevBuf& buf,
+                          fe* h_top, InvPlan& plan);
+void multi_inv_top(const InvPlan& plan);
+stark_status multi_inv_down(stark_ctx* ctx, const InvPlan& plan, hipStream_t s);
+fe* multi_inv_h_top(stark_ctx* ctx, int k);  // top array k < 2 in pinned slot 1 (null: no pinned memory)
+stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
 
 // Host worker threads shared by the host-side stages (trace build, proof
 // JSON): host_parallel(n, fn) runs fn(0) .. fn(n-1), fn(0) on the caller, the
@@ -175,6 +205,20 @@ stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
 // millisecond-scale work it splits).  host_threads() = workers + 1 (<= 16).
 unsigned host_threads();
 void host_parallel(unsigned n, const std::function<void(unsigned)>& fn);
+// A task run on the process's side thread while the caller goes on (the caller waits for it with
+// wait() or the destructor, so the task may use the caller's locals).  When the side thread is busy
+// with another caller's task, the task runs inline in the constructor.
+class HostTask {
+ public:
+  explicit HostTask(std::function<void()> fn);
+  ~HostTask() { wait(); }
+  void wait();
+  HostTask(const HostTask&) = delete;
+  HostTask& operator=(const HostTask&) = delete;
+
+ private:
+  uint64_t ticket_ = 0;  // 0: ran inline or already waited for
+};
 // Context-owned Merkle tree slot (created on first use).
 stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out);
 hipStream_t pick_stream(stark_ctx* ctx, void* stream);
@@ -270,9 +314,12 @@ struct DevTrace {
   uint64_t* perm = nullptr;
   std::vector<uint64_t> public_wires;       // canonical limbs, 4 per wire
   std::vector<size_t> public_first_indices;  // (wire, slot) pairs
+  const uint32_t* d_err = nullptr;           // defer_err: the device's wire-id flag, not yet read
 };
+// defer_err: no read-back when the host finds the public wires' first uses itself; the caller then
+// reads d_err (non-zero: a wire id >= n_wires, STARK_ERR_BAD_ARG) at its own first synchronisation.
 stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
-                               size_t wtns_len, DevTrace* out);
+                               size_t wtns_len, DevTrace* out, bool defer_err = false);
 // mk_r1cs_proof on trace columns given as host or device pointers, flags as
 // bytes (r1cs.hip).
 // The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the
@@ -317,7 +364,7 @@ stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_t
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,
                                       const size_t* permuted_indices, const uint64_t* coefficients,
                                       const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
-                                      stark_r1cs_proof** out);
+                                      stark_r1cs_proof** out, bool dev_in = false);
 
 // FRI prover on device values (fri.hip).  fri_enqueue puts every layer on the
 // context stream with a device-side transcript and queues the roots' download;

@@ -30,7 +30,6 @@
 #include "fe_db.h"
 
 namespace stark {
-stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
 void json_bytes(std::string& o, const uint8_t* p, size_t n);
 void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
                    const std::vector<uint8_t>& nodes, size_t k, size_t depth);
@@ -240,6 +239,39 @@ __global__ void r1cs_flags_kernel(const uint8_t* __restrict__ fb, uint64_t os, u
   if (g >= 3 * os) return;
   const uint64_t f = g / os, i = g - f * os;
   fe_store(dst + f * steps + i, fe_from_u64(fb[g]));
+}
+
+// The proof's input columns from device-resident trace columns in one launch (the device trace builder's
+// output, stark_prove_r1cs_bytes), in place of a dozen copies and fills: raw[c] (c < 6: K F0 F1 F2 S P) =
+// the column zero-padded to `steps` (F0-F2 widened from their 0/1 bytes), wcopy = S, perm copied, and
+// the transcript zeroed.
+struct PackArgs {
+  const fe* col[6];     // K, (F0, F1, F2 when given as elements), S, P
+  const uint8_t* fb;    // F0-F2 as 3 x os bytes (or null)
+  const uint64_t* perm_in;
+  uint64_t os, steps;
+  fe* raw;
+  fe* wcopy;
+  uint64_t* perm;
+  uint32_t* tr;         // the transcript, tr_words u32
+  uint32_t tr_words;
+};
+__global__ void r1cs_pack_kernel(PackArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < a.tr_words) a.tr[i] = 0;
+  if (i >= a.steps) return;
+  const bool in = i < a.os;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    fe v = fe_zero();
+    if (in) {
+      if (a.fb && c >= 1 && c <= 3) v = fe_from_u64(a.fb[(uint64_t)(c - 1) * a.os + i]);
+      else v = fe_load(a.col[c] + i);
+    }
+    fe_store(a.raw + (uint64_t)c * a.steps + i, v);
+    if (c == 4) fe_store(a.wcopy + i, v);
+  }
+  if (in) a.perm[i] = a.perm_in[i];
 }
 
 // val_nmr / val_dnm of calc_a_mini_evaluations (utils.rs:317-318), written as
@@ -826,7 +858,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                                const size_t* public_first_indices, size_t n_pfi, const size_t* permuted_indices,
                                const uint64_t* coefficients, const uint64_t* flag0, const uint64_t* flag1,
                                const uint64_t* flag2, const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
-                               stark_r1cs_proof** out, const fe* pre = nullptr) {
+                               stark_r1cs_proof** out, const fe* pre = nullptr, bool dev_in = false) {
+  // dev_in: every column, the flag bytes and the permutation are device pointers (one pack launch).
   // pre != nullptr: the circuit's LDE columns K F0 F1 F2 IDX PIDX (precision each) and the
   // inverses of Zb2, Zb3 (2 x precision), prepared once per circuit (stark_r1cs_circuit_new);
   // only S, P and A are extended here.
@@ -889,12 +922,31 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).  The
   // inputs may be host or device pointers (the device trace builder's columns): hipMemcpyDefault.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};
-  for (int c = pre ? 4 : 0; c < 6; ++c) {
+  const bool pack = dev_in && !pre;
+  if (pack) {
+    if (!flag_bytes && (!flag0 || !flag1 || !flag2)) return STARK_ERR_BAD_ARG;
+    PackArgs pa;
+    for (int c = 0; c < 6; ++c) pa.col[c] = (const fe*)src[c];
+    pa.fb = flag_bytes;
+    pa.perm_in = (const uint64_t*)permuted_indices;
+    pa.os = os;
+    pa.steps = steps;
+    pa.raw = raw;
+    pa.wcopy = wcopy;
+    pa.perm = perm;
+    static_assert(sizeof(Transcript) % 4 == 0, "transcript words");
+    pa.tr = (uint32_t*)d_tr;
+    pa.tr_words = (uint32_t)(sizeof(Transcript) / 4);
+    hipLaunchKernelGGL(r1cs_pack_kernel, dim3(blocks_for(std::max<uint64_t>(steps, pa.tr_words))), dim3(256), 0, s,
+                       pa);
+    STARK_HIP(ctx, hipGetLastError());
+  }
+  for (int c = pre ? 4 : 0; c < 6 && !pack; ++c) {
     if (!(flag_bytes && c >= 1 && c <= 3))
       STARK_HIP(ctx, hipMemcpyAsync(raw + c * steps, src[c], os * sizeof(fe), hipMemcpyDefault, s));
     if (steps > os) STARK_HIP(ctx, hipMemsetAsync(raw + c * steps + os, 0, (steps - os) * sizeof(fe), s));
   }
-  if (flag_bytes && !pre) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
+  if (flag_bytes && !pre && !pack) {  // 0/1 flags as bytes (the trace builder's compact form), widened on the GPU
     uint8_t* d_fb = (uint8_t*)zb;  // zb is free until the Zb kernel
     STARK_HIP(ctx, hipMemcpyAsync(d_fb, flag_bytes, 3 * os, hipMemcpyDefault, s));
     hipLaunchKernelGGL(r1cs_flags_kernel, dim3(blocks_for(3 * os)), dim3(256), 0, s, (const uint8_t*)d_fb,
@@ -902,10 +954,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     STARK_HIP(ctx, hipGetLastError());
   }
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
-  STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
-  STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
+  if (!pack) {
+    STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
+    STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
+    STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
+  }
   clk.mark("setup + uploads enqueued");
-  STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
   // (IDX is not materialised: idx_ext is the shared extension.)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
                      (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves);
@@ -934,19 +988,30 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
   STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
-  STARK_TRY(multi_inv_device(ctx, dnm_c, inv_dnm, steps, s));
-  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
-                     (const fe*)inv_dnm, steps, raw);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(lde(ctx, raw, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
-
-  if (!pre) {  // prepared circuits carry these (they depend on the public wires' positions only)
+  // The cold proof's two batch inverses (the A denominators over the steps; Zb2, Zb3 over the precision
+  // domain, which prepared circuits carry) share one host round trip: both up passes, one
+  // synchronisation, both top levels on the host, then the down passes.
+  InvPlan inv_d, inv_z;
+  fe* const top_d = multi_inv_h_top(ctx, 0);
+  fe* const top_z = multi_inv_h_top(ctx, 1);
+  if (!top_d || !top_z) return STARK_ERR_OOM;
+  if (!pre) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                        (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
                        zb, zb + prec);
     STARK_HIP(ctx, hipGetLastError());
-    STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * prec, s));
+    STARK_TRY(multi_inv_up(ctx, zb, inv_zb, 2 * prec, s, ctx->io2, top_z, inv_z));
   }
+  STARK_TRY(multi_inv_up(ctx, dnm_c, inv_dnm, steps, s, ctx->inv_tmp, top_d, inv_d));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  multi_inv_top(inv_d);
+  multi_inv_top(inv_z);
+  STARK_TRY(multi_inv_down(ctx, inv_d, s));
+  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
+                     (const fe*)inv_dnm, steps, raw);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(lde(ctx, raw, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
+  STARK_TRY(multi_inv_down(ctx, inv_z, s));  // (empty plan with a prepared circuit)
 
   // Constraint kernel.
   ConstraintArgs ca;
@@ -1009,8 +1074,14 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   // The roots and the constraint flags come down behind the L tree; an event marks them.
   Transcript* h_tr = nullptr;
-  STARK_TRY(ctx_pinned(ctx, 1, sizeof(Transcript) + 1024, (void**)&h_tr));
-  STARK_HIP(ctx, hipMemcpyAsync(h_tr, d_tr, sizeof(Transcript), hipMemcpyDeviceToHost, s));
+  // (slot 1 layout: internal.h kPinned1Bytes)
+  // (only the head: the constants' digit-basis tables stay on the device)
+  constexpr size_t kTrHead = offsetof(Transcript, k_db);
+  static_assert(kTrHead <= 2048, "pinned slot 1 layout");
+  STARK_TRY(ctx_pinned(ctx, 1, kPinned1Bytes, (void**)&h_tr));
+  uint32_t* h_trace_err = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(h_tr) + kPinned1TraceErrOff);
+  STARK_HIP(ctx, hipMemcpyAsync(h_tr, d_tr, kTrHead, hipMemcpyDeviceToHost, s));
+  if (ctx->trace_err) STARK_HIP(ctx, hipMemcpyAsync(h_trace_err, ctx->trace_err, 4, hipMemcpyDeviceToHost, s));
   if (!ctx->ev_aux) STARK_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_aux, hipEventDisableTiming));
   if (!ctx->aux) STARK_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, s));
@@ -1024,6 +1095,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // the second stream) and the StarkProof JSON up to fri_proof.
   STARK_HIP(ctx, hipEventSynchronize(ctx->ev_aux));
   clk.mark("wait for the L root");
+  if (ctx->trace_err && *h_trace_err) {  // a wire id >= n_wires (reader.rs:4-89 bounds), found by the trace builder
+    hipStreamSynchronize(s);
+    ctx->last_error = "constraint record with a wire id >= n_wires";
+    return STARK_ERR_BAD_ARG;
+  }
   if (h_tr->err) {
     hipStreamSynchronize(s);  // (the enqueued FRI work finishes before the proof is dropped)
     ctx->last_error = (h_tr->err & 1) ? "invalid D: Q does not vanish where Z does (utils.rs:379-418)"
@@ -1065,14 +1141,19 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   j.text(",\"linear_comb_branches\":");
   j.branches(l_leaves, 32, l_nodes, kSpotChecks, log_prec);
   j.text(",\"fri_proof\":");
-  j.prerender();
-  clk.mark("spot checks + their JSON (beside FRI)");
-  STARK_HIP(ctx, hipStreamSynchronize(s));  // the FRI layers
-  clk.mark("device wait");
+  clk.mark("spot-check openings");
   std::vector<GatherReq> extra;
   stark_fri_proof* fri = nullptr;
-  STARK_TRY(fri_finish(ctx, fri_pending.get(), extra, &fri));
-  clk.mark("FRI indices + gather");
+  {
+    // The head renders on the side thread while this one waits for the FRI layers and gathers their
+    // openings (for a small proof the FRI kernels finish before the head would be rendered).
+    HostTask head([&] { j.prerender(); });
+    const stark_status st = fri_finish(ctx, fri_pending.get(), extra, &fri);
+    clk.mark("FRI wait + indices + gather");
+    head.wait();
+    clk.mark("proof head JSON (beside them)");
+    if (st != STARK_OK) return st;
+  }
   proof->fri = fri;  // owned by the proof from here on
   fri_proof_json_pieces(fri, j);
   j.text("}");
@@ -1195,13 +1276,13 @@ stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_t
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,
                                       const size_t* permuted_indices, const uint64_t* coefficients,
                                       const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
-                                      stark_r1cs_proof** out) {
+                                      stark_r1cs_proof** out, bool dev_in) {
   if (!ctx || !out) return STARK_ERR_BAD_ARG;
   *out = nullptr;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   const stark_status st = prove_r1cs(ctx, witness_trace, computational_trace, os, public_wires, n_public,
                                      public_first_indices, n_pfi, permuted_indices, coefficients, nullptr, nullptr,
-                                     nullptr, flag_bytes, n_constraints, n_wires, out);
+                                     nullptr, flag_bytes, n_constraints, n_wires, out, nullptr, dev_in);
   hipStreamSynchronize(ctx->stream);
   return st;
 }

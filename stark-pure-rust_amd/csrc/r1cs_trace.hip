@@ -126,7 +126,7 @@ stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_t
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,
                                       const size_t* permuted_indices, const uint64_t* coefficients,
                                       const uint8_t* flag_bytes, size_t n_constraints, size_t n_wires,
-                                      stark_r1cs_proof** out);
+                                      stark_r1cs_proof** out, bool dev_in);
 }
 
 namespace stark {

@@ -113,7 +113,9 @@ __global__ void slot_fill_kernel(FillArgs a) {
   a.vals[push] = (uint32_t)slot;
 }
 
-// comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels).
+// comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels).  The
+// terms are loaded eight at a time ahead of their additions, so a long factor (hundreds of terms in
+// pedersen_test, a thousand in bits.r1cs) waits for one memory latency per eight terms, not per term.
 __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
                                    fe* __restrict__ comp) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,9 +124,18 @@ __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n
   const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
   fe* c = comp + (uint64_t)f * a_len + b0;
   fe acc = fe_zero();
-  for (uint32_t i = 0; i < n_coeff; ++i) {
-    acc = fe_add(acc, fe_load(c + i));
-    fe_store(c + i, acc);
+  constexpr uint32_t kAhead = 8;
+  for (uint32_t i = 0; i < n_coeff; i += kAhead) {
+    fe v[kAhead];
+#pragma unroll
+    for (uint32_t k = 0; k < kAhead; ++k)
+      if (i + k < n_coeff) v[k] = fe_load(c + i + k);
+#pragma unroll
+    for (uint32_t k = 0; k < kAhead; ++k)
+      if (i + k < n_coeff) {
+        acc = fe_add(acc, v[k]);
+        fe_store(c + i + k, acc);
+      }
   }
 }
 
@@ -216,6 +227,40 @@ stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, st
   return walk_records_into(cons, cons_len, n_c, fac.data(), base.data());
 }
 
+// The first use of every public wire (run.rs:411-419) read from the records on the host, in push order
+// (constraint, factor, slot; a factor's padding slots use the last wire), as perm_kernel finds it after
+// the sort.  Stops once every public wire is found; false (undecided) past `budget` slots or at a wire
+// id >= n_wires (the device flags that one and the caller reports it).
+bool host_first_uses(const uint8_t* cons, const uint32_t* fac, const uint32_t* base, uint32_t n_c, uint64_t a_len,
+                     size_t n_public, uint32_t n_wires, uint64_t budget, std::vector<uint64_t>& pf) {
+  pf.assign(n_public, ~0ull);
+  size_t found = 0;
+  uint64_t seen = 0;
+  const uint32_t* fac_rec = fac;
+  const uint32_t* fac_cnt = fac + (size_t)3 * n_c;
+  for (uint32_t ci = 0; ci < n_c && found < n_public; ++ci) {
+    const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
+    for (uint32_t f = 0; f < 3 && found < n_public; ++f) {
+      const uint32_t cnt = fac_cnt[3 * (size_t)ci + f];
+      const uint8_t* r = cons + fac_rec[3 * (size_t)ci + f];
+      for (uint32_t i = 0; i < n_coeff; ++i) {
+        uint32_t wire = n_wires - 1;
+        if (i < cnt) {
+          memcpy(&wire, r + 36 * (size_t)i, 4);
+          if (wire >= n_wires) return false;
+        }
+        if (wire < n_public && pf[wire] == ~0ull) {
+          pf[wire] = (uint64_t)f * a_len + b0 + i;
+          if (++found == n_public) break;
+        }
+      }
+      seen += n_coeff;
+      if (seen > budget) return false;
+    }
+  }
+  return true;
+}
+
 }  // namespace
 
 // Host-to-device copies of caller (pageable) memory through the context's pinned staging buffer:
@@ -284,7 +329,7 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
 }
 
 stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
-                               size_t wtns_len, DevTrace* out) {
+                               size_t wtns_len, DevTrace* out, bool defer_err) {
   PhaseClock clk("r1cs trace build (device)");
   const FieldHost& F = FieldHost::get();
   R1csHeader hd;
@@ -327,8 +372,16 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   hipStream_t s = ctx->stream;
   stark_status walk_st = STARK_OK;
   const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
-  st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers,
-                     [&] { walk_st = walk_records_into(cons, cons_len, n_c, fac, base); });
+  // defer_err: the public wires' first uses are also read on the host beside the uploads (a bounded scan
+  // that usually ends in the first constraints), so the build needs no read-back and the caller checks
+  // the device's wire-id flag at its own first synchronisation (d_err).
+  std::vector<uint64_t> pf_host;
+  bool pf_ok = false;
+  st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers, [&] {
+    walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
+    if (walk_st == STARK_OK && defer_err && n_wires > 0)
+      pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
+  });
   if (st != STARK_OK) return st;
   if (walk_st != STARK_OK) return walk_st;
   const uint64_t a_len = base[n_c];
@@ -409,13 +462,19 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
                      (uint32_t)n_public, (uint64_t*)(A + o_perm), (uint64_t*)(A + o_pf));
   STARK_HIP(ctx, hipGetLastError());
   clk.mark("kernels enqueued");
-  // First uses of the public wires and the error flag: the one host read-back.
   std::vector<uint64_t> pf(n_public);
-  uint32_t h_err = 0;
-  STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
-  if (h_err) return STARK_ERR_BAD_ARG;  // a wire id >= n_wires (reader.rs:4-89 bounds)
+  out->d_err = nullptr;
+  if (pf_ok) {  // the host scan found them: no read-back, the caller checks err later
+    pf = pf_host;
+    out->d_err = err;
+  } else {
+    // First uses of the public wires and the error flag: the one host read-back.
+    uint32_t h_err = 0;
+    STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
+    STARK_HIP(ctx, hipMemcpyAsync(&h_err, err, 4, hipMemcpyDeviceToHost, s));
+    STARK_HIP(ctx, hipStreamSynchronize(s));
+    if (h_err) return STARK_ERR_BAD_ARG;  // a wire id >= n_wires (reader.rs:4-89 bounds)
+  }
   out->public_first_indices.clear();
   for (size_t wi = 0; wi < n_public && wi < n_wires; ++wi)
     if (pf[wi] != ~0ull) {
@@ -610,13 +669,17 @@ stark_status stark_prove_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t 
   *out = nullptr;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   DevTrace dt;
-  const stark_status st = r1cs_trace_device(ctx, r1cs, r1cs_len, wtns, wtns_len, &dt);
+  stark_status st = r1cs_trace_device(ctx, r1cs, r1cs_len, wtns, wtns_len, &dt, true);
   if (st != STARK_OK) return st;
-  return mk_r1cs_proof_bytes_flags(ctx, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
-                                   dt.public_wires.data(), dt.public_wires.size() / 4,
-                                   dt.public_first_indices.data(), dt.public_first_indices.size() / 2,
-                                   (const size_t*)dt.perm, (const uint64_t*)dt.coef, dt.flags, dt.n_constraints,
-                                   dt.n_wires, out);
+  // (a deferred wire-id flag is read with the prover's first download and reported as STARK_ERR_BAD_ARG)
+  ctx->trace_err = dt.d_err;
+  st = mk_r1cs_proof_bytes_flags(ctx, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
+                                 dt.public_wires.data(), dt.public_wires.size() / 4,
+                                 dt.public_first_indices.data(), dt.public_first_indices.size() / 2,
+                                 (const size_t*)dt.perm, (const uint64_t*)dt.coef, dt.flags, dt.n_constraints,
+                                 dt.n_wires, out, true);  // (device columns: one pack launch)
+  ctx->trace_err = nullptr;
+  return st;
 }
 
 
