@@ -61,13 +61,10 @@ __global__ void fri_special_x_kernel(const uint32_t* __restrict__ root, fe* __re
 // Row i of q (local rows; global row g_add + (i << log_g) on a distributed
 // prover whose values are the residue class g_add mod 2^log_g, where the four
 // points of a row are local too since n/4 is a multiple of 2^log_g).
-__global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
-                                uint64_t g_add, uint32_t log_g,
-                                const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
-                                const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= q) return;
-  const fe s_m = *s_ptr;
+__device__ __forceinline__ void fri_fold_row(const fe* __restrict__ v, fe* __restrict__ col, uint64_t i, uint64_t q,
+                                             uint32_t shift, uint64_t g_add, uint32_t log_g,
+                                             const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
+                                             const fe& s_m, const fe& zeta_m, const fe& inv4_m) {
   const fe y0 = fe_load(v + i), y1 = fe_load(v + i + q), y2 = fe_load(v + i + 2 * q), y3 = fe_load(v + i + 3 * q);
   const uint64_t e = (g_add + (i << log_g)) << shift;
   const fe winv = fe_mul(lo[e & (((uint64_t)1 << kb) - 1)], hi[e >> kb]);  // Montgomery w^-i
@@ -81,6 +78,15 @@ __global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, 
   acc = fe_add(fe_mul(acc, u_m), d1);
   acc = fe_add(fe_mul(acc, u_m), d0);
   fe_store(col + i, fe_mul(acc, inv4_m));
+}
+
+__global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
+                                uint64_t g_add, uint32_t log_g,
+                                const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
+                                const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q) return;
+  fri_fold_row(v, col, i, q, shift, g_add, log_g, lo, hi, kb, *s_ptr, zeta_m, inv4_m);
 }
 
 // Roots of up to 16 trees gathered into one buffer (one D2H for the transcript).
@@ -370,11 +376,12 @@ void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, c
 }
 
 // Renders every piece into its own string on the host workers.
-static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, std::vector<std::string>& out) {
+static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, std::vector<std::string>& out,
+                          unsigned max_threads = 16) {
   out.assign(fns.size(), std::string());
   std::atomic<size_t> next{0};
   unsigned nt = host_threads();
-  if (nt > 16) nt = 16;
+  if (nt > max_threads) nt = max_threads;
   if (fns.size() < 8) nt = 1;
   host_parallel(nt, [&](unsigned) {
     for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
@@ -388,9 +395,9 @@ static void prepend_done(std::vector<std::string>& done, std::vector<std::string
   done.clear();
 }
 
-void JsonPieces::prerender() {
+void JsonPieces::prerender(unsigned max_threads) {
   std::vector<std::string> out;
-  render_pieces(fns, out);
+  render_pieces(fns, out, max_threads);
   for (std::string& x : out) done.push_back(std::move(x));
 }
 

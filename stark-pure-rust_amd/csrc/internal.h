@@ -286,7 +286,8 @@ struct JsonPieces {
                 size_t depth);
   void render(std::string& o);
   void render(JsonText& o);  // pieces rendered and copied to their offsets on the host workers
-  void prerender();          // renders the pieces added so far now (e.g. while the GPU still works)
+  // renders the pieces added so far now (e.g. while the GPU still works), on up to max_threads host threads
+  void prerender(unsigned max_threads = 16);
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
 

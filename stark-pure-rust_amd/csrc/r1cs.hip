@@ -1147,7 +1147,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   {
     // The head renders on the side thread while this one waits for the FRI layers and gathers their
     // openings (for a small proof the FRI kernels finish before the head would be rendered).
-    HostTask head([&] { j.prerender(); });
+    HostTask head([&] { j.prerender(16); });
     const stark_status st = fri_finish(ctx, fri_pending.get(), extra, &fri);
     clk.mark("FRI wait + indices + gather");
     head.wait();

@@ -114,8 +114,8 @@ __global__ void slot_fill_kernel(FillArgs a) {
 }
 
 // comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels).  The
-// terms are loaded eight at a time ahead of their additions, so a long factor (hundreds of terms in
-// pedersen_test, a thousand in bits.r1cs) waits for one memory latency per eight terms, not per term.
+// terms are loaded sixteen at a time ahead of their additions, so a long factor (hundreds of terms in
+// pedersen_test, a thousand in bits.r1cs) waits for one memory latency per sixteen terms, not per term.
 __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
                                    fe* __restrict__ comp) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -124,7 +124,7 @@ __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n
   const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
   fe* c = comp + (uint64_t)f * a_len + b0;
   fe acc = fe_zero();
-  constexpr uint32_t kAhead = 8;
+  constexpr uint32_t kAhead = 16;
   for (uint32_t i = 0; i < n_coeff; i += kAhead) {
     fe v[kAhead];
 #pragma unroll

@@ -7,7 +7,9 @@
 // 80 spot-check positions).  It is taken from a prepared circuit
 // (circuit_build: slot layout, flags, permutation and those LDEs on the GPU);
 // the rest -- Merkle paths, the FRI layer checks and the 80 spot checks -- is
-// a few thousand hashes and products on the host.
+// a few thousand hashes and products on the host (a one-launch GPU path check
+// measured slower than the host pass), and the cold entry
+// points read the proof on a side thread while the circuit is built.
 //
 // Status: STARK_OK for a valid proof, STARK_ERR_CHECK where the reference
 // would fail an assert (an invalid proof), STARK_ERR_BAD_ARG for malformed
@@ -692,21 +694,32 @@ stark_status stark_verify_low_degree_proof(const uint8_t merkle_root[32], const 
   return verify_fri(merkle_root, F.from_canonical(root_of_unity), proof, max_deg_plus_1, exclude_multiples_of);
 }
 
+}  // extern "C"
+
+namespace stark {
+// The StarkProof JSON into pr; false where serde_json::from_reader fails (run.rs:579).
+static bool read_proof(const char* proof_json, size_t json_len, ProofIn& pr) {
+  PhaseClock clk("verify: read proof");
+  PreBranches pre;
+  pre_parse_branches(proof_json, json_len, pre);
+  clk.mark("openings parsed (parallel)");
+  Json j(proof_json, json_len, &pre);
+  j.stark_proof(pr);
+  clk.mark("StarkProof JSON parsed");
+  return j.ok;
+}
+}  // namespace stark
+
+extern "C" {
+
 stark_status stark_verify_r1cs_circuit(stark_ctx* ctx, const stark_r1cs_circuit* circuit,
                                        const uint8_t* public_wires, size_t n_public, const char* proof_json,
                                        size_t json_len) {
   if (!ctx || !circuit || circuit->ctx != ctx || !public_wires || !proof_json || n_public == 0)
     return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
-  PhaseClock clk("verify: read proof");
   ProofIn pr;
-  PreBranches pre;
-  pre_parse_branches(proof_json, json_len, pre);
-  clk.mark("openings parsed (parallel)");
-  Json j(proof_json, json_len, &pre);
-  j.stark_proof(pr);
-  if (!j.ok) return STARK_ERR_BAD_ARG;  // serde_json::from_reader fails (run.rs:579)
-  clk.mark("StarkProof JSON parsed");
+  if (!read_proof(proof_json, json_len, pr)) return STARK_ERR_BAD_ARG;
   return verify_r1cs(ctx, circuit->c, public_wires, n_public, pr);
 }
 
@@ -722,10 +735,18 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
   PhaseClock clk("verify: circuit");
-  stark_status st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
-  hipStreamSynchronize(ctx->stream);
-  clk.mark("circuit build");
-  if (st == STARK_OK) st = stark_verify_r1cs_circuit(ctx, &circ, public_wires, n_public, proof_json, json_len);
+  // The proof is read on the side thread while this one builds the circuit (mostly device work and
+  // its synchronisations): the two do not depend on each other.
+  ProofIn pr;
+  bool parsed = false;
+  stark_status st;
+  {
+    HostTask read([&] { parsed = read_proof(proof_json, json_len, pr); });
+    st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
+    clk.mark("circuit build (proof read beside it)");
+  }
+  if (st == STARK_OK && !parsed) st = STARK_ERR_BAD_ARG;  // serde_json::from_reader fails (run.rs:579)
+  if (st == STARK_OK) st = verify_r1cs(ctx, circ.c, public_wires, n_public, pr);
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
   return st;
