@@ -158,6 +158,46 @@ def test_device_trace_rejects_bad_inputs(ctx):
         prove_with_witness(ctx, bytes(r1), bytes(badw))
 
 
+def _record_offsets(r1: bytes):
+    """Byte offsets of every constraint record (36 B: wire id + 32-B coefficient) of a .r1cs v1 file, in
+    push order (constraint, factor, record), from its header and constraint section."""
+    import struct
+    n_c = struct.unpack_from("<I", r1, 4 * 4 + 8 + 4 + 32 + 4 * 4 + 8)[0]
+    pos = 4 * 4 + 8 + 4 + 32 + 4 * 4 + 8 + 4 + 4 + 8
+    offs = []
+    for _ in range(n_c):
+        for _f in range(3):
+            nc = struct.unpack_from("<I", r1, pos)[0]
+            pos += 4
+            offs += [pos + 36 * i for i in range(nc)]
+            pos += 36 * nc
+    return offs
+
+
+@pytest.mark.parametrize("name", ["compute", "pedersen_test", "poseidon3_test"])
+def test_device_trace_late_bad_wire_is_rejected(ctx, name):
+    """A wire id >= n_wires in the LAST record.  compute and pedersen_test use every public wire before it,
+    so the host scan finds their first uses, the device trace builder does not read back, and the prover
+    reports the device's flag at its first synchronisation; poseidon3_test first uses public wire 1 in that
+    very record, so the scan meets the bad id and the builder reads back as before.  Both: STARK_ERR_BAD_ARG
+    (3), and the context proves correctly afterwards."""
+    import hashlib
+    import struct
+    from stark_amd import StarkError
+    from stark_amd.r1cs import prove_with_witness
+    r1, wt = _read(name, "r1cs"), _read(name, "wtns")
+    n_wires = struct.unpack_from("<I", r1, 4 * 4 + 8 + 4 + 32)[0]
+    offs = _record_offsets(r1)
+    assert struct.unpack_from("<I", r1, offs[0])[0] < n_wires
+    bad = bytearray(r1)
+    struct.pack_into("<I", bad, offs[-1], n_wires + 5)
+    with pytest.raises(StarkError) as e:
+        prove_with_witness(ctx, bytes(bad), wt)
+    assert e.value.code == 3
+    js = prove_with_witness(ctx, r1, wt).to_json()
+    assert hashlib.sha256(js.encode()).hexdigest() == GOLDEN[name]["json_sha256"]
+
+
 @pytest.mark.parametrize("name", list(GOLDEN))
 def test_prepared_circuit_matches_golden(ctx, name):
     """R1csCircuit (circuit-only work and LDE columns prepared once) gives the golden proof, twice."""
