@@ -325,10 +325,11 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // bytes (r1cs.hip).
 // The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the
 // inverses of Zb2, Zb3 at the points rank + world j (8 x precision/world; K, F0-F2 and the
-// inverses as Montgomery images).  world = 1: the whole domain.
+// inverses as Montgomery images).  world = 1: the whole domain.  with_zb = false (the verifier,
+// which reads only the first six and evaluates Zb2 / Zb3 at its spot positions): 6 x P, no inverses.
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s);
+                         hipStream_t s, bool with_zb = true);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                     size_t os, const uint64_t* public_wires, size_t n_public,
@@ -349,6 +350,7 @@ struct PreparedCircuit {
   size_t os = 0, n_wires = 0, n_public = 0;
   uint32_t n_c = 0;
   uint32_t world = 1, rank = 0;  // the points rank + world j of the precision domain (distributed prover)
+  bool with_zb = true;           // false: lde holds K F0 F1 F2 IDX PIDX only (the verifier's cold build)
   uint64_t a_len = 0;
   std::vector<size_t> pfi;
   const uint32_t* base = nullptr;

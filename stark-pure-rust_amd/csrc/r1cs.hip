@@ -1188,7 +1188,7 @@ __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, 
 // are the device trace builder's circuit columns (os slots).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s) {
+                         hipStream_t s, bool with_zb) {
   const FieldHost& F = FieldHost::get();
   if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
     return STARK_ERR_BAD_ARG;
@@ -1208,7 +1208,7 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     if (public_first_indices[2 * i + 1] >= steps) return STARK_ERR_BAD_ARG;
   DevBuf& tmp = ctx->lde_tmp;  // 6 step columns, then Zb2 / Zb3 and the x_k (2 P + n_pfi)
   STARK_TRY(ensure_buf(ctx, tmp, (6 * steps + 2 * P + n_pfi + 1) * sizeof(fe)));
-  stark_status st = ensure_buf(ctx, out, 8 * P * sizeof(fe));
+  stark_status st = ensure_buf(ctx, out, (with_zb ? 8 : 6) * P * sizeof(fe));
   if (st == STARK_OK) {
     fe* raw = (fe*)tmp.ptr;
     hipMemsetAsync(raw, 0, 6 * steps * sizeof(fe), s);
@@ -1235,10 +1235,10 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     fe* zb = raw + 6 * steps;
     fe* d_xk = zb + 2 * P;
     const Mont mc = mont();
-    if (st == STARK_OK && n_pfi &&
+    if (st == STARK_OK && with_zb && n_pfi &&
         hipMemcpyAsync(d_xk, xk.data(), n_pfi * sizeof(fe), hipMemcpyHostToDevice, s) != hipSuccess)
       st = STARK_ERR_HIP;
-    if (st == STARK_OK) {
+    if (st == STARK_OK && with_zb) {
       hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                          (uint64_t)rank, log_g, (const fe*)d_xk, (uint32_t)n_pfi,
                          to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + P);
@@ -1247,7 +1247,8 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     if (st == STARK_OK) {  // K, F0-F2 and the Zb inverses as Montgomery images (ConstraintArgs::mont_cols)
       fe* o = (fe*)out.ptr;
       hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * P)), dim3(256), 0, s, o, 4 * P, mc.r2);
-      hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * P)), dim3(256), 0, s, o + 6 * P, 2 * P, mc.r2);
+      if (with_zb)
+        hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * P)), dim3(256), 0, s, o + 6 * P, 2 * P, mc.r2);
       if (hipGetLastError() != hipSuccess) st = STARK_ERR_HIP;
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;

@@ -602,7 +602,8 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   c.flags = flags;
   c.perm = (const uint64_t*)(A + o_perm);
   c.slot_wire = (const uint32_t*)(A + o_sw);
-  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s);
+  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s,
+                     c.with_zb);
 }
 
 // The witness of one proof: decode, then S and P from the circuit's slot wires.

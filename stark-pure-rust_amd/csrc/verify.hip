@@ -734,6 +734,7 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
   circ.ctx = ctx;
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
+  circ.c.with_zb = false;  // verify_r1cs evaluates Zb2 / Zb3 at its spot positions on the host
   PhaseClock clk("verify: circuit");
   // The proof is read on the side thread while this one builds the circuit (mostly device work and
   // its synchronisations): the two do not depend on each other.

@@ -1,5 +1,5 @@
 """A/B of the verifier (cold verify_with_wtns and prepared verify_circuit on pedersen_test) across library
-builds, one process per build:  python tools/time_verify_libs.py a.so b.so ... [--reps 30]"""
+builds, one process per build:  python tools/time_verify_libs.py a.so b.so ... [--reps 30] [--synth]"""
 import argparse
 import os
 import subprocess
@@ -31,6 +31,15 @@ def best(fn):
 cb, cm = best(lambda: verify_with_wtns(ctx, r1, wt, jb))
 pb, pm = best(lambda: verify_circuit(ctx, c, pub, jb))
 print(f"{os.path.basename(LIB)}: cold best {cb:.3f} median {cm:.3f} ms  prepared best {pb:.3f} median {pm:.3f} ms", flush=True)
+if SYNTH:
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth_r1cs
+    rs, ws = synth_r1cs.for_steps(20)
+    js = R1csCircuit(ctx, rs).prove(ws).to_json().encode()
+    assert verify_with_wtns(ctx, rs, ws, js)
+    REPS = 5
+    sb, sm = best(lambda: verify_with_wtns(ctx, rs, ws, js))
+    print(f"{os.path.basename(LIB)}: 2^20-step cold best {sb:.3f} median {sm:.3f} ms", flush=True)
 '''
 
 
@@ -38,9 +47,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--synth", action="store_true", help="also the cold verify of a synthetic 2^20-step proof")
     a = ap.parse_args()
     for lib in a.libs:
-        code = f"ROOT = {ROOT!r}\nLIB = {os.path.abspath(lib)!r}\nREPS = {a.reps}\n" + CHILD
+        code = f"ROOT = {ROOT!r}\nLIB = {os.path.abspath(lib)!r}\nREPS = {a.reps}\nSYNTH = {a.synth}\n" + CHILD
         subprocess.run([sys.executable, "-c", code], check=True)
 
 
