@@ -134,7 +134,9 @@ struct stark_ctx {
   // (log_steps, log_prec, log_world, rank) -> the extension of the index column IDX[i] = i
   // (prove.rs:160-163) at that rank's points: it depends on the trace length only, so every
   // proof of that size shares it (r1cs.hip ext_index_column).
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, stark::CacheBuf> ext_idx;
+  // Size-only columns of the r1cs prover (r1cs.hip ext_const_column), key (kind, log_steps, log_prec,
+  // log_g, rank, os): kind 0 = IDX's extension, 1 = F0's (1 on the first os rows), 2 = 1 / Zb3.
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint64_t>, stark::CacheBuf> ext_idx;
   // (root canonical limbs, log_n, rank) -> post[k] = root^(rank k), k < n / world: the one-exchange
   // distributed NTT's twiddle, applied in the rank's last local pass (dist.hip).
   std::map<std::tuple<uint64_t, uint64_t, uint64_t, uint64_t, uint32_t, uint32_t>, stark::CacheBuf> post_tw;
@@ -362,6 +364,8 @@ struct PreparedCircuit {
 stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c);
 // lagrange_interp (fri/src/poly_utils.rs:409-439): coefficients, low degree first (r1cs.hip).
 std::vector<HostFp> lagrange_interp(const std::vector<HostFp>& xs, const std::vector<HostFp>& ys);
+// mk_r1cs_proof with the flags as 3 x os bytes from a trace builder (calc_flags, run.rs:283-308):
+// flag0 must be 1 on every row (the prover then takes F0's shared extension instead of extending it).
 stark_status mk_r1cs_proof_bytes_flags(stark_ctx* ctx, const uint64_t* witness_trace,
                                       const uint64_t* computational_trace, size_t os, const uint64_t* public_wires,
                                       size_t n_public, const size_t* public_first_indices, size_t n_pfi,

@@ -255,6 +255,7 @@ struct PackArgs {
   uint64_t* perm;
   uint32_t* tr;         // the transcript, tr_words u32
   uint32_t tr_words;
+  uint32_t k_slot;      // K's raw slot: 0, or 1 when F0's extension is the shared one (F0 not written)
 };
 __global__ void r1cs_pack_kernel(PackArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,12 +264,13 @@ __global__ void r1cs_pack_kernel(PackArgs a) {
   const bool in = i < a.os;
 #pragma unroll
   for (int c = 0; c < 6; ++c) {
+    if (c == 1 && a.k_slot) continue;  // (uniform)
     fe v = fe_zero();
     if (in) {
       if (a.fb && c >= 1 && c <= 3) v = fe_from_u64(a.fb[(uint64_t)(c - 1) * a.os + i]);
       else v = fe_load(a.col[c] + i);
     }
-    fe_store(a.raw + (uint64_t)c * a.steps + i, v);
+    fe_store(a.raw + (uint64_t)(c == 0 ? a.k_slot : c) * a.steps + i, v);
     if (c == 4) fe_store(a.wcopy + i, v);
   }
   if (in) a.perm[i] = a.perm_in[i];
@@ -393,12 +395,13 @@ __global__ void r1cs_zb_kernel(const fe* __restrict__ lo, const fe* __restrict__
   fe acc = one_m;
   for (uint32_t k = 0; k < npub; ++k) acc = fe_mul(acc, fe_sub(x_m, xpub_m[k]));
   fe_store(zb2 + i, fe_mul(acc, unit));
-  fe_store(zb3 + i, fe_mul(fe_sub(x_m, xlast_m), unit));
+  if (zb3) fe_store(zb3 + i, fe_mul(fe_sub(x_m, xlast_m), unit));  // (null: 1 / Zb3 is the shared column)
 }
 
 struct ConstraintArgs {
   const fe* col[9];      // K F0 F1 F2 S P IDX PIDX A, precision (local points) each
-  const fe* inv_zb;      // inv Zb2 (precision) then inv Zb3 (precision)
+  const fe* inv_zb;      // inv Zb2 (precision)
+  const fe* inv_zb3;     // inv Zb3 (precision): inv_zb + precision, or the shared column
   const fe* interp2;     // canonical coefficients, low degree first
   const fe* interp3;
   const fe* lo;          // g2 tables
@@ -473,7 +476,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   for (uint32_t k = a.n2; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
   fe i3 = fe_zero();
   for (uint32_t k = a.n3; k-- > 0;) i3 = fe_add(fe_mul(i3, x_m), a.interp3[k]);
-  const fe izb2 = fe_load(a.inv_zb + i), izb3 = fe_load(a.inv_zb + n + i);
+  const fe izb2 = fe_load(a.inv_zb + i), izb3 = fe_load(a.inv_zb3 + i);
   const fe e2 = fe_sub(s, i2), e3 = fe_sub(av, i3);
   if (fe_is_zero(izb2) && !fe_is_zero(e2)) atomicOr(a.err, 2);
   if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
@@ -734,19 +737,29 @@ static stark_status lde(stark_ctx* ctx, fe* coef, uint32_t batch, fe* out, uint3
   return coset_lde(ctx, coef, batch, out, log_steps, log_prec, 0, 0, tw_g1_inv, tw_g2, tw_g2, s);
 }
 
-__global__ void iota_kernel(fe* __restrict__ out, uint64_t n) {
+// tag 0: IDX[i] = i; tag > 0: F0[i] = 1 for i < tag (calc_flags' flag0, run.rs:283-308), 0 after.
+__global__ void const_column_kernel(fe* __restrict__ out, uint64_t n, uint64_t tag) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) fe_store(out + i, fe_from_u64(i));
+  if (i < n) fe_store(out + i, fe_from_u64(tag ? (i < tag ? 1 : 0) : i));
 }
 
-// ext_indices (prove.rs:160-163): the extension of IDX[i] = i over the rank's points (coset_lde with
-// log_g, r; the whole domain for log_g = r = 0).  It depends on the trace length only, so it is
-// computed on a context's first proof of that size and shared by every later one.  Call it before
-// the proof enqueues work on `s`: a first call synchronises s once.
-static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t log_g,
-                                     uint32_t r, const Twiddles& tw_g1_inv, const Twiddles& tw_g2,
-                                     const Twiddles& tw_h, hipStream_t s, const fe** out) {
-  const auto key = std::make_tuple(log_steps, log_prec, log_g, r);
+// Columns of a proof that depend on its size only, over the rank's points r + 2^log_g j (the whole
+// domain for log_g = r = 0); each is computed on a context's first proof of that size and shared by
+// every later one:
+//   kExtIdx: ext_indices (prove.rs:160-163), the extension of IDX[i] = i (coset_lde with log_g, r);
+//   kExtF0:  the extension of F0, which calc_flags (run.rs:283-308) sets to 1 on each of the os trace
+//            rows (zero-padded to steps);
+//   kInvZb3: 1 / Zb3 = 1 / (x - x_last) (utils.rs:466-474; x_last = g2^((steps - 1) skips) depends on
+//            the size alone), 0 at x_last as multi_inv gives it, canonical.
+// Call before the proof enqueues work on `s`: a first call synchronises s.  An IDX extension larger
+// than the cache cap lives in a per-context buffer for this proof only; the other two are not built
+// when they cannot be cached (*out = nullptr: the caller computes them as part of the proof).
+enum : uint32_t { kExtIdx = 0, kExtF0 = 1, kInvZb3 = 2 };
+static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os, uint32_t log_steps,
+                                     uint32_t log_prec, uint32_t log_g, uint32_t r, const Twiddles& tw_g1_inv,
+                                     const Twiddles& tw_g2, const Twiddles& tw_h, hipStream_t s, const fe** out) {
+  const uint64_t tag = kind == kExtF0 ? os : 0;
+  const auto key = std::make_tuple(kind, log_steps, log_prec, log_g, r, tag);
   auto it = ctx->ext_idx.find(key);
   if (it != ctx->ext_idx.end()) {
     it->second.used = ++ctx->cache_clock;
@@ -754,13 +767,22 @@ static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_
     return STARK_OK;
   }
   const uint64_t steps = (uint64_t)1 << log_steps, P = (uint64_t)1 << (log_prec - log_g);
-  // Counted in the context's capped cache (stark_ctx_set_cache_limit).  An extension larger than the
-  // cap lives in a per-context buffer for this proof only and is recomputed by the next one.
+  // Counted in the context's capped cache (stark_ctx_set_cache_limit).
   const bool cached = cache_reserve(ctx, P * sizeof(fe), true);
   void *col = nullptr, *coef = nullptr;
   if (cached) {
-    if (hipMalloc(&col, P * sizeof(fe)) != hipSuccess) return STARK_ERR_OOM;
+    if (hipMalloc(&col, P * sizeof(fe)) != hipSuccess) {
+      hipGetLastError();
+      if (kind != kExtIdx) {
+        *out = nullptr;
+        return STARK_OK;
+      }
+      return STARK_ERR_OOM;
+    }
     ctx->ext_idx[key] = CacheBuf{col, P * sizeof(fe), ++ctx->cache_clock};  // counted while it is built
+  } else if (kind != kExtIdx) {
+    *out = nullptr;
+    return STARK_OK;
   } else {
     STARK_TRY(ensure_buf(ctx, ctx->ext_idx_tmp, P * sizeof(fe)));
     col = ctx->ext_idx_tmp.ptr;
@@ -771,14 +793,29 @@ static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_
       hipFree(col);
     }
   };
-  if (hipMalloc(&coef, steps * sizeof(fe)) != hipSuccess) {
+  const uint64_t tmp_n = kind == kInvZb3 ? 2 * P : steps;
+  if (hipMalloc(&coef, tmp_n * sizeof(fe)) != hipSuccess) {
+    hipGetLastError();
     drop();
     return STARK_ERR_OOM;
   }
-  hipLaunchKernelGGL(iota_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (fe*)coef, steps);
-  stark_status st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
-  if (st == STARK_OK)
-    st = coset_lde(ctx, (fe*)coef, 1, (fe*)col, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s);
+  stark_status st = STARK_OK;
+  if (kind == kInvZb3) {  // r1cs_zb_kernel with no public points: Zb2 = 1 (unused), Zb3 in the second half
+    const FieldHost& F = FieldHost::get();
+    const Mont mc = mont();
+    const uint64_t prec = (uint64_t)1 << log_prec, skips = prec >> log_steps;
+    fe* z = (fe*)coef;
+    hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, P,
+                       (uint64_t)r, log_g, (const fe*)nullptr, 0u, to_dev(F.pow_u64(tw_g2.root, prec - skips)),
+                       mc.unit, mc.one, z, z + P);
+    st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
+    if (st == STARK_OK) st = multi_inv_device(ctx, z + P, (fe*)col, P, s);
+  } else {
+    hipLaunchKernelGGL(const_column_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (fe*)coef, steps, tag);
+    st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
+    if (st == STARK_OK)
+      st = coset_lde(ctx, (fe*)coef, 1, (fe*)col, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s);
+  }
   if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
   hipFree(coef);
   if (st != STARK_OK) {
@@ -787,6 +824,12 @@ static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_
   }
   *out = (const fe*)col;
   return STARK_OK;
+}
+
+static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t log_g,
+                                     uint32_t r, const Twiddles& tw_g1_inv, const Twiddles& tw_g2,
+                                     const Twiddles& tw_h, hipStream_t s, const fe** out) {
+  return ext_const_column(ctx, kExtIdx, 0, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s, out);
 }
 
 // The proof's roots (prove.rs:71-94): g2 = 7^((p-1)/precision), g1 = g2^skips = xs[skips], and
@@ -888,7 +931,21 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   const Twiddles* tw1i = roots.tw1i;
   const Mont mc = mont();
   const fe* idx_ext = nullptr;  // the shared extension of IDX (prepared circuits carry their own)
-  if (!pre) STARK_TRY(ext_index_column(ctx, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &idx_ext));
+  // F0 is 1 on the os trace rows whenever the flags are the trace builder's (flag bytes, calc_flags
+  // run.rs:283-308), so its extension is shared too and only K F1 F2 S P PIDX are extended here.
+  // 1 / Zb3 is shared likewise, so the proof's batch inverse covers Zb2 alone.
+  // (Each later reservation may evict an earlier one: looked up again after the last.)
+  const fe *f0_ext = nullptr, *izb3 = nullptr;
+  if (!pre) {
+    STARK_TRY(ext_const_column(ctx, kInvZb3, 0, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &izb3));
+    if (flag_bytes)
+      STARK_TRY(ext_const_column(ctx, kExtF0, os, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &f0_ext));
+    STARK_TRY(ext_index_column(ctx, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &idx_ext));
+    if (f0_ext && !ctx->ext_idx.count(std::make_tuple(kExtF0, log_steps, log_prec, 0u, 0u, (uint64_t)os)))
+      f0_ext = nullptr;
+    if (izb3 && !ctx->ext_idx.count(std::make_tuple(kInvZb3, log_steps, log_prec, 0u, 0u, (uint64_t)0)))
+      izb3 = nullptr;
+  }
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
   uint64_t* perm;
@@ -937,6 +994,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     static_assert(sizeof(Transcript) % 4 == 0, "transcript words");
     pa.tr = (uint32_t*)d_tr;
     pa.tr_words = (uint32_t)(sizeof(Transcript) / 4);
+    pa.k_slot = f0_ext ? 1 : 0;
     hipLaunchKernelGGL(r1cs_pack_kernel, dim3(blocks_for(std::max<uint64_t>(steps, pa.tr_words))), dim3(256), 0, s,
                        pa);
     STARK_HIP(ctx, hipGetLastError());
@@ -955,6 +1013,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   }
   static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t is 64-bit");
   if (!pack) {
+    if (f0_ext)  // K into F0's slot: the six extended columns are contiguous from slot 1
+      STARK_HIP(ctx, hipMemcpyAsync(raw + steps, raw, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
     STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
     STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
     STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
@@ -974,6 +1034,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
   if (pre)  // S and P only: K, the flags, IDX and PIDX are the circuit's
     STARK_TRY(lde(ctx, raw + 4 * steps, 2, cols + 4 * prec, log_steps, log_prec, *tw1i, *tw2, s));
+  else if (f0_ext)  // K (in F0's slot) F1 F2 S P PIDX
+    STARK_TRY(lde(ctx, raw + steps, 6, cols + prec, log_steps, log_prec, *tw1i, *tw2, s));
   else  // K F0 F1 F2 S P PIDX
     STARK_TRY(lde(ctx, raw, 7, cols, log_steps, log_prec, *tw1i, *tw2, s));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(acc_tree),
@@ -998,9 +1060,9 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   if (!pre) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                        (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
-                       zb, zb + prec);
+                       zb, izb3 ? nullptr : zb + prec);
     STARK_HIP(ctx, hipGetLastError());
-    STARK_TRY(multi_inv_up(ctx, zb, inv_zb, 2 * prec, s, ctx->io2, top_z, inv_z));
+    STARK_TRY(multi_inv_up(ctx, zb, inv_zb, izb3 ? prec : 2 * prec, s, ctx->io2, top_z, inv_z));
   }
   STARK_TRY(multi_inv_up(ctx, dnm_c, inv_dnm, steps, s, ctx->inv_tmp, top_d, inv_d));
   STARK_HIP(ctx, hipStreamSynchronize(s));
@@ -1019,9 +1081,14 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.col[6] = ext_idx;
   ca.col[8] = cols + 7 * prec;  // A
   ca.col[7] = ext_pidx;
+  if (f0_ext) {
+    ca.col[0] = cols + prec;  // K
+    ca.col[1] = f0_ext;
+  }
   if (pre)
     for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * prec;
   ca.inv_zb = pre ? pre + 6 * prec : inv_zb;
+  ca.inv_zb3 = izb3 ? izb3 : ca.inv_zb + prec;
   ca.interp2 = consts + n_pfi;
   ca.interp3 = consts + 2 * n_pfi;
   ca.lo = tw2->d_lo;
@@ -1217,11 +1284,27 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                        raw + steps);
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
-    // K F0 F1 F2, then PIDX; IDX is the shared extension (ext_index_column), copied into its slot.
-    const fe* idx_ext = nullptr;
-    st = ext_index_column(ctx, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext);
+    // K F0 F1 F2, then PIDX; IDX and F0 (1 on the os rows: the flags are circuit_build's calc_flags)
+    // are the shared extensions (ext_const_column), copied into their slots.  With F0's: K is moved
+    // over F0's step column, K F1 F2 are extended into slots 1-3, and K then copied to slot 0.
+    const fe *idx_ext = nullptr, *f0_ext = nullptr;
+    st = ext_const_column(ctx, kExtF0, os, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s, &f0_ext);
     if (st == STARK_OK)
-      st = coset_lde(ctx, raw, 4, (fe*)out.ptr, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+      st = ext_index_column(ctx, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext);
+    if (f0_ext && !ctx->ext_idx.count(std::make_tuple(kExtF0, log_steps, log_prec, log_g, rank, (uint64_t)os)))
+      f0_ext = nullptr;  // evicted by IDX's reservation
+    fe* const o = (fe*)out.ptr;
+    if (st == STARK_OK && f0_ext) {
+      if (hipMemcpyAsync(raw + steps, raw, steps * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess)
+        st = STARK_ERR_HIP;
+      if (st == STARK_OK)
+        st = coset_lde(ctx, raw + steps, 3, o + P, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+      if (st == STARK_OK && (hipMemcpyAsync(o, o + P, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                             hipMemcpyAsync(o + P, f0_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess))
+        st = STARK_ERR_HIP;
+    } else if (st == STARK_OK) {
+      st = coset_lde(ctx, raw, 4, o, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+    }
     if (st == STARK_OK)
       st = coset_lde(ctx, raw + 5 * steps, 1, (fe*)out.ptr + 5 * P, log_steps, log_prec, log_g, rank, *tw1i, *tw2,
                      *twh, s);
@@ -1245,7 +1328,6 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
       st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * P, 2 * P, s);
     }
     if (st == STARK_OK) {  // K, F0-F2 and the Zb inverses as Montgomery images (ConstraintArgs::mont_cols)
-      fe* o = (fe*)out.ptr;
       hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * P)), dim3(256), 0, s, o, 4 * P, mc.r2);
       if (with_zb)
         hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * P)), dim3(256), 0, s, o + 6 * P, 2 * P, mc.r2);
@@ -1461,6 +1543,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * P;
   ca.col[8] = cols + 7 * P;  // A
   ca.inv_zb = pre ? pre + 6 * P : inv_zb;
+  ca.inv_zb3 = ca.inv_zb + P;
   ca.col[6] = pre ? pre + 4 * P : idx_ext;
   ca.col[7] = pre ? pre + 5 * P : cols + 6 * P;
   if (pre)

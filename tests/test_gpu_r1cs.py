@@ -239,3 +239,34 @@ def test_prepared_circuit_rejects_bad_inputs(ctx):
     with pytest.raises(StarkError) as e:
         c.prove(bytes(bad))
     assert e.value.code == 8
+
+
+def test_shared_f0_extension_under_cache_caps():
+    """F0 is 1 on every trace row (calc_flags, run.rs:283-308) and Zb3 = x - x_last depends on the size
+    alone, so the cold prover shares F0's extension and 1 / Zb3 per size like IDX's extension
+    (csrc/r1cs.hip ext_const_column).  Bit-exact under the default cap (all three cached), under a cap of 0
+    (F0 extended with the other columns, Zb3 inverted with Zb2, IDX in a per-proof buffer) and under a cap
+    of one column (each reservation evicts the previous column: the prover falls back for F0 and 1 / Zb3).
+    compute's precision is below the full-twiddle-table sizes, so the cache holds only these columns."""
+    import stark_amd as S
+    from stark_amd.r1cs import prove_with_witness
+    r1, wt = _read("compute", "r1cs"), _read("compute", "wtns")
+    want = GOLDEN["compute"]["json_sha256"]
+    digest = lambda c: hashlib.sha256(prove_with_witness(c, r1, wt).to_json().encode()).hexdigest()  # noqa: E731
+    col = 128 * 32  # one extension: os = 15 -> 16 steps -> precision 128
+    c = S.Context(0)
+    try:
+        assert digest(c) == want
+        assert c.memory()["cached"] >= 3 * col  # IDX's and F0's extensions, 1 / Zb3
+        assert digest(c) == want  # from the cached extensions
+    finally:
+        c.close()
+    for cap in (0, col):
+        c = S.Context(0)
+        try:
+            c.set_cache_limit(cap)
+            assert digest(c) == want, cap
+            assert digest(c) == want, cap
+            assert c.memory()["cached"] <= cap
+        finally:
+            c.close()
