@@ -1460,7 +1460,18 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   const Mont mc = mont();
   const fe* idx_ext = nullptr;  // this rank's share of the extension of IDX (shared across proofs)
-  if (!pre) STARK_TRY(ext_index_column(ctx, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext));
+  // ... and of F0's extension (flags from a trace builder) and 1 / Zb3, as in prove_r1cs.
+  const fe *f0_ext = nullptr, *izb3 = nullptr;
+  if (!pre) {
+    STARK_TRY(ext_const_column(ctx, kInvZb3, 0, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &izb3));
+    if (flag_bytes)
+      STARK_TRY(ext_const_column(ctx, kExtF0, os, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &f0_ext));
+    STARK_TRY(ext_index_column(ctx, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext));
+    if (f0_ext && !ctx->ext_idx.count(std::make_tuple(kExtF0, log_steps, log_prec, d.log_g, rank, (uint64_t)os)))
+      f0_ext = nullptr;
+    if (izb3 && !ctx->ext_idx.count(std::make_tuple(kInvZb3, log_steps, log_prec, d.log_g, rank, (uint64_t)0)))
+      izb3 = nullptr;
+  }
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts;
   uint64_t* perm;
@@ -1503,6 +1514,8 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
                        (uint64_t)os, steps, raw + steps);
     STARK_HIP(ctx, hipGetLastError());
   }
+  if (f0_ext)  // K into F0's slot: the six extended columns are contiguous from slot 1
+    STARK_HIP(ctx, hipMemcpyAsync(raw + steps, raw, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   STARK_HIP(ctx, hipMemcpyAsync(perm, permuted_indices, os * sizeof(uint64_t), hipMemcpyDefault, s));
   STARK_HIP(ctx, hipMemcpyAsync(wcopy, raw + 4 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(d.d_tr, 0, sizeof(Transcript), s));
@@ -1515,6 +1528,8 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_TRY(merkle_build(ctx, d.acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
   if (pre)
     STARK_TRY(lde_coset(d, raw + 4 * steps, 2, cols + 4 * P, *tw1i, *tw2, *twh));
+  else if (f0_ext)  // K (in F0's slot) F1 F2 S P PIDX
+    STARK_TRY(lde_coset(d, raw + steps, 6, cols + P, *tw1i, *tw2, *twh));
   else  // K F0 F1 F2 S P PIDX
     STARK_TRY(lde_coset(d, raw, 7, cols, *tw1i, *tw2, *twh));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
@@ -1535,17 +1550,21 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   if (!pre) {  // Zb2 / Zb3 at this rank's points and their inverses
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                        (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
-                       zb, zb + P);
+                       zb, izb3 ? nullptr : zb + P);
     STARK_HIP(ctx, hipGetLastError());
-    STARK_TRY(multi_inv_device(ctx, zb, inv_zb, 2 * P, s));
+    STARK_TRY(multi_inv_device(ctx, zb, inv_zb, izb3 ? P : 2 * P, s));
   }
   ConstraintArgs ca;
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * P;
   ca.col[8] = cols + 7 * P;  // A
   ca.inv_zb = pre ? pre + 6 * P : inv_zb;
-  ca.inv_zb3 = ca.inv_zb + P;
+  ca.inv_zb3 = izb3 ? izb3 : ca.inv_zb + P;
   ca.col[6] = pre ? pre + 4 * P : idx_ext;
   ca.col[7] = pre ? pre + 5 * P : cols + 6 * P;
+  if (f0_ext) {
+    ca.col[0] = cols + P;  // K
+    ca.col[1] = f0_ext;
+  }
   if (pre)
     for (int c = 0; c < 4; ++c) ca.col[c] = pre + (size_t)c * P;
   ca.interp2 = consts + n_pfi;
