@@ -63,6 +63,7 @@ constexpr uint32_t kScanBlock = 1024;   // elements per workgroup in the product
 // Montgomery image of R (montmul(x, r2) = Montgomery image of x) and of 1.
 struct Mont {
   fe r2, one, unit;  // unit = canonical 1 (montmul(x_m, unit) = canonical x)
+  fe rinv;           // R^-1 as a canonical value (montmul(x_m, rinv) = x R^-1)
 };
 
 static Mont mont() {
@@ -73,6 +74,8 @@ static Mont mont() {
   m.one = to_dev(one);
   m.unit = fe_zero_host();
   m.unit.w[0] = 1;
+  const HostFp rv = F.from_canonical(one.v);  // the value R
+  m.rinv = to_dev(F.inv(F.mul(rv, rv)));      // the value R^-2, whose Montgomery image is R^-1
   return m;
 }
 
@@ -382,7 +385,8 @@ __global__ void r1cs_a_mini_kernel(const fe* __restrict__ nmr_m, const fe* __res
 }
 
 // Zb2(x) = prod_k (x - x_k) (utils.rs:438-455) and Zb3(x) = x - x_last
-// (utils.rs:466-474), canonical, for the batch inverse.
+// (utils.rs:466-474) for the batch inverse, each as Zb R^-1 (unit = R^-1, Mont::rinv): their
+// inverses are then the Montgomery images of 1 / Zb, which the constraint kernel multiplies exactly.
 // Local point i is the global evaluation point g_add + (i << log_g) (a residue
 // class of the precision domain on a distributed prover; g_add = log_g = 0 on one GPU).
 __global__ void r1cs_zb_kernel(const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb, uint64_t prec,
@@ -416,12 +420,11 @@ struct ConstraintArgs {
   uint32_t log_g;
   uint32_t log_prec, kb, n2, n3;
   const Transcript* tr;  // r0, r1, r2 (device transcript)
-  fe mr2;
   // inv(Z) at the points t = i mod 8 (multi_inv of Z, prove.rs:203; 0 for t = 0) as the
   // Montgomery images of inv(Z) R^k, k = 0, 1, 2: the constraint kernel forms some Q's scaled by
   // R^-k (one product fewer per conversion it skips) and undoes the scale in D = Q inv(Z).
   fe invz_m[3][8];
-  int mont_cols;         // K, F0-F2 and inv Zb2/Zb3 are Montgomery images (prepared circuits)
+  int mont_cols;         // K, F0-F2 are Montgomery images (prepared circuits); inv Zb2/Zb3 always are
 };
 
 // Q1/Q2/Q3 (utils.rs:181-248, 344-376) -> D1..D3 (utils.rs:379-418), I2/I3
@@ -480,8 +483,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe e2 = fe_sub(s, i2), e3 = fe_sub(av, i3);
   if (fe_is_zero(izb2) && !fe_is_zero(e2)) atomicOr(a.err, 2);
   if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
-  const fe b2 = mc ? fe_mul(e2, izb2) : fe_mul(fe_mul(e2, a.mr2), izb2);
-  const fe b3 = mc ? fe_mul(e3, izb3) : fe_mul(fe_mul(e3, a.mr2), izb3);
+  const fe b2 = fe_mul(e2, izb2), b3 = fe_mul(e3, izb3);  // (Montgomery images of the inverses: exact)
   // Row i = P|A|S|D1|D2|D3|B2|B3: contiguous (256 B), or column c at rows + c * plane + i
   const uint64_t cs = a.plane ? a.plane : 1;
   fe* row = a.plane ? a.rows + i : a.rows + 8 * i;
@@ -750,7 +752,7 @@ __global__ void const_column_kernel(fe* __restrict__ out, uint64_t n, uint64_t t
 //   kExtF0:  the extension of F0, which calc_flags (run.rs:283-308) sets to 1 on each of the os trace
 //            rows (zero-padded to steps);
 //   kInvZb3: 1 / Zb3 = 1 / (x - x_last) (utils.rs:466-474; x_last = g2^((steps - 1) skips) depends on
-//            the size alone), 0 at x_last as multi_inv gives it, canonical.
+//            the size alone), 0 at x_last as multi_inv gives it, as Montgomery images (r1cs_zb_kernel).
 // Call before the proof enqueues work on `s`: a first call synchronises s.  An IDX extension larger
 // than the cache cap lives in a per-context buffer for this proof only; the other two are not built
 // when they cannot be cached (*out = nullptr: the caller computes them as part of the proof).
@@ -807,7 +809,7 @@ static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os,
     fe* z = (fe*)coef;
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, P,
                        (uint64_t)r, log_g, (const fe*)nullptr, 0u, to_dev(F.pow_u64(tw_g2.root, prec - skips)),
-                       mc.unit, mc.one, z, z + P);
+                       mc.rinv, mc.one, z, z + P);
     st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
     if (st == STARK_OK) st = multi_inv_device(ctx, z + P, (fe*)col, P, s);
   } else {
@@ -1059,7 +1061,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   if (!top_d || !top_z) return STARK_ERR_OOM;
   if (!pre) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
-                       (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
+                       (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
                        zb, izb3 ? nullptr : zb + prec);
     STARK_HIP(ctx, hipGetLastError());
     STARK_TRY(multi_inv_up(ctx, zb, inv_zb, izb3 ? prec : 2 * prec, s, ctx->io2, top_z, inv_z));
@@ -1107,7 +1109,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.n2 = (uint32_t)n_pfi;
   ca.n3 = 1;
   ca.tr = d_tr;
-  ca.mr2 = mc.r2;
   set_inv_z(ca, g2, steps);
   ca.mont_cols = pre ? 1 : 0;
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
@@ -1324,13 +1325,11 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     if (st == STARK_OK && with_zb) {
       hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                          (uint64_t)rank, log_g, (const fe*)d_xk, (uint32_t)n_pfi,
-                         to_dev(F.pow_u64(g2, prec - skips)), mc.unit, mc.one, zb, zb + P);
+                         to_dev(F.pow_u64(g2, prec - skips)), mc.rinv, mc.one, zb, zb + P);
       st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * P, 2 * P, s);
     }
-    if (st == STARK_OK) {  // K, F0-F2 and the Zb inverses as Montgomery images (ConstraintArgs::mont_cols)
+    if (st == STARK_OK) {  // K, F0-F2 as Montgomery images (ConstraintArgs::mont_cols; the Zb inverses are)
       hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * P)), dim3(256), 0, s, o, 4 * P, mc.r2);
-      if (with_zb)
-        hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(2 * P)), dim3(256), 0, s, o + 6 * P, 2 * P, mc.r2);
       if (hipGetLastError() != hipSuccess) st = STARK_ERR_HIP;
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
@@ -1549,7 +1548,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_TRY(lde_coset(d, raw, 1, cols + 7 * P, *tw1i, *tw2, *twh));  // A in slot 7
   if (!pre) {  // Zb2 / Zb3 at this rank's points and their inverses
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
-                       (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.unit, mc.one,
+                       (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
                        zb, izb3 ? nullptr : zb + P);
     STARK_HIP(ctx, hipGetLastError());
     STARK_TRY(multi_inv_device(ctx, zb, inv_zb, izb3 ? P : 2 * P, s));
@@ -1585,7 +1584,6 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   ca.n2 = (uint32_t)n_pfi;
   ca.n3 = 1;
   ca.tr = d.d_tr;
-  ca.mr2 = mc.r2;
   set_inv_z(ca, g2, steps);
   ca.mont_cols = pre ? 1 : 0;
   {
