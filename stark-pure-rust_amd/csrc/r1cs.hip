@@ -406,6 +406,12 @@ struct ConstraintArgs {
   const fe* col[9];      // K F0 F1 F2 S P IDX PIDX A, precision (local points) each
   const fe* inv_zb;      // inv Zb2 (precision)
   const fe* inv_zb3;     // inv Zb3 (precision): inv_zb + precision, or the shared column
+  // tinv != null: inv Zb2 by partial fractions instead of inv_zb, sum_k pf_coef[k] tinv[i - pf_shift[k]]
+  // over the shared table tinv[m] = 1 / (x_m - 1) (kInvXm1; zb2_partial_fractions)
+  const fe* tinv;
+  uint32_t n_pf;
+  uint64_t pf_shift[8];
+  fe pf_coef[8];
   const fe* interp2;     // canonical coefficients, low degree first
   const fe* interp3;
   const fe* lo;          // g2 tables
@@ -479,7 +485,20 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   for (uint32_t k = a.n2; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
   fe i3 = fe_zero();
   for (uint32_t k = a.n3; k-- > 0;) i3 = fe_add(fe_mul(i3, x_m), a.interp3[k]);
-  const fe izb2 = fe_load(a.inv_zb + i), izb3 = fe_load(a.inv_zb3 + i);
+  fe izb2;
+  if (a.tinv) {  // (uniform)
+    izb2 = fe_zero();
+    bool root = false;  // x = x_k: Zb2 = 0, whose batch inverse is 0
+    for (uint32_t k = 0; k < a.n_pf; ++k) {
+      const uint64_t m = (i + n - a.pf_shift[k]) & mask;
+      root = root || (m == 0 && a.g_add == 0);
+      izb2 = fe_add(izb2, fe_mul(a.pf_coef[k], fe_load(a.tinv + m)));
+    }
+    if (root) izb2 = fe_zero();
+  } else {
+    izb2 = fe_load(a.inv_zb + i);
+  }
+  const fe izb3 = fe_load(a.inv_zb3 + i);
   const fe e2 = fe_sub(s, i2), e3 = fe_sub(av, i3);
   if (fe_is_zero(izb2) && !fe_is_zero(e2)) atomicOr(a.err, 2);
   if (fe_is_zero(izb3) && !fe_is_zero(e3)) atomicOr(a.err, 4);
@@ -752,11 +771,12 @@ __global__ void const_column_kernel(fe* __restrict__ out, uint64_t n, uint64_t t
 //   kExtF0:  the extension of F0, which calc_flags (run.rs:283-308) sets to 1 on each of the os trace
 //            rows (zero-padded to steps);
 //   kInvZb3: 1 / Zb3 = 1 / (x - x_last) (utils.rs:466-474; x_last = g2^((steps - 1) skips) depends on
-//            the size alone), 0 at x_last as multi_inv gives it, as Montgomery images (r1cs_zb_kernel).
+//            the size alone), 0 at x_last as multi_inv gives it, as Montgomery images (r1cs_zb_kernel);
+//   kInvXm1: 1 / (x - 1), the same way (0 at x = 1): the table of 1 / Zb2's partial fractions.
 // Call before the proof enqueues work on `s`: a first call synchronises s.  An IDX extension larger
-// than the cache cap lives in a per-context buffer for this proof only; the other two are not built
+// than the cache cap lives in a per-context buffer for this proof only; the others are not built
 // when they cannot be cached (*out = nullptr: the caller computes them as part of the proof).
-enum : uint32_t { kExtIdx = 0, kExtF0 = 1, kInvZb3 = 2 };
+enum : uint32_t { kExtIdx = 0, kExtF0 = 1, kInvZb3 = 2, kInvXm1 = 3 };
 static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os, uint32_t log_steps,
                                      uint32_t log_prec, uint32_t log_g, uint32_t r, const Twiddles& tw_g1_inv,
                                      const Twiddles& tw_g2, const Twiddles& tw_h, hipStream_t s, const fe** out) {
@@ -795,21 +815,22 @@ static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os,
       hipFree(col);
     }
   };
-  const uint64_t tmp_n = kind == kInvZb3 ? 2 * P : steps;
+  const bool inv = kind == kInvZb3 || kind == kInvXm1;
+  const uint64_t tmp_n = inv ? 2 * P : steps;
   if (hipMalloc(&coef, tmp_n * sizeof(fe)) != hipSuccess) {
     hipGetLastError();
     drop();
     return STARK_ERR_OOM;
   }
   stark_status st = STARK_OK;
-  if (kind == kInvZb3) {  // r1cs_zb_kernel with no public points: Zb2 = 1 (unused), Zb3 in the second half
+  if (inv) {  // r1cs_zb_kernel with no public points: Zb2 = 1 (unused), x - c in the second half
     const FieldHost& F = FieldHost::get();
     const Mont mc = mont();
     const uint64_t prec = (uint64_t)1 << log_prec, skips = prec >> log_steps;
+    const fe c = kind == kInvZb3 ? to_dev(F.pow_u64(tw_g2.root, prec - skips)) : mc.one;
     fe* z = (fe*)coef;
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw_g2.d_lo, tw_g2.d_hi, tw_g2.kb, P,
-                       (uint64_t)r, log_g, (const fe*)nullptr, 0u, to_dev(F.pow_u64(tw_g2.root, prec - skips)),
-                       mc.rinv, mc.one, z, z + P);
+                       (uint64_t)r, log_g, (const fe*)nullptr, 0u, c, mc.rinv, mc.one, z, z + P);
     st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
     if (st == STARK_OK) st = multi_inv_device(ctx, z + P, (fe*)col, P, s);
   } else {
@@ -826,6 +847,60 @@ static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os,
   }
   *out = (const fe*)col;
   return STARK_OK;
+}
+
+// The size-only columns of one proof (ext_const_column), taken in one place: every later reservation
+// may evict an earlier column, so each is looked up again once all are taken (IDX last: its pointer is
+// always valid).  want_f0: the flags are a trace builder's (F0 = 1 on the os rows).
+struct SharedCols {
+  const fe *idx = nullptr, *f0 = nullptr, *izb3 = nullptr, *tinv = nullptr;
+};
+static stark_status shared_columns(stark_ctx* ctx, bool want_f0, uint64_t os, uint32_t log_steps, uint32_t log_prec,
+                                   uint32_t log_g, uint32_t r, const Twiddles& tw_g1_inv, const Twiddles& tw_g2,
+                                   const Twiddles& tw_h, hipStream_t s, SharedCols& o) {
+  STARK_TRY(ext_const_column(ctx, kInvZb3, 0, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s, &o.izb3));
+  STARK_TRY(ext_const_column(ctx, kInvXm1, 0, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s, &o.tinv));
+  if (want_f0)
+    STARK_TRY(ext_const_column(ctx, kExtF0, os, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s, &o.f0));
+  STARK_TRY(ext_const_column(ctx, kExtIdx, 0, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s, &o.idx));
+  auto live = [&](uint32_t kind, uint64_t tag) {
+    return ctx->ext_idx.count(std::make_tuple(kind, log_steps, log_prec, log_g, r, tag)) != 0;
+  };
+  if (o.izb3 && !live(kInvZb3, 0)) o.izb3 = nullptr;
+  if (o.tinv && !live(kInvXm1, 0)) o.tinv = nullptr;
+  if (o.f0 && !live(kExtF0, os)) o.f0 = nullptr;
+  return STARK_OK;
+}
+
+// 1 / Zb2 = 1 / prod_k (x - x_k) (utils.rs:438-455) by partial fractions: sum_k c_k / (x - x_k) with
+// c_k = 1 / prod_(j != k) (x_k - x_j), and 1 / (x - x_k) = x_k^-1 / (x / x_k - 1), where x / x_k is the
+// domain point e_k = skips j_k places back, so the term is a_k tinv[i - e_k / 2^log_g] with
+// a_k = c_k / x_k (Montgomery, like the table).  The same field value as the batch inverse, bit for
+// bit (both canonical); at x = x_k the kernel gives 0 as the batch inverse does.  Up to 8 distinct
+// points (false otherwise: the proof takes the batch inverse).
+static bool zb2_partial_fractions(const HostFp& g2, uint64_t prec, uint64_t skips, uint32_t log_g,
+                                  const size_t* public_first_indices, size_t n_pfi, ConstraintArgs& ca) {
+  const FieldHost& F = FieldHost::get();
+  constexpr size_t kMaxPf = sizeof(ca.pf_shift) / sizeof(ca.pf_shift[0]);
+  if (n_pfi == 0 || n_pfi > kMaxPf) return false;
+  std::vector<HostFp> xs(n_pfi);
+  for (size_t k = 0; k < n_pfi; ++k) {
+    const uint64_t e = (skips * (uint64_t)public_first_indices[2 * k + 1]) % prec;  // a multiple of skips
+    xs[k] = F.pow_u64(g2, e);
+    ca.pf_shift[k] = e >> log_g;
+  }
+  for (size_t k = 0; k < n_pfi; ++k) {
+    HostFp c = xs[k];
+    for (size_t j = 0; j < n_pfi; ++j) {
+      if (j == k) continue;
+      const HostFp d = F.sub(xs[k], xs[j]);
+      if (FieldHost::eq(d, F.zero())) return false;  // a repeated point
+      c = F.mul(c, d);
+    }
+    ca.pf_coef[k] = to_dev(F.inv(c));
+  }
+  ca.n_pf = (uint32_t)n_pfi;
+  return true;
 }
 
 static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t log_g,
@@ -932,22 +1007,17 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   const Twiddles* tw2 = roots.tw2;
   const Twiddles* tw1i = roots.tw1i;
   const Mont mc = mont();
-  const fe* idx_ext = nullptr;  // the shared extension of IDX (prepared circuits carry their own)
-  // F0 is 1 on the os trace rows whenever the flags are the trace builder's (flag bytes, calc_flags
-  // run.rs:283-308), so its extension is shared too and only K F1 F2 S P PIDX are extended here.
-  // 1 / Zb3 is shared likewise, so the proof's batch inverse covers Zb2 alone.
-  // (Each later reservation may evict an earlier one: looked up again after the last.)
-  const fe *f0_ext = nullptr, *izb3 = nullptr;
-  if (!pre) {
-    STARK_TRY(ext_const_column(ctx, kInvZb3, 0, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &izb3));
-    if (flag_bytes)
-      STARK_TRY(ext_const_column(ctx, kExtF0, os, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &f0_ext));
-    STARK_TRY(ext_index_column(ctx, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, &idx_ext));
-    if (f0_ext && !ctx->ext_idx.count(std::make_tuple(kExtF0, log_steps, log_prec, 0u, 0u, (uint64_t)os)))
-      f0_ext = nullptr;
-    if (izb3 && !ctx->ext_idx.count(std::make_tuple(kInvZb3, log_steps, log_prec, 0u, 0u, (uint64_t)0)))
-      izb3 = nullptr;
-  }
+  // The shared size-only columns (prepared circuits carry their own): IDX's extension; F0's whenever
+  // the flags are the trace builder's (flag bytes, calc_flags run.rs:283-308: 1 on the os rows), so only
+  // K F1 F2 S P PIDX are extended here; 1 / Zb3; and the table that gives 1 / Zb2 by partial fractions,
+  // so the proof has no batch inverse over the domain at all (zb2_partial_fractions).
+  SharedCols sc;
+  if (!pre)
+    STARK_TRY(shared_columns(ctx, flag_bytes != nullptr, os, log_steps, log_prec, 0, 0, *tw1i, *tw2, *tw2, s, sc));
+  const fe *idx_ext = sc.idx, *f0_ext = sc.f0, *izb3 = sc.izb3;
+  ConstraintArgs ca;
+  ca.tinv = nullptr;
+  if (sc.tinv && izb3 && zb2_partial_fractions(g2, prec, skips, 0, public_first_indices, n_pfi, ca)) ca.tinv = sc.tinv;
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts, *rows, *lvals;
   uint64_t* perm;
@@ -1059,7 +1129,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   fe* const top_d = multi_inv_h_top(ctx, 0);
   fe* const top_z = multi_inv_h_top(ctx, 1);
   if (!top_d || !top_z) return STARK_ERR_OOM;
-  if (!pre) {
+  if (!pre && !ca.tinv) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                        (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
                        zb, izb3 ? nullptr : zb + prec);
@@ -1078,7 +1148,6 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(multi_inv_down(ctx, inv_z, s));  // (empty plan with a prepared circuit)
 
   // Constraint kernel.
-  ConstraintArgs ca;
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * prec;
   ca.col[6] = ext_idx;
   ca.col[8] = cols + 7 * prec;  // A
@@ -1458,19 +1527,16 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   memcpy(d.g2c, roots.g2c, 32);
   const Twiddles *tw2 = roots.tw2, *tw1i = roots.tw1i, *twh = roots.twh;
   const Mont mc = mont();
-  const fe* idx_ext = nullptr;  // this rank's share of the extension of IDX (shared across proofs)
-  // ... and of F0's extension (flags from a trace builder) and 1 / Zb3, as in prove_r1cs.
-  const fe *f0_ext = nullptr, *izb3 = nullptr;
-  if (!pre) {
-    STARK_TRY(ext_const_column(ctx, kInvZb3, 0, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &izb3));
-    if (flag_bytes)
-      STARK_TRY(ext_const_column(ctx, kExtF0, os, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &f0_ext));
-    STARK_TRY(ext_index_column(ctx, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s, &idx_ext));
-    if (f0_ext && !ctx->ext_idx.count(std::make_tuple(kExtF0, log_steps, log_prec, d.log_g, rank, (uint64_t)os)))
-      f0_ext = nullptr;
-    if (izb3 && !ctx->ext_idx.count(std::make_tuple(kInvZb3, log_steps, log_prec, d.log_g, rank, (uint64_t)0)))
-      izb3 = nullptr;
-  }
+  // This rank's share of the shared size-only columns, as in prove_r1cs.
+  SharedCols sc;
+  if (!pre)
+    STARK_TRY(shared_columns(ctx, flag_bytes != nullptr, os, log_steps, log_prec, d.log_g, rank, *tw1i, *tw2, *twh, s,
+                             sc));
+  const fe *idx_ext = sc.idx, *f0_ext = sc.f0, *izb3 = sc.izb3;
+  ConstraintArgs ca;
+  ca.tinv = nullptr;
+  if (sc.tinv && izb3 && zb2_partial_fractions(g2, prec, skips, d.log_g, public_first_indices, n_pfi, ca))
+    ca.tinv = sc.tinv;
 
   fe *raw, *wcopy, *cols, *nmr, *dnm, *tot, *dnm_c, *inv_dnm, *zb, *inv_zb, *consts;
   uint64_t* perm;
@@ -1546,14 +1612,13 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
                      (const fe*)inv_dnm, steps, raw);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(lde_coset(d, raw, 1, cols + 7 * P, *tw1i, *tw2, *twh));  // A in slot 7
-  if (!pre) {  // Zb2 / Zb3 at this rank's points and their inverses
+  if (!pre && !ca.tinv) {  // Zb2 / Zb3 at this rank's points and their inverses
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                        (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
                        zb, izb3 ? nullptr : zb + P);
     STARK_HIP(ctx, hipGetLastError());
     STARK_TRY(multi_inv_device(ctx, zb, inv_zb, izb3 ? P : 2 * P, s));
   }
-  ConstraintArgs ca;
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * P;
   ca.col[8] = cols + 7 * P;  // A
   ca.inv_zb = pre ? pre + 6 * P : inv_zb;
