@@ -20,6 +20,23 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what) {
   return e == hipErrorOutOfMemory ? STARK_ERR_OOM : STARK_ERR_HIP;
 }
 
+// STARK_POISON=1 (diagnostics): every device allocation of the library and every pinned staging buffer
+// is filled with 0xA5 bytes when it is made, so a kernel that reads memory nobody wrote gives a
+// reproducible wrong result instead of one that depends on what the memory held before.
+bool poison_on() {
+  static const bool on = [] {
+    const char* v = getenv("STARK_POISON");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+void poison_dev(void* p, size_t bytes) {
+  if (poison_on() && p && bytes) {
+    hipMemset(p, 0xA5, bytes);
+    hipDeviceSynchronize();
+  }
+}
+
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.ptr) return STARK_OK;
   if (b.ptr) {
@@ -33,6 +50,7 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
     b.ptr = nullptr;
     return hip_fail(ctx, e, "hipMalloc");
   }
+  poison_dev(b.ptr, bytes);
   b.bytes = bytes;
   return STARK_OK;
 }
@@ -252,6 +270,7 @@ stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
     const size_t want = bytes < 4096 ? 4096 : bytes;
     // Coherent: kernels read and write this memory directly (zero-copy gathers).
     STARK_HIP(ctx, hipHostMalloc(&ctx->pinned[slot], want, hipHostMallocCoherent));
+    if (poison_on()) memset(ctx->pinned[slot], 0xA5, want);
     ctx->pinned_bytes[slot] = want;
   }
   *out = ctx->pinned[slot];
@@ -527,6 +546,7 @@ stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr) {
   if (!ctx || !d_ptr) return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   STARK_HIP(ctx, hipMalloc(d_ptr, bytes ? bytes : 16));
+  poison_dev(*d_ptr, bytes);
   return STARK_OK;
 }
 stark_status stark_dev_free(stark_ctx* ctx, void* d_ptr) {

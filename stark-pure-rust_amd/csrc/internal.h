@@ -161,6 +161,9 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
     if (st_ != STARK_OK) return st_; \
   } while (0)
 
+// STARK_POISON=1: fill new device allocations with 0xA5 (api.hip; diagnostics only).
+bool poison_on();
+void poison_dev(void* p, size_t bytes);
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
 // Bytes held by the context's cached tables (full twiddle tables and IDX extensions).
 size_t cache_bytes(const stark_ctx* ctx);
