@@ -321,7 +321,7 @@ def end_to_end(ctx):
     for key, (rb, wb, jb) in (("pedersen", (r1, wt, js)), ("synth_2^20_steps", (rs, ws, js_s))):
         ok = verify_with_wtns(ctx, rb, wb, jb)
         tv = []
-        for _ in range(3):
+        for _ in range(10):
             t0 = time.perf_counter()
             verify_with_wtns(ctx, rb, wb, jb)
             tv.append(time.perf_counter() - t0)
