@@ -23,7 +23,18 @@ def _worker(rank, world, port, prepared, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=180))
+    if os.environ.get("DIAG_POISON_TORCH"):  # every torch.empty / empty_like filled with 0xA5 bytes
+        _empty, _empty_like = torch.empty, torch.empty_like
+
+        def _poison(t):
+            if t.numel() and t.is_contiguous():
+                t.view(torch.uint8).fill_(0xA5)
+            return t
+        torch.empty = lambda *a, **k: _poison(_empty(*a, **k))
+        torch.empty_like = lambda *a, **k: _poison(_empty_like(*a, **k))
     import stark_amd as S
+    if os.environ.get("STARK_LIB"):
+        S.load_library(os.environ["STARK_LIB"])
     from stark_amd.dprove import DistCircuit, GpuProverOps, prove_distributed
     import synth_r1cs
     torch.cuda.set_device(0)
@@ -53,7 +64,19 @@ def main():
     import synth_r1cs
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "large_digests.json")))["prove_synth_2^20_steps"]
     ref = None
+    hold = None
+    if os.environ.get("DIAG_PARENT_GPU"):  # like pytest's session context: the parent holds a GPU context
+        if os.environ.get("STARK_LIB"):
+            S.load_library(os.environ["STARK_LIB"])
+        hold = S.Context(0)
+        r1h, wth = synth_r1cs.for_steps(14)
+        prove_with_witness(hold, r1h, wth).to_json()
     for k in range(runs):
+        alt = os.environ.get("DIAG_ALTERNATE")  # a cold proof before each prepared one, as the test file runs them
+        if alt:
+            res0 = dict(run_ranks(_worker, world, (False,), timeout=230))
+            ok0 = hashlib.sha256(res0[0].encode()).hexdigest() == want["json_sha256"]
+            print(f"run {k}: world {world} cold: {'ok' if ok0 else 'MISMATCH'}", flush=True)
         res = dict(run_ranks(_worker, world, (prepared,), timeout=230))
         js = res[0]
         ok = hashlib.sha256(js.encode()).hexdigest() == want["json_sha256"]
