@@ -16,7 +16,11 @@
  *    (suffix _dev) take device pointers and a hipStream_t (NULL = the context
  *    stream) and are asynchronous on that stream.
  *  - Every call returns a stark_status; 0 = success.  Nothing unwinds.
- *  - One context per GPU; a context is not shared between threads.
+ *  - One context per GPU; a context is not shared between threads.  Calls on one context may take
+ *    different streams: the context's own buffers and cached tables are ordered across streams
+ *    by the library (events), so results never depend on which stream a call used.
+ *  - ABI changes bump STARK_ABI_VERSION; a client built against this header checks
+ *    stark_abi_version() == STARK_ABI_VERSION at start-up (INTEGRATION.md lists the changes).
  */
 #ifndef STARK_HIP_H
 #define STARK_HIP_H
@@ -27,6 +31,11 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* 2: stark_r1cs_proof_branches takes leaves_cap / nodes_cap (round 4). */
+#define STARK_ABI_VERSION 2u
+/* The ABI version the loaded library implements (no reference counterpart: a linking check). */
+uint32_t stark_abi_version(void);
 
 typedef enum {
   STARK_OK = 0,

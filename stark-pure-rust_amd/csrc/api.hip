@@ -40,6 +40,11 @@ void poison_dev(void* p, size_t bytes) {
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.ptr) return STARK_OK;
   if (b.ptr) {
+    if (b.ev && b.last) {  // the last enqueued use (any stream) has finished before the buffer goes
+      hipError_t e = hipEventSynchronize(b.ev);
+      if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize(buffer)");
+      b.last = nullptr;
+    }
     hipError_t e = hipFree(b.ptr);
     b.ptr = nullptr;
     b.bytes = 0;
@@ -52,6 +57,44 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   }
   poison_dev(b.ptr, bytes);
   b.bytes = bytes;
+  return STARK_OK;
+}
+
+stark_status buf_acquire(stark_ctx* ctx, DevBuf& b, hipStream_t s) {
+  if (!b.last || b.last == s) return STARK_OK;
+  const hipError_t q = hipEventQuery(b.ev);
+  if (q == hipSuccess) {  // complete: no wait needed
+    b.last = nullptr;
+    return STARK_OK;
+  }
+  if (q != hipErrorNotReady) return hip_fail(ctx, q, "hipEventQuery(buffer)");
+  STARK_HIP(ctx, hipStreamWaitEvent(s, b.ev, 0));
+  return STARK_OK;
+}
+
+stark_status buf_release(stark_ctx* ctx, DevBuf& b, hipStream_t s) {
+  if (!b.ev) STARK_HIP(ctx, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+  STARK_HIP(ctx, hipEventRecord(b.ev, s));
+  b.last = s;
+  return STARK_OK;
+}
+
+stark_status fill_wait(stark_ctx* ctx, hipEvent_t ev, hipStream_t& fill, hipStream_t s) {
+  if (!fill || fill == s) return STARK_OK;
+  const hipError_t q = hipEventQuery(ev);
+  if (q == hipSuccess) {
+    fill = nullptr;  // the table is complete for every later reader
+    return STARK_OK;
+  }
+  if (q != hipErrorNotReady) return hip_fail(ctx, q, "hipEventQuery(table fill)");
+  STARK_HIP(ctx, hipStreamWaitEvent(s, ev, 0));
+  return STARK_OK;
+}
+
+stark_status fill_mark(stark_ctx* ctx, hipEvent_t& ev, hipStream_t& fill, hipStream_t s) {
+  if (!ev) STARK_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  STARK_HIP(ctx, hipEventRecord(ev, s));
+  fill = s;
   return STARK_OK;
 }
 
@@ -97,9 +140,9 @@ bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext) {
           ext_it = it;
           full_slot = nullptr;
         }
-    auto post_it = ctx->post_tw.end();  // (only read inside a launch: always a candidate)
+    auto post_it = ctx->post_tw.end();  // (a candidate unless a call in progress holds it)
     for (auto it = ctx->post_tw.begin(); it != ctx->post_tw.end(); ++it)
-      if (it->second.used < oldest) {
+      if (!it->second.in_use && it->second.used < oldest) {
         oldest = it->second.used;
         post_it = it;
         full_slot = nullptr;
@@ -107,15 +150,22 @@ bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext) {
       }
     if (!full_slot && ext_it == ctx->ext_idx.end() && post_it == ctx->post_tw.end()) return false;
     if (!synced) {
-      hipDeviceSynchronize();
+      // A kernel of any stream may still read the victim.  After a failed synchronisation (a sticky
+      // device error) nothing is freed: the caller does not cache, and the error surfaces at its
+      // own next HIP call.
+      if (hipDeviceSynchronize() != hipSuccess) return false;
       synced = true;
     }
     if (full_slot) {
       hipFree(*full_slot);
       *full_slot = nullptr;
       have -= full_bytes;
+      for (auto& kv : ctx->tw)  // the victim's fill is complete (synchronised above)
+        for (int d = 0; d < 2; ++d)
+          if (full_slot == (d ? &kv.second->d_full_s : &kv.second->d_full)) kv.second->full_fill[d] = nullptr;
     } else if (post_it != ctx->post_tw.end()) {
       hipFree(post_it->second.ptr);
+      if (post_it->second.ev) hipEventDestroy(post_it->second.ev);
       have -= post_it->second.bytes;
       ctx->post_tw.erase(post_it);
     } else {
@@ -136,6 +186,11 @@ class HostWorkers {
     return *w;
   }
   unsigned threads() const { return (unsigned)workers_ + 1; }
+  // Each call is a Job of its own (on the caller's stack): a worker takes a reference to the current
+  // job under the lock and claims items from that job's counter only, and the caller returns once
+  // every item is done AND every worker that joined has let go of the job.  (The previous form kept
+  // one counter for all calls: a worker still leaving call k could claim, run and count an item of
+  // call k + 1 while that call was being set up, so the call could return with an item unfinished.)
   void run(unsigned n, const std::function<void(unsigned)>& fn) {
     if (n == 0) return;
     if (n == 1 || workers_ == 0 || in_job()) {  // a job that calls host_parallel runs the inner one serially
@@ -143,25 +198,28 @@ class HostWorkers {
       return;
     }
     std::lock_guard<std::mutex> serial(call_);  // one parallel call at a time
+    Job job{&fn, n};
     {
       std::lock_guard<std::mutex> g(m_);
-      job_ = &fn;
-      n_ = n;
-      next_.store(1);
-      pending_ = n - 1;
+      cur_ = &job;
       ++gen_;
     }
     cv_.notify_all();
     in_job() = true;
-    fn(0);
-    drain();
+    work(job);
     in_job() = false;
     std::unique_lock<std::mutex> g(m_);
-    done_.wait(g, [&] { return pending_ == 0; });
-    job_ = nullptr;
+    cur_ = nullptr;  // no worker joins from here on
+    done_.wait(g, [&] { return job.done == job.n && job.refs == 0; });
   }
 
  private:
+  struct Job {
+    const std::function<void(unsigned)>* fn;
+    unsigned n;
+    std::atomic<unsigned> next{0};
+    unsigned done = 0, refs = 0;  // under m_
+  };
   HostWorkers() {
     unsigned hw = std::thread::hardware_concurrency();
     hw = hw < 1 ? 1 : (hw > 16 ? 16 : hw);
@@ -172,32 +230,38 @@ class HostWorkers {
     thread_local bool flag = false;
     return flag;
   }
-  void drain() {
-    for (unsigned k; (k = next_.fetch_add(1)) < n_;) {
-      (*job_)(k);
+  void work(Job& job) {
+    unsigned mine = 0;
+    for (unsigned k; (k = job.next.fetch_add(1)) < job.n; ++mine) (*job.fn)(k);
+    if (mine) {
       std::lock_guard<std::mutex> g(m_);
-      if (--pending_ == 0) done_.notify_all();
+      job.done += mine;
+      if (job.done == job.n) done_.notify_all();
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      Job* job;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [&] { return gen_ != seen; });
         seen = gen_;
+        job = cur_;
+        if (!job) continue;  // that call has already finished
+        ++job->refs;
       }
       in_job() = true;
-      drain();
+      work(*job);
       in_job() = false;
+      std::lock_guard<std::mutex> g(m_);
+      if (--job->refs == 0) done_.notify_all();
     }
   }
   size_t workers_ = 0;
   std::mutex call_, m_;
   std::condition_variable cv_, done_;
-  const std::function<void(unsigned)>* job_ = nullptr;
-  unsigned n_ = 0, pending_ = 0;
-  std::atomic<unsigned> next_{0};
+  Job* cur_ = nullptr;
   uint64_t gen_ = 0;
 };
 
@@ -262,7 +326,8 @@ void host_parallel(unsigned n, const std::function<void(unsigned)>& fn) { HostWo
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
   if (ctx->pinned_bytes[slot] < bytes) {
     if (ctx->pinned[slot]) {
-      hipStreamSynchronize(ctx->stream);  // no copy may still target the old buffer
+      // no copy or zero-copy kernel of any stream may still use the old buffer (it only ever grows)
+      STARK_HIP(ctx, hipDeviceSynchronize());
       hipHostFree(ctx->pinned[slot]);
     }
     ctx->pinned[slot] = nullptr;
@@ -353,6 +418,8 @@ const char* stark_status_str(stark_status s) {
   return "unknown";
 }
 
+uint32_t stark_abi_version(void) { return STARK_ABI_VERSION; }
+
 stark_status stark_ctx_create(int device, stark_ctx** out) {
   if (!out) return STARK_ERR_BAD_ARG;
   *out = nullptr;
@@ -376,10 +443,13 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
   hipStreamSynchronize(ctx->stream);
+  hipDeviceSynchronize();  // (work the caller enqueued on its own streams may still read context buffers)
   for (auto& kv : ctx->tw) {
     if (kv.second->d_lo) hipFree(kv.second->d_lo);
     if (kv.second->d_full) hipFree(kv.second->d_full);
     if (kv.second->d_full_s) hipFree(kv.second->d_full_s);
+    for (hipEvent_t e : kv.second->full_ev)
+      if (e) hipEventDestroy(e);
   }
   for (stark_merkle_tree*& t : ctx->trees) {
     stark_merkle_free(t);
@@ -390,15 +460,19 @@ void stark_ctx_destroy(stark_ctx* ctx) {
     if (p) hipHostFree(p);
   for (auto& kv : ctx->ext_idx)
     if (kv.second.ptr) hipFree(kv.second.ptr);
-  for (auto& kv : ctx->post_tw)
+  for (auto& kv : ctx->post_tw) {
     if (kv.second.ptr) hipFree(kv.second.ptr);
+    if (kv.second.ev) hipEventDestroy(kv.second.ev);
+  }
   if (ctx->staged) hipEventDestroy(ctx->staged);
   if (ctx->ev_aux) hipEventDestroy(ctx->ev_aux);
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->inv_tmp, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
-                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp})
+                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp}) {
     if (b->ptr) hipFree(b->ptr);
+    if (b->ev) hipEventDestroy(b->ev);
+  }
   hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -245,27 +245,40 @@ stark_status stark_cyclic_ntt_local_dev(stark_ctx* ctx, uint64_t* d_data, uint32
   F.to_canonical(w, wc);
   const auto key = std::make_tuple(wc[0], wc[1], wc[2], wc[3], log_n, rank);
   hipStream_t s = pick_stream(ctx, stream);
-  const fe* post = nullptr;
   auto it = ctx->post_tw.find(key);
-  if (it != ctx->post_tw.end()) {
-    it->second.used = ++ctx->cache_clock;
-    post = (const fe*)it->second.ptr;
-  } else {
+  if (it == ctx->post_tw.end()) {
     const Twiddles* tn = nullptr;
     STARK_TRY(get_twiddles(ctx, wc, log_n, &tn));
     const uint64_t M = (uint64_t)1 << log_m;
     void* p = nullptr;
-    if (!cache_reserve(ctx, M * sizeof(fe), false) || hipMalloc(&p, M * sizeof(fe)) != hipSuccess) {
+    const bool cached = cache_reserve(ctx, M * sizeof(fe), false);
+    if (hipMalloc(&p, M * sizeof(fe)) != hipSuccess) {
       hipGetLastError();
       return STARK_ERR_OOM;
     }
     hipLaunchKernelGGL(post_tw_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (fe*)p, M, (uint64_t)rank,
                        log_n, tn->d_lo, tn->d_hi, tn->kb);
     STARK_HIP(ctx, hipGetLastError());
-    ctx->post_tw[key] = CacheBuf{p, M * sizeof(fe), ++ctx->cache_clock};
-    post = (const fe*)p;
+    if (!cached) {
+      // Larger than the cache cap: this call's own table, freed once the transform has run.
+      const stark_status st = ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, (const fe*)p);
+      hipStreamSynchronize(s);
+      hipFree(p);
+      return st;
+    }
+    CacheBuf cb{p, M * sizeof(fe), 0};
+    STARK_TRY(fill_mark(ctx, cb.ev, cb.fill, s));  // complete once the fill has run on s
+    it = ctx->post_tw.emplace(key, cb).first;
   }
-  return ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, post);
+  CacheBuf& e = it->second;
+  e.used = ++ctx->cache_clock;
+  STARK_TRY(fill_wait(ctx, e.ev, e.fill, s));  // (filled by a call on another stream)
+  // Held while the transform is enqueued: its last pass's full table (ntt_device -> cache_reserve)
+  // must not evict this entry and launch with a freed pointer.
+  e.in_use = true;
+  const stark_status st = ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, (const fe*)e.ptr);
+  e.in_use = false;
+  return st;
 }
 
 stark_status stark_twiddle2d_dev(stark_ctx* ctx, uint64_t* d_data, size_t rows, size_t cols, uint64_t row_base,

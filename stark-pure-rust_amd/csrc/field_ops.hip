@@ -328,10 +328,14 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
   fe* h_top = multi_inv_h_top(ctx, 0);
   if (!h_top) return STARK_ERR_OOM;
   InvPlan plan;
+  // io2 and the pinned top array are the context's: a previous inverse on another stream may still
+  // read them in its down kernels (the host rewrites the top array below, after s has waited for it).
+  STARK_TRY(buf_acquire(ctx, ctx->io2, s));
   STARK_TRY(multi_inv_up(ctx, d_in, d_out, n, s, ctx->io2, h_top, plan));
   STARK_HIP(ctx, hipStreamSynchronize(s));
   multi_inv_top(plan);
-  return multi_inv_down(ctx, plan, s);
+  STARK_TRY(multi_inv_down(ctx, plan, s));
+  return buf_release(ctx, ctx->io2, s);
 }
 
 }  // namespace stark
@@ -440,10 +444,12 @@ stark_status stark_lincomb_dev(stark_ctx* ctx, const uint64_t* d_cols, uint32_t 
   stark_status st = ensure_buf(ctx, ctx->io2, h.size() * sizeof(fe));
   if (st != STARK_OK) return st;
   hipStream_t s = pick_stream(ctx, stream);
+  STARK_TRY(buf_acquire(ctx, ctx->io2, s));
   STARK_HIP(ctx, hipMemcpyAsync(ctx->io2.ptr, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const fe*)d_cols, n_cols,
                      (uint64_t)n, (const fe*)ctx->io2.ptr, (fe*)d_out);
   STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(buf_release(ctx, ctx->io2, s));
   // h is pageable and goes out of scope: the copy must have consumed it.
   STARK_HIP(ctx, hipStreamSynchronize(s));
   return STARK_OK;

@@ -162,6 +162,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   if (st != STARK_OK) return st;
   st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
   if (st != STARK_OK) return st;
+  STARK_TRY(buf_acquire(ctx, ctx->fri_misc, s));  // (the distributed fold's slot 15 is on the caller's stream)
   uint8_t* pinned = nullptr;
   st = ctx_pinned(ctx, 1, kPinned1Bytes, (void**)&pinned);
   if (st != STARK_OK) return st;
@@ -218,6 +219,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
                        (uint32_t*)p->h_roots);
     STARK_HIP(ctx, hipGetLastError());
   }
+  STARK_TRY(buf_release(ctx, ctx->fri_misc, s));
   *out = std::move(p);
   return STARK_OK;
 }
@@ -524,6 +526,7 @@ static stark_status fri_fold(stark_ctx* ctx, const uint64_t* values, uint64_t* c
   if (st != STARK_OK) return st;
   st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
   if (st != STARK_OK) return st;
+  STARK_TRY(buf_acquire(ctx, ctx->fri_misc, s));  // (prove_low_degree writes slots 0-14 on the context stream)
   fe* d_sx = (fe*)ctx->fri_misc.ptr + 15;  // slot 15: unused by prove_low_degree's <= 15 layers
   fe sx;
   if (m_root) {
@@ -540,6 +543,7 @@ static stark_status fri_fold(stark_ctx* ctx, const uint64_t* values, uint64_t* c
                      (fe*)column, (uint64_t)q, (uint32_t)0, (uint64_t)rank, log_g, tw->d_lo, tw->d_hi, tw->kb,
                      (const fe*)d_sx, to_dev(zeta), to_dev(F.inv(F.from_u64(4))));
   STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(buf_release(ctx, ctx->fri_misc, s));
   if (m_root) STARK_HIP(ctx, hipStreamSynchronize(s));  // sx lives on this stack frame
   return STARK_OK;
 }

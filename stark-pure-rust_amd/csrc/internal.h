@@ -49,10 +49,15 @@ struct PhaseClock {
   }
 };
 
-// Device buffer owned by a context.
+// Device buffer owned by a context.  A context buffer that calls on different streams share (the NTT
+// ping-pong, the batch inverse's scratch, the fold's special_x slot, ...) also carries the stream of
+// its last enqueued use and an event recorded after that use: buf_acquire makes the next user's
+// stream wait for it, buf_release marks the uses just enqueued (api.hip).
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
 };
 
 // Twiddle set for one (root, log_n): everything in Montgomery form.
@@ -77,6 +82,10 @@ struct Twiddles {
   fe* d_full = nullptr;
   fe* d_full_s = nullptr;
   uint64_t full_used = 0, full_s_used = 0;  // cache clock of their last use (LRU eviction, cache_reserve)
+  // The fill of d_full / d_full_s ([1]) is enqueued on the stream of the call that first needs it;
+  // a call on another stream waits for this event until the fill is known to be complete (fill = null).
+  hipEvent_t full_ev[2] = {nullptr, nullptr};
+  hipStream_t full_fill[2] = {nullptr, nullptr};
   size_t base_bytes = 0;         // device bytes of the tables above d_full (one allocation at d_lo)
   size_t n_small_pairs = 0;      // Shoup pairs in d_small
   // Digit-basis tables (fe_db.h) of w_R^k, k < R/2, for every radix R = 2^l >= 16: the constants of the
@@ -92,6 +101,9 @@ struct CacheBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
   uint64_t used = 0;
+  bool in_use = false;          // held by a call in progress: never evicted (cache_reserve)
+  hipEvent_t ev = nullptr;      // the fill's event while it may still run (stream `fill`), as Twiddles::full_ev
+  hipStream_t fill = nullptr;
 };
 
 // Default cap on a context's cached tables (the last-pass full twiddle tables, 2^log_n x 32 B per
@@ -165,6 +177,13 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
 bool poison_on();
 void poison_dev(void* p, size_t bytes);
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
+// Cross-stream use of a context buffer (DevBuf::ev): acquire before the first enqueued use on s (s
+// waits for the last use on another stream, unless that is already complete), release after the
+// last one.  The same for a cached table filled on one stream and read on another (fill_wait).
+stark_status buf_acquire(stark_ctx* ctx, DevBuf& b, hipStream_t s);
+stark_status buf_release(stark_ctx* ctx, DevBuf& b, hipStream_t s);
+stark_status fill_wait(stark_ctx* ctx, hipEvent_t ev, hipStream_t& fill, hipStream_t s);
+stark_status fill_mark(stark_ctx* ctx, hipEvent_t& ev, hipStream_t& fill, hipStream_t s);
 // Bytes held by the context's cached tables (full twiddle tables and IDX extensions).
 size_t cache_bytes(const stark_ctx* ctx);
 // Makes room for `need` more cached bytes under ctx->cache_limit by freeing least recently used

@@ -899,19 +899,25 @@ static stark_status full_table(stark_ctx* ctx, const Twiddles& tw_c, uint32_t lo
                                const fe** out) {
   Twiddles& tw = const_cast<Twiddles&>(tw_c);  // lazily filled cache entry
   fe*& slot = scaled ? tw.d_full_s : tw.d_full;
+  const int d = scaled ? 1 : 0;
   (scaled ? tw.full_s_used : tw.full_used) = ++ctx->cache_clock;
   if (!slot) {
     const uint64_t n = (uint64_t)1 << tw.log_n;
-    void* d = nullptr;
-    if (!cache_reserve(ctx, n * sizeof(fe), false) || hipMalloc(&d, n * sizeof(fe)) != hipSuccess) {
+    void* p = nullptr;
+    if (!cache_reserve(ctx, n * sizeof(fe), false) || hipMalloc(&p, n * sizeof(fe)) != hipSuccess) {
       hipGetLastError();  // (a failed allocation is not an error here)
       *out = nullptr;     // no room: fall back to the two-level form
       return STARK_OK;
     }
     hipLaunchKernelGGL(full_tw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, tw.d_lo, tw.d_hi,
-                       tw.kb, log_r, n, to_dev(tw.inv_n), scaled ? 1 : 0, (fe*)d);
+                       tw.kb, log_r, n, to_dev(tw.inv_n), scaled ? 1 : 0, (fe*)p);
     STARK_HIP(ctx, hipGetLastError());
-    slot = (fe*)d;
+    // Published now, complete only when the fill has run on `stream`: a call on another stream
+    // waits for this event (fill_wait below) instead of reading a table still being written.
+    STARK_TRY(fill_mark(ctx, tw.full_ev[d], tw.full_fill[d], stream));
+    slot = (fe*)p;
+  } else {
+    STARK_TRY(fill_wait(ctx, tw.full_ev[d], tw.full_fill[d], stream));
   }
   *out = slot;
   return STARK_OK;
@@ -962,9 +968,17 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     return STARK_OK;
   }
   const PassPlan plan = plan_passes(log_n);
-  stark_status st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
-  if (st != STARK_OK) return st;
-  fe* scratch = (fe*)ctx->scratch.ptr;
+  // The ping-pong buffer is the context's, shared by every stream that calls in: this stream waits
+  // for the last use on another one (buf_acquire) and marks its own after the passes (buf_release).
+  // (A single-pass transform never touches it.)
+  fe* scratch = nullptr;
+  stark_status st = STARK_OK;
+  if (plan.n_pass > 1) {
+    st = ensure_buf(ctx, ctx->scratch, n * batch * sizeof(fe));
+    if (st != STARK_OK) return st;
+    STARK_TRY(buf_acquire(ctx, ctx->scratch, stream));
+    scratch = (fe*)ctx->scratch.ptr;
+  }
   const fe* cur = src ? src : d_data;
   uint32_t log_ns = 0;
   for (int p = 0; p < plan.n_pass; ++p) {
@@ -1009,6 +1023,7 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     cur = dst;
     log_ns += lr;
   }
+  if (scratch) STARK_TRY(buf_release(ctx, ctx->scratch, stream));
   return STARK_OK;
 }
 

@@ -1129,6 +1129,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   fe* const top_d = multi_inv_h_top(ctx, 0);
   fe* const top_z = multi_inv_h_top(ctx, 1);
   if (!top_d || !top_z) return STARK_ERR_OOM;
+  // (io2's guard covers the pinned top arrays too: multi_inv_device on another stream uses both)
+  STARK_TRY(buf_acquire(ctx, ctx->io2, s));
   if (!pre && !ca.tinv) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                        (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
@@ -1146,6 +1148,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(lde(ctx, raw, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
   STARK_TRY(multi_inv_down(ctx, inv_z, s));  // (empty plan with a prepared circuit)
+  STARK_TRY(buf_release(ctx, ctx->io2, s));
 
   // Constraint kernel.
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * prec;

@@ -45,6 +45,7 @@ _szp = ctypes.POINTER(ctypes.c_size_t)
 _vp = ctypes.c_void_p
 
 _SIGNATURES = {
+    "stark_abi_version": ([], ctypes.c_uint32),
     "stark_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_ctx_destroy": ([_vp], None),
     "stark_status_str": ([ctypes.c_int], ctypes.c_char_p),
@@ -174,8 +175,32 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    want = header_abi_version()
+    if lib.stark_abi_version() != want:
+        raise RuntimeError(f"{path} implements ABI {lib.stark_abi_version()}, include/stark_hip.h declares {want}: "
+                           "rebuild the library")
     _lib = lib
     return lib
+
+
+def header_abi_version(path: str = HEADER_PATH) -> int:
+    """STARK_ABI_VERSION of include/stark_hip.h."""
+    import re
+    m = re.search(r"#define\s+STARK_ABI_VERSION\s+(\d+)u?", open(path).read())
+    return int(m.group(1))
+
+
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy (hip_runtime_api.h): the legacy default stream as a handle
+
+
+def torch_stream() -> int:
+    """torch's current stream as the handle the library's _dev calls take.  torch's default stream
+    has handle 0, which the library reads as "the context's own stream" (a non-blocking stream the
+    default stream does not order against): it is passed as hipStreamLegacy instead, so the library's
+    kernels and torch's copies and collectives run in one stream order either way."""
+    import torch
+    s = torch.cuda.current_stream().cuda_stream
+    return s if s else HIP_STREAM_LEGACY
 
 
 def header_symbols(path: str = HEADER_PATH) -> list:

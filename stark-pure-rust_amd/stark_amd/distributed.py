@@ -191,7 +191,8 @@ class GpuOps:
 
     @staticmethod
     def _stream() -> int:
-        return torch.cuda.current_stream().cuda_stream
+        from . import torch_stream
+        return torch_stream()
 
     def ntt(self, t: torch.Tensor, log_len: int, batch: int, root: int, inverse: bool) -> None:
         self.ctx.ntt_dev(t.data_ptr(), log_len, batch, root, inverse=inverse, stream=self._stream())

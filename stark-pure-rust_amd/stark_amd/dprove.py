@@ -297,7 +297,9 @@ def prove_distributed(ops, r1cs: bytes, wtns: bytes, group=None, fri_tail_log: i
     """prove_with_witness (run.rs:310-452) over the G ranks of `group`.
     Every rank calls it; rank 0 returns the StarkProof JSON, the others None.
     circuit: this rank's DistCircuit (the .r1cs-only work done once; r1cs is then unused).
-    stats: filled (when given) with this rank's per-phase times and host-synchronising step count."""
+    stats: filled (when given) with this rank's per-phase times and host-synchronising step count.
+    On a GPU every step runs on torch's current stream (GpuProverOps): the library's kernels,
+    torch's copies and the collectives share one stream order."""
     G = dist.get_world_size(group)
     r = dist.get_rank(group)
     dev = getattr(ops, "dev", None)
@@ -438,7 +440,8 @@ class GpuProverOps:
 
     @staticmethod
     def _stream():
-        return torch.cuda.current_stream().cuda_stream
+        from . import torch_stream
+        return torch_stream()
 
     @staticmethod
     def _ptr(buf) -> int:
