@@ -18,7 +18,9 @@
  *  - Every call returns a stark_status; 0 = success.  Nothing unwinds.
  *  - One context per GPU; a context is not shared between threads.  Calls on one context may take
  *    different streams: the context's own buffers and cached tables are ordered across streams
- *    by the library (events), so results never depend on which stream a call used.
+ *    by the library (events), so results never depend on which stream a call used.  A stream
+ *    handed to a call must stay valid until the context's next call on another stream (the
+ *    library then records an event on it) or until stark_ctx_synchronize.
  *  - ABI changes bump STARK_ABI_VERSION; a client built against this header checks
  *    stark_abi_version() == STARK_ABI_VERSION at start-up (INTEGRATION.md lists the changes).
  */

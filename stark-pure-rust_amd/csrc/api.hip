@@ -40,11 +40,7 @@ void poison_dev(void* p, size_t bytes) {
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.ptr) return STARK_OK;
   if (b.ptr) {
-    if (b.ev && b.last) {  // the last enqueued use (any stream) has finished before the buffer goes
-      hipError_t e = hipEventSynchronize(b.ev);
-      if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize(buffer)");
-      b.last = nullptr;
-    }
+    STARK_TRY(buf_drain(ctx, b));  // the last enqueued use (any stream) has finished before the buffer goes
     hipError_t e = hipFree(b.ptr);
     b.ptr = nullptr;
     b.bytes = 0;
@@ -60,27 +56,42 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
   return STARK_OK;
 }
 
+// Lazy ordering: a use only notes its stream (buf_release, no GPU work); when a call on another
+// stream comes, an event recorded on the previous stream at that moment covers every use enqueued
+// there, and the new stream waits for it.  (An event recorded after every use cost ~4 us of GPU time
+// per NTT, tools/ab_libs.py; this costs one marker per change of stream.)  Hence the ABI rule that a
+// stream handed to a call stays valid until the context's next call on another stream.
+// The stream of a last use is kept as a non-null handle: the HIP null stream (stream 0) as kNullStream.
+static const hipStream_t kNullStream = hipStreamLegacy;
+static hipStream_t tag(hipStream_t s) { return s ? s : kNullStream; }
+static hipStream_t untag(hipStream_t s) { return s == kNullStream ? nullptr : s; }
+
 stark_status buf_acquire(stark_ctx* ctx, DevBuf& b, hipStream_t s) {
-  if (!b.last || b.last == s) return STARK_OK;
-  const hipError_t q = hipEventQuery(b.ev);
-  if (q == hipSuccess) {  // complete: no wait needed
-    b.last = nullptr;
-    return STARK_OK;
+  if (b.last && b.last != tag(s)) {
+    if (!b.ev) STARK_HIP(ctx, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+    STARK_HIP(ctx, hipEventRecord(b.ev, untag(b.last)));
+    STARK_HIP(ctx, hipStreamWaitEvent(s, b.ev, 0));
   }
-  if (q != hipErrorNotReady) return hip_fail(ctx, q, "hipEventQuery(buffer)");
-  STARK_HIP(ctx, hipStreamWaitEvent(s, b.ev, 0));
+  b.last = tag(s);
   return STARK_OK;
 }
 
 stark_status buf_release(stark_ctx* ctx, DevBuf& b, hipStream_t s) {
-  if (!b.ev) STARK_HIP(ctx, hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
-  STARK_HIP(ctx, hipEventRecord(b.ev, s));
-  b.last = s;
+  (void)ctx;
+  b.last = tag(s);
+  return STARK_OK;
+}
+
+stark_status buf_drain(stark_ctx* ctx, DevBuf& b) {
+  if (b.last) {
+    STARK_HIP(ctx, hipStreamSynchronize(untag(b.last)));
+    b.last = nullptr;
+  }
   return STARK_OK;
 }
 
 stark_status fill_wait(stark_ctx* ctx, hipEvent_t ev, hipStream_t& fill, hipStream_t s) {
-  if (!fill || fill == s) return STARK_OK;
+  if (!fill || fill == tag(s)) return STARK_OK;
   const hipError_t q = hipEventQuery(ev);
   if (q == hipSuccess) {
     fill = nullptr;  // the table is complete for every later reader
@@ -94,7 +105,7 @@ stark_status fill_wait(stark_ctx* ctx, hipEvent_t ev, hipStream_t& fill, hipStre
 stark_status fill_mark(stark_ctx* ctx, hipEvent_t& ev, hipStream_t& fill, hipStream_t s) {
   if (!ev) STARK_HIP(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   STARK_HIP(ctx, hipEventRecord(ev, s));
-  fill = s;
+  fill = tag(s);
   return STARK_OK;
 }
 
@@ -351,7 +362,13 @@ stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out) {
   return STARK_OK;
 }
 
-hipStream_t pick_stream(stark_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+// NULL = the context's stream; hipStreamLegacy (the legacy default stream as a handle: how a caller on
+// torch's default stream names it, stark_amd.torch_stream) = the HIP null stream itself, which every HIP
+// call takes as 0 (not every one accepts the handle value: hipStreamWaitEvent faults on it).
+hipStream_t pick_stream(stark_ctx* ctx, void* stream) {
+  if (!stream) return ctx->stream;
+  return (hipStream_t)stream == hipStreamLegacy ? nullptr : (hipStream_t)stream;
+}
 
 // Host-buffer NTT: copy in (zero-padded), transform on the GPU, copy out.
 static stark_status fft_host(stark_ctx* ctx, const uint64_t* in, size_t len, const uint64_t root[4], uint32_t log_n,
@@ -647,6 +664,8 @@ stark_status stark_ctx_synchronize(stark_ctx* ctx) {
   if (!ctx) return STARK_ERR_BAD_ARG;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // Every stream the context's buffers were last used on is drained, and no longer referenced.
+  for (DevBuf* b : {&ctx->scratch, &ctx->io2, &ctx->fri_misc}) STARK_TRY(buf_drain(ctx, *b));
   return STARK_OK;
 }
 

@@ -51,8 +51,8 @@ struct PhaseClock {
 
 // Device buffer owned by a context.  A context buffer that calls on different streams share (the NTT
 // ping-pong, the batch inverse's scratch, the fold's special_x slot, ...) also carries the stream of
-// its last enqueued use and an event recorded after that use: buf_acquire makes the next user's
-// stream wait for it, buf_release marks the uses just enqueued (api.hip).
+// its last enqueued use: buf_acquire makes a call on another stream wait for everything enqueued on
+// that one (an event recorded there at that moment), buf_release notes the stream (api.hip).
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -177,11 +177,13 @@ stark_status hip_fail(stark_ctx* ctx, hipError_t e, const char* what);
 bool poison_on();
 void poison_dev(void* p, size_t bytes);
 stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes);
-// Cross-stream use of a context buffer (DevBuf::ev): acquire before the first enqueued use on s (s
-// waits for the last use on another stream, unless that is already complete), release after the
-// last one.  The same for a cached table filled on one stream and read on another (fill_wait).
+// Cross-stream use of a context buffer (DevBuf::last): acquire before the first enqueued use on s (s
+// waits for what the previous user's stream has enqueued so far), release after the last one.  A
+// cached table filled on one stream and read on another: fill_mark records the fill's event, fill_wait
+// makes another stream wait for it until it is known to be complete.
 stark_status buf_acquire(stark_ctx* ctx, DevBuf& b, hipStream_t s);
 stark_status buf_release(stark_ctx* ctx, DevBuf& b, hipStream_t s);
+stark_status buf_drain(stark_ctx* ctx, DevBuf& b);  // host-waits for the last use's stream, forgets it
 stark_status fill_wait(stark_ctx* ctx, hipEvent_t ev, hipStream_t& fill, hipStream_t s);
 stark_status fill_mark(stark_ctx* ctx, hipEvent_t& ev, hipStream_t& fill, hipStream_t s);
 // Bytes held by the context's cached tables (full twiddle tables and IDX extensions).

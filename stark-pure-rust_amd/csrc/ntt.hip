@@ -1015,15 +1015,14 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
     // data image + staged Shoup pairs + digit-basis tables (DbPlan of this instance)
     const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
     const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
-    hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)total), dim3(threads), lds, stream, cur, dst, log_n, log_ns, lb, ct,
-                       tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
-                       (inverse && last && !fold) ? 1 : 0, log_tiles,
-                       (uint32_t)total, sp);
+    hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)total), dim3(threads), lds, stream, cur, dst, log_n,
+                       log_ns, lb, ct, tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], scale,
+                       (inverse && last && !fold) ? 1 : 0, log_tiles, (uint32_t)total, sp);
     STARK_HIP(ctx, hipGetLastError());
     cur = dst;
     log_ns += lr;
   }
-  if (scratch) STARK_TRY(buf_release(ctx, ctx->scratch, stream));
+  if (scratch) buf_release(ctx, ctx->scratch, stream);
   return STARK_OK;
 }
 
