@@ -20,6 +20,7 @@ import hashlib
 import json
 import os
 import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -401,6 +402,64 @@ MERKLE_SQ = os.path.join(ROOT, "profiles", "r04_pmc_merkle32.json")
 CPU_PROVE_2_20 = os.path.join(ROOT, "profiles", "r04_cpu_prove_synth_2_20.json")
 
 
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (MI355X: 7 links per GPU, task brief)
+
+
+def distributed_phases(buf, log_total, w_total, ops, stream, on_gloo, local, reps=5) -> dict:
+    """Median device time of each phase of one distributed step (the timed loop's transform, run
+    unpipelined with HIP events on the step's stream between the phases), max over ranks: the local
+    M-point NTT (stark_amd/distributed.py cyclic_ntt_local), the all-to-all, the cross-rank G-point
+    DFT (cyclic_ntt_finish)."""
+    from stark_amd.distributed import _exchange, cyclic_ntt_finish, cyclic_ntt_local
+    a = buf.clone()
+    z = torch.empty_like(a)
+    names = ("local_ms", "exchange_ms", "finish_ms")
+    got = {k: [] for k in names}
+    for _ in range(reps + 1):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        dist.barrier()
+        torch.cuda.synchronize()
+        ev[0].record()
+        y = cyclic_ntt_local(a, log_total, w_total, ops, in_place=True)
+        ev[1].record()
+        _exchange(z, y)
+        ev[2].record()
+        cyclic_ntt_finish(z, log_total, w_total, ops)
+        ev[3].record()
+        ev[3].synchronize()
+        for i, k in enumerate(names):
+            got[k].append(ev[i].elapsed_time(ev[i + 1]))
+    med = torch.tensor([statistics.median(got[k][1:]) for k in names], dtype=torch.float64,
+                       device="cpu" if on_gloo else f"cuda:{local}")
+    dist.all_reduce(med, op=dist.ReduceOp.MAX)
+    return dict(zip(names, (round(float(x), 4) for x in med.cpu())))
+
+
+def distributed_roofline(ph: dict, n: int, world: int, log_n: int, plan: list, on_gloo: bool) -> dict:
+    """The distributed step's rooflines, kept apart: its HBM-bound local kernels (the M-point NTT's pass
+    launches and the strided G-point DFT, each 64 B per element read + written) at this
+    rank's shard, and the all-to-all's bytes ((G-1)/G of the 32-B shard leave each rank, one G-th to
+    each peer) against the direct xGMI links (G-1 of them at XGMI_LINK_GBS per rank)."""
+    local_bytes = 64.0 * n * 2
+    local_ms = ph["local_ms"] + ph["finish_ms"]
+    achieved = local_bytes / (local_ms / 1000.0) / 1e9
+    x_bytes = (world - 1) / world * n * 32.0
+    x_peak = (world - 1) * XGMI_LINK_GBS
+    x_ach = x_bytes / (ph["exchange_ms"] / 1000.0) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "traffic_note": "no counter pass of the distributed step (the committed PMC profiles are the "
+                            "1-GPU transform's)",
+            "kernel": f"local: {len(plan)} NTT pass launches (radices 2^{plan}) of this rank's 2^{log_n}-point "
+                      "transform + the strided G-point DFT across the received chunks",
+            "algorithmic_bytes_per_rank": local_bytes, "phases_ms": ph,
+            "step_ms_unpipelined": round(sum(ph.values()), 4),
+            "exchange": {"bound": "host-staged gloo (rehearsal: not an xGMI figure)" if on_gloo
+                         else f"xGMI: {world - 1} direct links per rank", "bytes_per_rank": x_bytes,
+                         "ms": ph["exchange_ms"], "achieved": round(x_ach, 2), "peak": x_peak, "unit": "GB/s",
+                         "frac": round(x_ach / x_peak, 4)}}
+
+
 def merkle_valu_roofline(n: int, ms: float) -> dict:
     """Blake2s issue roofline of a 2^log n x 32-B tree build: n leaf compressions (one 32-B block
     each) + n - 1 node compressions (64-B blocks) = 2n - 1.  From the committed counter passes over
@@ -776,12 +835,10 @@ def main():
     # write 32) x n / transform time (HIP events on the launch stream).
     ntt_bytes = 64.0 * n
     if world > 1:
-        # The timed step also holds the all-to-all and the cross-rank DFT: time this rank's local
-        # 2^log_n transform (the same ntt_pass_kernel launches) on its own for the kernel roofline.
-        tmp = buf.clone()
-        ctx.ntt_dev(tmp.data_ptr(), log_n, 1, w, inverse=False, stream=sptr)
-        ev_ms = steady_ms(lambda: ctx.ntt_dev(tmp.data_ptr(), log_n, 1, w, inverse=False, stream=sptr), stream)
-        del tmp
+        # The distributed step, phase by phase (its own roofline below, nothing from a 1-GPU profile):
+        # this rank's local M-point transform, the all-to-all, the cross-rank G-point DFT.
+        dphase = distributed_phases(buf, log_total, w_total, ops, stream, on_gloo, local)
+        ev_ms = dphase["local_ms"]
     achieved = ntt_bytes / (ev_ms / 1000.0) / 1e9
     plan = S.ntt_plan(log_n)
     passes = len(plan)
@@ -792,6 +849,8 @@ def main():
     traffic = prof_avg = prof_med = None
     knames, sq, timed = [], {}, None
     try:
+        if world > 1:
+            raise OSError("the committed profiles are of the 1-GPU transform")
         prof = json.load(open(PROFILE))
         knames = sorted(k for k in prof["kernels"] if "ntt_pass_kernel" in k)
         if log_n == 24 and knames and all(k in prof["pmc_bytes_per_launch"] for k in knames):
@@ -804,7 +863,7 @@ def main():
     except (OSError, KeyError, ValueError):
         pass
     try:
-        if log_n == 24:
+        if log_n == 24 and world == 1:
             pmc = json.load(open(PMC))["kernels"]
             sq = {k: v for k, v in pmc.items() if "ntt_pass_kernel" in k and "valu_issue_frac" in v}
     except (OSError, KeyError, ValueError):
@@ -817,6 +876,8 @@ def main():
                 "rocprof_ms_per_transform_avg": round(prof_avg, 4) if prof_avg else None,
                 "rocprof_ms_per_transform_steady_median": round(prof_med, 4) if prof_med else None,
                 "rocprof_kernels": knames, "rocprof_summary": os.path.relpath(PROFILE, ROOT)}
+    if world > 1:
+        roofline = distributed_roofline(dphase, n, world, log_n, plan, on_gloo)
     if timed:  # the profiled run's kernels over its own timed steps vs that run's ms_per_step
         roofline["rocprof_timed_region_ms_per_transform"] = round(timed["kernel_ms_per_transform"], 4)
         roofline["rocprof_run_ms_per_step"] = round(timed["bench_ms_per_step_same_run"], 4)
@@ -861,6 +922,22 @@ def main():
         roofline["power_during_ntt"] = extras["power_during_ntt"]
 
     cpu = None
+    if rank == 0 and world > 1 and not args.no_cpu_baseline:
+        # One rank's share on the host: best_fft (fft.rs:327-357, the oracle's C restatement with the
+        # Worker split's 2^floor(log2 cores) threads) of this rank's 2^log_n shard.  The reference has no
+        # multi-node form; the whole job's CPU time is world times this.
+        o = O.Oracle()
+        physical, usable = host_cpus()
+        threads = 1 << (min(physical, usable).bit_length() - 1)
+        t2 = time.perf_counter()
+        o.best_fft(host, w, log_n, cpus=threads)
+        tc = time.perf_counter() - t2
+        cpu = {"value": n / tc, "unit": "field-elems/s", "cores": threads, "threads": threads,
+               "host_physical_cores": physical, "cpus_granted": usable, "kind": "port",
+               "sample": f"rank 0's 2^{log_n}-element shard as one 2^{log_n}-point best_fft (oracle C restatement "
+                         f"of fft.rs parallel_fft, {threads} threads), {tc:.2f} s; the whole 2^{log_total} job on "
+                         f"this host would be {world} such shards or more",
+               "scope": "one rank's shard (per-GPU work of the weak-scaling step)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # The reference algorithm on the host: the oracle's C restatement of best_fft / parallel_fft
         # (fft.rs:195-251, 327-357) with T = 2^floor(log2(cores)) threads as Worker::new splits it,
