@@ -102,6 +102,25 @@ struct DbPlan {
   static constexpr int occupancy = on ? 3 : 4;                     // workgroups per CU the LDS allows
 };
 
+// Streaming (non-temporal) forms of fe_load / fe_store: one use per transform, nothing to keep in L2.
+// The passes store through fe_store_nt and the last pass reads its full twiddle table through
+// fe_load_nt (2^20 -3.5 %, 2^22 -1.9 %, 2^26 -1.4 %, 2^24 within noise; tools/ab_libs.py,
+// profiles/r05_nt_ab.txt).  Non-temporal tile loads measured +3.6 % at 2^24 and are not used.
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ fe fe_load_nt(const fe* p) {
+  const u32x4_nt* q = reinterpret_cast<const u32x4_nt*>(p);
+  const u32x4_nt lo = __builtin_nontemporal_load(q), hi = __builtin_nontemporal_load(q + 1);
+  fe r;
+  r.w[0] = lo.x; r.w[1] = lo.y; r.w[2] = lo.z; r.w[3] = lo.w;
+  r.w[4] = hi.x; r.w[5] = hi.y; r.w[6] = hi.z; r.w[7] = hi.w;
+  return r;
+}
+__device__ __forceinline__ void fe_store_nt(fe* p, const fe& v) {
+  u32x4_nt* q = reinterpret_cast<u32x4_nt*>(p);
+  __builtin_nontemporal_store(u32x4_nt{v.w[0], v.w[1], v.w[2], v.w[3]}, q);
+  __builtin_nontemporal_store(u32x4_nt{v.w[4], v.w[5], v.w[6], v.w[7]}, q + 1);
+}
+
 // LDS data image of a pass, element index i = (row << log_b) + column.  The two 16-B halves of each
 // element sit in separate planes (lo at v[i], hi at v[n + i]), so the 16 lanes of a ds_read_b128 group
 // read 16 adjacent 16-B slots instead of every other one.
@@ -213,7 +232,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       fe tw[4];
       if (COL == kColFull) {  // the transform's last pass (lnr == log_n) with a full table
 #pragma unroll
-        for (int t = 0; t < 4; ++t) tw[t] = ct.full[(((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]];
+        for (int t = 0; t < 4; ++t) tw[t] = fe_load_nt(ct.full + ((((j0 + eb[t]) & ns_mask) << LOG_R) + er[t]));
         // Montgomery images (the table streams from HBM once per transform, so it stays 32 B per
         // entry): v < 4p, tw < p -> [0, 2p); two interleaved products per block
         mul2(v[0], v[1], v[0], tw[0], v[1], tw[1]);
@@ -576,7 +595,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           if (last) fe_reduce_lazy(val);
           if (do_scale) val = fe_mul(val, scale);
         }
-        fe_store(dst + o, val);
+        fe_store_nt(dst + o, val);
       }
     } else {
       // Ns < B: the tile's output is the contiguous run [j0 R, (j0 + B) R).
@@ -591,7 +610,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         if (last) fe_reduce_lazy(val);
         if (do_scale) val = fe_mul(val, scale);
         if (last && ct.post) val = fe_mul(val, ct.post[(j0 << LOG_R) + o]);
-        fe_store(dst + (j0 << LOG_R) + o, val);
+        fe_store_nt(dst + (j0 << LOG_R) + o, val);
       }
     }
   }
