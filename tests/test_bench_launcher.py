@@ -38,3 +38,21 @@ def test_single_gpu_runs_in_process():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_distributed_roofline_fields():
+    """The N > 1 line's roofline (bench.py distributed_roofline): the local kernels' 2 x 64 B per shard
+    element against HBM and the all-to-all's (G-1)/G x 32 B per element against G-1 xGMI links, from
+    the phase times; nothing taken from the 1-GPU profiles."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n, world = 1 << 24, 8
+    ph = {"local_ms": 1.5, "exchange_ms": 0.5, "finish_ms": 0.25}
+    r = bench.distributed_roofline(ph, n, world, 24, [8, 8, 8], on_gloo=False)
+    assert r["bound"] == "hbm" and r["traffic"] is None and r["phases_ms"] == ph
+    assert abs(r["achieved"] - 128.0 * n / 1.75e-3 / 1e9) < 0.01
+    x = r["exchange"]
+    assert x["bytes_per_rank"] == 7 / 8 * n * 32 and x["peak"] == 7 * bench.XGMI_LINK_GBS
+    assert abs(x["achieved"] - x["bytes_per_rank"] / 0.5e-3 / 1e9) < 0.01
+    assert "xGMI" in x["bound"]
+    assert "not an xGMI figure" in bench.distributed_roofline(ph, n, 2, 24, [8, 8, 8], on_gloo=True)["exchange"]["bound"]
