@@ -98,6 +98,47 @@ __global__ void collect_roots_kernel(RootPtrs r, uint32_t count, uint32_t* __res
   if (t < 8 * count) out[t] = r.p[t / 8][t % 8];
 }
 
+// get_pseudorandom_indices(root2_l, q_l, 40, excl) (fri/src/utils.rs:84-111; stark_get_pseudorandom_indices)
+// for every layer on the device, so the openings' gather follows the last layer in stream order with no
+// host round trip: thread l extends layer l's root by four chained Blake2s hashes (160 bytes), reads the
+// 40 big-endian words and writes the column indices ys and the poly indices ys + j q (fri.rs:181-204)
+// into the gather's index array.  (fri_enqueue checked q < 2^24 and the exclusion's divisor up front.)
+struct FriIdxArgs {
+  const uint32_t* root[16];  // root2 of layer l: the root of the layer's column tree
+  uint32_t q[16];
+  uint64_t col_at[16], poly_at[16];  // first slots in the index array
+};
+__global__ void fri_indices_kernel(FriIdxArgs a, uint32_t layers, uint32_t excl, uint64_t* __restrict__ idx) {
+  const uint32_t l = threadIdx.x;
+  if (l >= layers) return;
+  uint32_t data[40];  // 160 bytes, little-endian words
+#pragma unroll
+  for (int k = 0; k < 8; ++k) data[k] = a.root[l][k];
+#pragma unroll
+  for (int b = 1; b < 5; ++b) {
+    uint32_t h[8], m[16];
+    b2s_init(h);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m[k] = data[8 * (b - 1) + k];
+      m[k + 8] = 0;
+    }
+    b2s_compress(h, m, 32, 0, true);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) data[8 * b + k] = h[k];
+  }
+  const uint32_t q = a.q[l];
+  const uint32_t real_mod = excl ? (uint32_t)((uint64_t)q * (excl - 1) / excl) : q;
+  for (int i = 0; i < 40; ++i) {
+    const uint32_t w = __builtin_bswap32(data[i]);
+    const uint32_t v = w % real_mod;
+    const uint64_t y = excl ? v + 1 + v / (excl - 1) : v;
+    idx[a.col_at[l] + i] = y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) idx[a.poly_at[l] + 4 * i + j] = y + (uint64_t)q * j;
+  }
+}
+
 // Pinned slot 1 layout: [0, 2048) mk_r1cs_proof's transcript, [2048, 2560) FRI roots.
 constexpr size_t kFriRootsOff = 2048;
 
@@ -224,27 +265,22 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   return STARK_OK;
 }
 
-// Phase 2: the host transcript (fri.rs:181-204), every opening in one gather
-// batch together with the caller's `extra` requests, and the Last layer
-// (fri.rs:108-110).
+// Phase 2: every opening in one gather batch together with the caller's `extra` requests, and the Last
+// layer (fri.rs:108-110).  The layers' indices (the transcript, fri.rs:181-204) are derived on the device
+// behind the last layer, so the gather needs no host round trip: one synchronisation in all.  The host
+// then takes the indices from the index array and checks them against its own derivation.
 stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out) {
   hipStream_t s = ctx->stream;
-  STARK_HIP(ctx, hipStreamSynchronize(s));
   std::vector<stark_merkle_tree*>& trees = p->trees;
   stark_fri_proof* proof = p->proof.get();
   proof->layers.resize(p->layers);
   std::vector<GatherReq> reqs = extra;
+  const size_t n_extra = reqs.size();
   for (size_t layer = 0; layer < p->layers; ++layer) {
     stark_fri_layer& L = proof->layers[layer];
     const size_t q = p->qs[layer];
-    memcpy(L.root2, p->h_roots + 32 * (layer + 1), 32);
-    // ys = get_pseudorandom_indices(m2_root, column.len(), 40, exclude) (fri.rs:181-189)
-    uint32_t ys[40];
-    stark_status st = stark_get_pseudorandom_indices(L.root2, 32, (uint32_t)q, 40, p->excl, ys);
-    if (st != STARK_OK) return st;
-    L.col_idx.assign(ys, ys + 40);
-    for (int i = 0; i < 40; ++i)
-      for (int j = 0; j < 4; ++j) L.poly_idx.push_back((size_t)ys[i] + q * j);  // fri.rs:193-204
+    L.col_idx.resize(40);
+    L.poly_idx.resize(160);
     L.col_depth = 0;
     while (((size_t)1 << L.col_depth) < q) ++L.col_depth;
     L.poly_depth = L.col_depth + 2;
@@ -252,19 +288,52 @@ stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& e
     L.col_nodes.resize(40 * L.col_depth * 32);
     L.poly_leaves.resize(160 * 32);
     L.poly_nodes.resize(160 * L.poly_depth * 32);
-    reqs.push_back({trees[layer + 1], L.col_idx.data(), 40, L.col_leaves.data(), L.col_nodes.data()});
-    reqs.push_back({trees[layer], L.poly_idx.data(), 160, L.poly_leaves.data(), L.poly_nodes.data()});
+    reqs.push_back({trees[layer + 1], nullptr, 40, L.col_leaves.data(), L.col_nodes.data()});
+    reqs.push_back({trees[layer], nullptr, 160, L.poly_leaves.data(), L.poly_nodes.data()});
   }
+  uint64_t* h_idx = nullptr;
+  std::vector<size_t> first;
+  auto indices = [&](uint64_t* hi, const std::vector<size_t>& f) -> stark_status {
+    h_idx = hi;
+    first = f;
+    FriIdxArgs a;
+    for (size_t l = 0; l < p->layers; ++l) {
+      a.root[l] = (const uint32_t*)merkle_root_dev(trees[l + 1]);
+      a.q[l] = (uint32_t)p->qs[l];
+      a.col_at[l] = f[n_extra + 2 * l];
+      a.poly_at[l] = f[n_extra + 2 * l + 1];
+    }
+    hipLaunchKernelGGL(fri_indices_kernel, dim3(1), dim3(64), 0, s, a, (uint32_t)p->layers, p->excl, hi);
+    STARK_HIP(ctx, hipGetLastError());
+    return STARK_OK;
+  };
   // The last layer's values come down with the gather (one synchronisation) when they fit the pinned slot.
   const size_t last_bytes = p->last_len * 32;
   uint8_t* h_last = const_cast<uint8_t*>(p->h_roots) - kFriRootsOff + kPinned1LastOff;
   const bool last_pinned = last_bytes && last_bytes <= kPinned1Bytes - kPinned1LastOff;
   if (last_pinned) STARK_HIP(ctx, hipMemcpyAsync(h_last, p->last_dev, last_bytes, hipMemcpyDeviceToHost, s));
-  stark_status st = merkle_gather_batch(ctx, reqs, s);
+  stark_status st = merkle_gather_batch(ctx, reqs, s, indices);
   if (st != STARK_OK) return st;
   size_t gathered = 0;
   for (const GatherReq& q : reqs) gathered += q.k;
-  if (last_pinned && gathered == 0) STARK_HIP(ctx, hipStreamSynchronize(s));  // (no gather: no synchronisation)
+  if (gathered == 0) STARK_HIP(ctx, hipStreamSynchronize(s));  // (no gather: no synchronisation)
+  for (size_t layer = 0; layer < p->layers; ++layer) {
+    stark_fri_layer& L = proof->layers[layer];
+    const size_t q = p->qs[layer];
+    memcpy(L.root2, p->h_roots + 32 * (layer + 1), 32);
+    // ys = get_pseudorandom_indices(m2_root, column.len(), 40, exclude) (fri.rs:181-189)
+    uint32_t ys[40];
+    st = stark_get_pseudorandom_indices(L.root2, 32, (uint32_t)q, 40, p->excl, ys);
+    if (st != STARK_OK) return st;
+    for (int i = 0; i < 40; ++i) {
+      L.col_idx[i] = (size_t)h_idx[first[n_extra + 2 * layer] + i];
+      for (int j = 0; j < 4; ++j) L.poly_idx[4 * i + j] = (size_t)h_idx[first[n_extra + 2 * layer + 1] + 4 * i + j];
+      if (L.col_idx[i] != ys[i]) {
+        ctx->last_error = "FRI indices derived on the device differ from the host's";
+        return STARK_ERR_HIP;
+      }
+    }
+  }
   stark_fri_layer last;
   last.last = true;
   last.last_values.resize(last_bytes);

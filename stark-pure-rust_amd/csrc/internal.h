@@ -284,13 +284,18 @@ stark_status merkle_gather(stark_ctx* ctx, stark_merkle_tree* t, const size_t* i
 
 struct GatherReq {
   stark_merkle_tree* t;
-  const size_t* idx;
+  const size_t* idx;    // null: the indices are written on the device by `before_launch` (below)
   size_t k;
   uint8_t* leaves_out;  // k * leaf_len bytes
   uint8_t* nodes_out;   // k * depth * 32 bytes
 };
-// All requests in one pinned upload, one download, one synchronisation.
-stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream);
+// All requests in one pinned upload, one download, one synchronisation.  before_launch (optional) is
+// called once the host's indices are in the pinned index array h_idx and before the gather is enqueued,
+// with h_idx and each request's first slot in it; it enqueues on `stream` what writes the indices of
+// the requests whose idx is null (they must be below the tree's leaf count).
+using GatherHook = std::function<stark_status(uint64_t* h_idx, const std::vector<size_t>& first)>;
+stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream,
+                                 const GatherHook& before_launch = GatherHook());
 
 // A rendered JSON text: one uninitialised allocation written once (a std::string would be
 // zero-filled first), so a multi-MB proof is assembled by several threads in parallel.

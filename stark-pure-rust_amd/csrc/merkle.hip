@@ -508,13 +508,17 @@ __global__ __launch_bounds__(64) void merkle_gather_multi_kernel(GatherDescs g, 
   }
 }
 
-stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream) {
+stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& reqs, hipStream_t stream,
+                                 const GatherHook& before_launch) {
   size_t n_idx = 0, out_bytes = 0;
-  std::vector<size_t> off(reqs.size());
+  std::vector<size_t> off(reqs.size()), first(reqs.size());
   for (size_t r = 0; r < reqs.size(); ++r) {
     const GatherReq& q = reqs[r];
-    for (size_t i = 0; i < q.k; ++i)
-      if (q.idx[i] >= q.t->n) return STARK_ERR_BAD_ARG;
+    if (!q.idx && q.k && !before_launch) return STARK_ERR_BAD_ARG;
+    if (q.idx)
+      for (size_t i = 0; i < q.k; ++i)
+        if (q.idx[i] >= q.t->n) return STARK_ERR_BAD_ARG;
+    first[r] = n_idx;
     n_idx += q.k;
     off[r] = out_bytes;
     out_bytes += ((q.k * q.t->leaf_len + 15) & ~(size_t)15) + q.k * q.t->depth * sizeof(Digest);
@@ -527,11 +531,10 @@ stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& r
   if (st != STARK_OK) return st;
   uint64_t* h_idx = (uint64_t*)host;
   uint8_t* h_out = host + idx_bytes;
-  size_t at = 0;
-  for (const GatherReq& q : reqs) {
-    for (size_t i = 0; i < q.k; ++i) h_idx[at + i] = q.idx[i];
-    at += q.k;
-  }
+  for (size_t r = 0; r < reqs.size(); ++r)
+    if (reqs[r].idx)
+      for (size_t i = 0; i < reqs[r].k; ++i) h_idx[first[r] + i] = reqs[r].idx[i];
+  if (before_launch) STARK_TRY(before_launch(h_idx, first));
   // Launches of up to kGatherMaxReq requests; proofs are numbered across the batch.
   size_t r0 = 0, p0 = 0;
   while (r0 < reqs.size()) {

@@ -52,6 +52,51 @@ __device__ __forceinline__ void bfly_lt2p(fe& x, fe& y, const fe& t) {
   fe_bfly_lazy_reduced(x, y, t);
 }
 
+// The pass's lazy range is [0, 4p + 2^224) (4p + 2^224 < 2^256: top word 0xc19139cb).
+// csub2p_top: x <- x - 2p when x's top word is above 2p's (so x > 2p), a branch over the 8-word
+// subtraction (exec-masked: 1 compare + 8 VALU instead of the 8 + 8 of a select); the result is
+// below 2p + 2^224 (an x not subtracted has a top word <= 2p's).
+__device__ __forceinline__ void sub2p(fe& t) {
+  const P2Limbs q = p2_vgprs();  // (a literal and VCC would both take gfx950's one constant-bus read)
+  asm("v_sub_co_u32 %0, vcc, %0, %8\n\t"
+      "v_subb_co_u32 %1, vcc, %1, %9, vcc\n\t"
+      "v_subb_co_u32 %2, vcc, %2, %10, vcc\n\t"
+      "v_subb_co_u32 %3, vcc, %3, %11, vcc\n\t"
+      "v_subb_co_u32 %4, vcc, %4, %12, vcc\n\t"
+      "v_subb_co_u32 %5, vcc, %5, %13, vcc\n\t"
+      "v_subb_co_u32 %6, vcc, %6, %14, vcc\n\t"
+      "v_subb_co_u32 %7, vcc, %7, %15, vcc"
+      : "+v"(t.w[0]), "+v"(t.w[1]), "+v"(t.w[2]), "+v"(t.w[3]), "+v"(t.w[4]), "+v"(t.w[5]), "+v"(t.w[6]),
+        "+v"(t.w[7])
+      : "v"(q.l[0]), "v"(q.l[1]), "v"(q.l[2]), "v"(q.l[3]), "v"(q.l[4]), "v"(q.l[5]), "v"(q.l[6]), "v"(q.l[7])
+      : "vcc");
+}
+__device__ __forceinline__ void csub2p_top(fe& t) {
+  if (t.w[7] > STARK_2P7) sub2p(t);
+}
+// X in [0, 4p + 2^224), T in [0, 2p): x <- X' + T, y <- X' + 2p - T, both in [0, 4p + 2^224).
+template <bool FAST>
+__device__ __forceinline__ void bfly(fe& x, fe& y, const fe& t) {
+  if (FAST) {
+    csub2p_top(x);
+    fe_bfly_lazy_reduced(x, y, t);
+  } else {
+    fe_bfly_lazy(x, y, t);
+  }
+}
+// [0, 4p + 2^224) -> [0, 2p) (an unmultiplied value taking a butterfly's T role).
+template <bool FAST>
+__device__ __forceinline__ void csub2p_t(fe& t) {
+  if (FAST) csub2p_top(t);
+  fe_csub2p(t);
+}
+// [0, 4p + 2^224) -> canonical.
+template <bool FAST>
+__device__ __forceinline__ void reduce_full(fe& t) {
+  csub2p_t<FAST>(t);
+  fe_reduce_once(t);
+}
+
 // The digit-basis table of constant k in LDS: 72 u32 per constant, 16-B aligned.  Constants 8 apart
 // would share banks (72 * 8 = 0 mod 64 banks) and a radix-4 step reads k, k + 8, k + 16, k + 24 in
 // one ds_read_b128 lane group, so each group of 8 constants starts 4 banks after the previous one.
@@ -149,6 +194,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
     uint32_t total_tiles, Sparse sp) {
   constexpr uint32_t R = 1u << LOG_R;
   using DB = DbPlan<LOG_R, COL>;
+  // The top-word reduction (csub2p_top) in the radix-2^6 passes only: there it measured 1.2 % faster at
+  // 2^26 (6, 6, 6, 8); in the 16 x 16 radix-2^8 passes it was 1.1 % slower at 2^24, and 2 % slower in the
+  // radix-2^4 pass of 2^20 (profiles/r05_csub_top_ab.txt).
+  constexpr bool FAST = LOG_R == 6;
   extern __shared__ __attribute__((aligned(16))) fe lds[];
   fe* sm = lds;          // R/2 small roots w_R^k as Shoup pairs: sm[2k] = w_R^k, sm[2k + 1] = its quotient
   uint32_t* sdb = reinterpret_cast<uint32_t*>(lds + DB::shoup_fe);  // digit-basis tables (DbPlan)
@@ -275,8 +324,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           t3 = fe_mul_shoup(v[3], small[ic], small[ic + 1]);
         }
         fe_csub2p(v[1]);
-        fe_bfly_lazy(v[0], v[1], v[1]);
-        fe_bfly_lazy(v[2], v[3], t3);
+        bfly<FAST>(v[0], v[1], v[1]);
+        bfly<FAST>(v[2], v[3], t3);
       } else {
         bfly_lt2p(v[0], v[2], v[2]);
         bfly_lt2p(v[1], v[3], v[3]);
@@ -322,10 +371,10 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       const uint32_t st = (1u << kS0) << log_b;  // m rows
       fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
       if (jj == 0) {
-        fe_csub2p(x1);
-        fe_csub2p(x3);
-        fe_bfly_lazy(x0, x1, x1);
-        fe_bfly_lazy(x2, x3, x3);
+        csub2p_t<FAST>(x1);
+        csub2p_t<FAST>(x3);
+        bfly<FAST>(x0, x1, x1);
+        bfly<FAST>(x2, x3, x3);
         fe t3;
         if (DB::on) {
           t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_{4m}^m = w_4^1
@@ -333,21 +382,21 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           const uint32_t ic = 2 * (1u << (LOG_R - 2));
           t3 = fe_mul_shoup(x3, sm[ic], sm[ic + 1]);
         }
-        fe_csub2p(x2);
-        fe_bfly_lazy(x0, x2, x2);
-        fe_bfly_lazy(x1, x3, t3);
+        csub2p_t<FAST>(x2);
+        bfly<FAST>(x0, x2, x2);
+        bfly<FAST>(x1, x3, t3);
       } else if (DB::on && DB::s_end > kS0 && lq >= 6) {
         // every wave has one jj: the constants come from the global table into SGPRs (no LDS reads)
         const uint32_t ju = __builtin_amdgcn_readfirstlane(jj);
         const uint32_t* wa = db + 72u * (ju << (LOG_R - 1 - kS0));  // w_{2m}^jj
         const fe t1 = fe_mul_db(x1, wa);
         fe t3 = fe_mul_db(x3, wa);
-        fe_bfly_lazy(x0, x1, t1);
-        fe_bfly_lazy(x2, x3, t3);
+        bfly<FAST>(x0, x1, t1);
+        bfly<FAST>(x2, x3, t3);
         const fe t2 = fe_mul_db(x2, db + 72u * (ju << (LOG_R - 2 - kS0)));                // w_{4m}^jj
         t3 = fe_mul_db(x3, db + 72u * ((ju + (1u << kS0)) << (LOG_R - 2 - kS0)));  // w_{4m}^(jj+m)
-        fe_bfly_lazy(x0, x2, t2);
-        fe_bfly_lazy(x1, x3, t3);
+        bfly<FAST>(x0, x2, t2);
+        bfly<FAST>(x1, x3, t3);
       } else if (DB::on && DB::s_end > kS0) {
         constexpr uint32_t S = DB::stride;
         // (four: no LDS table; small tiles read the global one per lane)
@@ -355,26 +404,26 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         const uint32_t* wa = tab(jj << (LOG_R - 1 - kS0));  // w_{2m}^jj
         const fe t1 = fe_mul_db(x1, wa);
         fe t3 = fe_mul_db(x3, wa);
-        fe_bfly_lazy(x0, x1, t1);
-        fe_bfly_lazy(x2, x3, t3);
+        bfly<FAST>(x0, x1, t1);
+        bfly<FAST>(x2, x3, t3);
         const fe t2 = fe_mul_db(x2, tab(jj << (LOG_R - 2 - kS0)));                // w_{4m}^jj
         t3 = fe_mul_db(x3, tab((jj + (1u << kS0)) << (LOG_R - 2 - kS0)));  // w_{4m}^(jj+m)
-        fe_bfly_lazy(x0, x2, t2);
-        fe_bfly_lazy(x1, x3, t3);
+        bfly<FAST>(x0, x2, t2);
+        bfly<FAST>(x1, x3, t3);
       } else {
         fe t1, t3;
         const uint32_t ia = 2 * (jj << (LOG_R - 1 - kS0));
         const fe ta = sm[ia], taq = sm[ia + 1];
         shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
-        fe_bfly_lazy(x0, x1, t1);
-        fe_bfly_lazy(x2, x3, t3);
+        bfly<FAST>(x0, x1, t1);
+        bfly<FAST>(x2, x3, t3);
         const uint32_t ic = 2 * ((jj + (1u << kS0)) << (LOG_R - 2 - kS0));
         const fe tc = sm[ic], tcq = sm[ic + 1];
         const uint32_t ib = 2 * (jj << (LOG_R - 2 - kS0));
         const fe t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
         t3 = fe_mul_shoup(x3, tc, tcq);
-        fe_bfly_lazy(x0, x2, t2);
-        fe_bfly_lazy(x1, x3, t3);
+        bfly<FAST>(x0, x2, t2);
+        bfly<FAST>(x1, x3, t3);
       }
       XI.st(i0, x0);
       XI.st(i0 + 2 * st, x2);
@@ -410,8 +459,8 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       bfly_lt2p(x[2], x[3], x[3]);
       const fe t3 = fe_mul_db(x[3], db + 72u * (1u << (LOG_R - 2)));
       fe_csub2p(x[2]);
-      fe_bfly_lazy(x[0], x[2], x[2]);
-      fe_bfly_lazy(x[1], x[3], t3);
+      bfly<FAST>(x[0], x[2], x[2]);
+      bfly<FAST>(x[1], x[3], t3);
 #pragma unroll
       for (int k = 0; k < 4; ++k) XI.st(i0 + k * st, x[k]);
     }
@@ -422,24 +471,24 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       fe x0 = XI.ld(i0), x1 = XI.ld(i0 + st), x2 = XI.ld(i0 + 2 * st), x3 = XI.ld(i0 + 3 * st);
       auto step = [&](const uint32_t a) {
         if (a == 0) {
-          fe_csub2p(x1);
-          fe_csub2p(x3);
-          fe_bfly_lazy(x0, x1, x1);
-          fe_bfly_lazy(x2, x3, x3);
+          csub2p_t<FAST>(x1);
+          csub2p_t<FAST>(x3);
+          bfly<FAST>(x0, x1, x1);
+          bfly<FAST>(x2, x3, x3);
           const fe t3 = fe_mul_db(x3, db + 72u * (1u << (LOG_R - 2)));  // w_4
-          fe_csub2p(x2);
-          fe_bfly_lazy(x0, x2, x2);
-          fe_bfly_lazy(x1, x3, t3);
+          csub2p_t<FAST>(x2);
+          bfly<FAST>(x0, x2, x2);
+          bfly<FAST>(x1, x3, t3);
         } else {
           const uint32_t* wa = db + 72u * (a << (LOG_R - 3));  // w_8^a = w_R^(a R/8)
           const fe t1 = fe_mul_db(x1, wa);
           fe t3 = fe_mul_db(x3, wa);
-          fe_bfly_lazy(x0, x1, t1);
-          fe_bfly_lazy(x2, x3, t3);
+          bfly<FAST>(x0, x1, t1);
+          bfly<FAST>(x2, x3, t3);
           const fe t2 = fe_mul_db(x2, db + 72u * (a << LT));  // w_16^a = w_R^(a R/16)
           t3 = fe_mul_db(x3, db + 72u * ((a + 4) << LT));     // w_16^(a + 4)
-          fe_bfly_lazy(x0, x2, t2);
-          fe_bfly_lazy(x1, x3, t3);
+          bfly<FAST>(x0, x2, t2);
+          bfly<FAST>(x1, x3, t3);
         }
       };
       // a wave holds 64 / B consecutive q, all with one a when 64 / B <= T (the 1024-element tile): a is
@@ -472,12 +521,12 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         const uint32_t* wa = dbt(sdb, (jj << (LOG_R - 1 - s)) / S);  // w_{2m}^jj
         const fe t1 = fe_mul_db(x1, wa);
         fe t3 = fe_mul_db(x3, wa);
-        fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
-        fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
+        bfly<FAST>(x0, x1, t1);  // (y0, y1)
+        bfly<FAST>(x2, x3, t3);  // (y2, y3)
         const fe t2 = fe_mul_db(x2, dbt(sdb, (jj << (LOG_R - 2 - s)) / S));  // w_{4m}^jj
         t3 = fe_mul_db(x3, dbt(sdb, ((jj + m) << (LOG_R - 2 - s)) / S));   // w_{4m}^(jj+m)
-        fe_bfly_lazy(x0, x2, t2);
-        fe_bfly_lazy(x1, x3, t3);
+        bfly<FAST>(x0, x2, t2);
+        bfly<FAST>(x1, x3, t3);
         XI.st((base << log_b) + b, x0);
         XI.st(((base + 2 * m) << log_b) + b, x2);
         XI.st(((base + m) << log_b) + b, x1);
@@ -505,15 +554,15 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       const uint32_t ia = 2 * (jj << (LOG_R - 1 - s));  // w_{2m}^jj, Shoup pairs staged in LDS
       const fe ta = sm[ia], taq = sm[ia + 1];
       shoup2(t1, t3, x1, ta, taq, x3, ta, taq);
-      fe_bfly_lazy(x0, x1, t1);  // (y0, y1)
-      fe_bfly_lazy(x2, x3, t3);  // (y2, y3)
+      bfly<FAST>(x0, x1, t1);  // (y0, y1)
+      bfly<FAST>(x2, x3, t3);  // (y2, y3)
       const uint32_t ic = 2 * ((jj + m) << (LOG_R - 2 - s));  // w_{4m}^(jj+m)
       const fe tc = sm[ic], tcq = sm[ic + 1];
       const uint32_t ib = 2 * (jj << (LOG_R - 2 - s));  // w_{4m}^jj
       const fe t2 = fe_mul_shoup(x2, sm[ib], sm[ib + 1]);
       t3 = fe_mul_shoup(x3, tc, tcq);
-      fe_bfly_lazy(x0, x2, t2);
-      fe_bfly_lazy(x1, x3, t3);
+      bfly<FAST>(x0, x2, t2);
+      bfly<FAST>(x1, x3, t3);
       if (keep) {
         yl[0] = x0;
         yl[1] = x1;
@@ -553,12 +602,12 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       const uint32_t* wa = dbt(ft, 2 * jj);  // w_{2m}^jj = w_R^(2 jj)
       const fe t1 = fe_mul_db(x1, wa);
       fe t3 = fe_mul_db(x3, wa);
-      fe_bfly_lazy(x0, x1, t1);
-      fe_bfly_lazy(x2, x3, t3);
+      bfly<FAST>(x0, x1, t1);
+      bfly<FAST>(x2, x3, t3);
       const fe t2 = fe_mul_db(x2, dbt(ft, jj));  // w_{4m}^jj
       t3 = fe_mul_db(x3, dbt(ft, jj + m));       // w_{4m}^(jj+m)
-      fe_bfly_lazy(x0, x2, t2);
-      fe_bfly_lazy(x1, x3, t3);
+      bfly<FAST>(x0, x2, t2);
+      bfly<FAST>(x1, x3, t3);
       yl[0] = x0;
       yl[1] = x1;
       yl[2] = x2;
@@ -592,7 +641,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
           if (do_scale) val = fe_mul(val, scale);
           val = fe_mul(val, ct.post[o]);
         } else {
-          if (last) fe_reduce_lazy(val);
+          if (last) reduce_full<FAST>(val);
           if (do_scale) val = fe_mul(val, scale);
         }
         fe_store_nt(dst + o, val);
@@ -607,7 +656,7 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
         const uint32_t r = rem >> log_ns;
         const uint32_t bb = (qq << log_ns) + (rem & (uint32_t)ns_mask);
         fe val = XI.ld((r << log_b) + bb);
-        if (last) fe_reduce_lazy(val);
+        if (last) reduce_full<FAST>(val);
         if (do_scale) val = fe_mul(val, scale);
         if (last && ct.post) val = fe_mul(val, ct.post[(j0 << LOG_R) + o]);
         fe_store_nt(dst + (j0 << LOG_R) + o, val);

@@ -481,10 +481,11 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe d1 = fe_mul(q1, mc ? iz0 : iz2), d2 = fe_mul(q2, mc ? iz1 : iz2), d3 = fe_mul(q3, iz1);
   // I2 / I3 at x = g2^i (Horner; the interpolants are canonical).
   const fe x_m = pow_tab(a.lo, a.hi, a.kb, gi);
-  fe i2 = fe_zero();
-  for (uint32_t k = a.n2; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
-  fe i3 = fe_zero();
-  for (uint32_t k = a.n3; k-- > 0;) i3 = fe_add(fe_mul(i3, x_m), a.interp3[k]);
+  // (Horner from the leading coefficient: the first step's 0 * x + c is c itself)
+  fe i2 = a.n2 ? a.interp2[a.n2 - 1] : fe_zero();
+  for (uint32_t k = a.n2 ? a.n2 - 1 : 0; k-- > 0;) i2 = fe_add(fe_mul(i2, x_m), a.interp2[k]);
+  fe i3 = a.n3 ? a.interp3[a.n3 - 1] : fe_zero();
+  for (uint32_t k = a.n3 ? a.n3 - 1 : 0; k-- > 0;) i3 = fe_add(fe_mul(i3, x_m), a.interp3[k]);
   fe izb2;
   if (a.tinv) {  // (uniform)
     izb2 = fe_zero();

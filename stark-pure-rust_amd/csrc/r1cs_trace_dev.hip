@@ -290,13 +290,17 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
     uint8_t* stage;
     size_t len;
   };
+  // The first pieces are small (256 KB, doubling up to kChunk) so the first DMA starts after a short
+  // memcpy instead of a 2 MB one; the rest stay at kChunk (each DMA costs ~9 us of engine overhead).
   std::vector<Piece> pieces;
-  size_t at = 0;
+  size_t at = 0, piece = kChunk / 8;
   for (const Upload& u : ups)
-    for (size_t o = 0; o < u.len; o += kChunk) {
-      const size_t len = std::min(kChunk, u.len - o);
+    for (size_t o = 0; o < u.len;) {
+      const size_t len = std::min(piece, u.len - o);
       pieces.push_back({(uint8_t*)u.dst + o, (const uint8_t*)u.src + o, stage + at, len});
       at += len;
+      o += len;
+      piece = std::min(kChunk, 2 * piece);
     }
   std::atomic<size_t> next{0};
   // The first failing copy's error, recorded by the worker that saw it (HIP's last-error state is

@@ -142,10 +142,11 @@ class Json {
       } else if (k == "nodes") {
         expect('[');
         if (!accept(']')) {
+          b.nodes.reserve(32 * 32);
           do {
-            uint8_t d[32];
-            digest(d);
-            b.nodes.insert(b.nodes.end(), d, d + 32);
+            const size_t at = b.nodes.size();
+            b.nodes.resize(at + 32);
+            digest(b.nodes.data() + at);
           } while (ok && accept(','));
           expect(']');
         }
@@ -339,26 +340,18 @@ struct PathCheck {
   size_t index;
   const Branch* b;
 };
-bool paths_valid(const std::vector<PathCheck>& v) {
+// ok[i] = check i's path leads to its root.
+void paths_check(const std::vector<PathCheck>& v, std::vector<uint8_t>& ok) {
+  ok.assign(v.size(), 0);
   std::vector<size_t> cost(v.size() + 1, 0);
   for (size_t i = 0; i < v.size(); ++i) cost[i + 1] = cost[i] + 1 + v[i].b->nodes.size() / 32;
-  const unsigned parts = (unsigned)std::min<size_t>(host_threads(), (v.size() + 31) / 32);
-  std::vector<uint8_t> good(std::max(parts, 1u), 1);
-  host_parallel(std::max(parts, 1u), [&](unsigned t) {
-    const unsigned np = std::max(parts, 1u);
-    const size_t lo = std::lower_bound(cost.begin(), cost.end(), cost.back() * t / np) - cost.begin();
-    const size_t hi = std::lower_bound(cost.begin(), cost.end(), cost.back() * (t + 1) / np) - cost.begin();
-    for (size_t i = lo; i < hi && i < v.size(); ++i)
-      if (!branch_valid(v[i].root, v[i].index, *v[i].b)) {
-        good[t] = 0;
-        return;
-      }
+  const unsigned parts = std::max(1u, (unsigned)std::min<size_t>(host_threads(), (v.size() + 31) / 32));
+  host_parallel(parts, [&](unsigned t) {
+    const size_t lo = std::lower_bound(cost.begin(), cost.end(), cost.back() * t / parts) - cost.begin();
+    const size_t hi = std::lower_bound(cost.begin(), cost.end(), cost.back() * (t + 1) / parts) - cost.begin();
+    for (size_t i = lo; i < hi && i < v.size(); ++i) ok[i] = branch_valid(v[i].root, v[i].index, *v[i].b);
   });
-  for (uint8_t g : good)
-    if (!g) return false;
-  return true;
 }
-
 bool sampler(const uint8_t seed[32], size_t modulus, uint32_t count, uint32_t excl, std::vector<size_t>& out) {
   if (modulus > 0xFFFFFFFFull) return false;
   std::vector<uint32_t> v(count);
@@ -368,8 +361,11 @@ bool sampler(const uint8_t seed[32], size_t modulus, uint32_t count, uint32_t ex
 }
 
 // verify_low_degree_proof_rec (fri.rs:244-404).
+// `extra` (optional): more path checks to run in the same parallel pass as the layers' (the verifier's
+// main and L openings); *extra_ok tells whether they all hold, whatever this function returns.
 stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std::vector<FriIn>& proof,
-                        size_t max_deg_plus_1, uint32_t excl) {
+                        size_t max_deg_plus_1, uint32_t excl, const std::vector<PathCheck>* extra = nullptr,
+                        bool* extra_ok = nullptr) {
   const FieldHost& F = FieldHost::get();
   if (proof.empty()) return STARK_ERR_BAD_ARG;
   uint64_t rou_deg = 1;
@@ -413,44 +409,72 @@ stark_status verify_fri(const uint8_t merkle_root_in[32], HostFp root, const std
       for (size_t i = 0; i < pos_l[l].size(); ++i) checks.push_back({root_l, pos_l[l][i], &L.poly[i]});
       root_l = L.root2;
     }
-    if (!paths_valid(checks)) return STARK_ERR_CHECK;
+    const size_t n_fri = checks.size();
+    if (extra) checks.insert(checks.end(), extra->begin(), extra->end());
+    std::vector<uint8_t> ok;
+    paths_check(checks, ok);
+    if (extra_ok) *extra_ok = std::find(ok.begin() + n_fri, ok.end(), 0) == ok.end();
+    if (std::find(ok.begin(), ok.begin() + n_fri, 0) != ok.begin() + n_fri) return STARK_ERR_CHECK;
+  }
+  // Every row of every layer is independent once the roots are known: the cubic checks run on the host
+  // workers, and the layer loop below reports the first failure in the reference's order
+  // (fri.rs:318-345).  x1 = root_l^y has order dividing rou_deg_l, so 1 / x1^3 = root_l^(-3y mod rou_deg_l)
+  // needs no inversion.
+  std::vector<uint8_t> row_ok(ys_l.size(), 1);
+  {
+    struct Row {
+      size_t l, i;
+    };
+    std::vector<Row> rows;
+    std::vector<HostFp> root_at(ys_l.size()), sx_at(ys_l.size());
+    std::vector<uint64_t> deg_at(ys_l.size());
+    HostFp rt = root;
+    uint64_t dg = rou_deg;
+    const uint8_t* mr = merkle_root_in;
+    for (size_t l = 0; l < ys_l.size(); ++l) {
+      root_at[l] = rt;
+      deg_at[l] = dg;
+      sx_at[l] = F.from_bytes_le(mr, 32);
+      for (size_t i = 0; i < ys_l[l].size(); ++i) rows.push_back({l, i});
+      mr = proof[l].root2;
+      rt = F.pow_u64(rt, 4);
+      dg /= 4;
+    }
+    std::vector<uint8_t> good(rows.size(), 0);
+    std::atomic<size_t> next{0};
+    host_parallel(std::max(1u, std::min<unsigned>(host_threads(), (unsigned)((rows.size() + 7) / 8))), [&](unsigned) {
+      for (size_t k; (k = next.fetch_add(4)) < rows.size();)
+        for (size_t q = k; q < std::min(rows.size(), k + 4); ++q) {
+          const size_t l = rows[q].l, i = rows[q].i;
+          const FriIn& L = proof[l];
+          const uint64_t y = ys_l[l][i], dl = deg_at[l];
+          // The cubic through (x1 zeta^j, row_j) at special_x (multi_interp_4 + eval_quartic,
+          // poly_utils.rs:442-511): Lagrange weights prod_{k != j}(sx - x_k) / (4 x1^3 zeta^(3j)).
+          const HostFp x1 = F.pow_u64(root_at[l], y);
+          const HostFp inv_x13 = F.pow_u64(root_at[l], (dl - (3 * y) % dl) % dl);
+          const HostFp& sx = sx_at[l];
+          HostFp xs[4], num[4];
+          for (int j = 0; j < 4; ++j) xs[j] = F.mul(quartic[j], x1);
+          for (int j = 0; j < 4; ++j) {
+            num[j] = F.one();
+            for (int t = 0; t < 4; ++t)
+              if (t != j) num[j] = F.mul(num[j], F.sub(sx, xs[t]));
+          }
+          const HostFp inv_den = F.mul(inv4, inv_x13);  // 1 / (4 x1^3); zeta^(-3j) = zeta^j
+          HostFp val = F.zero();
+          for (int j = 0; j < 4; ++j)
+            val = F.add(val, F.mul(F.mul(fe_from_bytes(L.poly[i * 4 + j].leaf), num[j]), F.mul(inv_den, quartic[j])));
+          good[q] = FieldHost::eq(val, fe_from_bytes(L.col[i].leaf));  // assert_eq (fri.rs:337)
+        }
+    });
+    for (size_t q = 0; q < rows.size(); ++q)
+      if (!good[q]) row_ok[rows[q].l] = 0;
   }
   for (size_t l = 0; l + 1 < proof.size(); ++l) {
     const FriIn& L = proof[l];
     if (L.last) return STARK_ERR_BAD_ARG;  // "FRI proofs must consist of FriProof::Middle except the last element."
-    const HostFp special_x = F.from_bytes_le(m_root, 32);
     if (l >= ys_l.size()) return STARK_ERR_CHECK;  // get_pseudorandom_indices panics
-    const std::vector<size_t>& ys = ys_l[l];
-    // x1 = root^y per row and 1 / x1^3 for all rows with one inversion (Montgomery's trick).
-    const size_t k_rows = ys.size();
-    std::vector<HostFp> x1s(k_rows), inv_x13(k_rows), pre(k_rows + 1);
-    pre[0] = F.one();
-    for (size_t i = 0; i < k_rows; ++i) {
-      x1s[i] = F.pow_u64(root, ys[i]);
-      pre[i + 1] = F.mul(pre[i], F.mul(F.mul(x1s[i], x1s[i]), x1s[i]));
-    }
-    HostFp acc_inv = F.inv(pre[k_rows]);  // every x1 is a root of unity, never zero
-    for (size_t i = k_rows; i-- > 0;) {
-      inv_x13[i] = F.mul(acc_inv, pre[i]);
-      acc_inv = F.mul(acc_inv, F.mul(F.mul(x1s[i], x1s[i]), x1s[i]));
-    }
-    for (size_t i = 0; i < ys.size(); ++i) {
-      // The cubic through (x1 zeta^j, row_j) at special_x (multi_interp_4 + eval_quartic,
-      // poly_utils.rs:442-511): Lagrange weights prod_{k != j}(sx - x_k) / (4 x1^3 zeta^(3j)).
-      const HostFp x1 = x1s[i];
-      HostFp xs[4], num[4];
-      for (int j = 0; j < 4; ++j) xs[j] = F.mul(quartic[j], x1);
-      for (int j = 0; j < 4; ++j) {
-        num[j] = F.one();
-        for (int k = 0; k < 4; ++k)
-          if (k != j) num[j] = F.mul(num[j], F.sub(special_x, xs[k]));
-      }
-      const HostFp inv_den = F.mul(inv4, inv_x13[i]);  // 1 / (4 x1^3); zeta^(-3j) = zeta^j
-      HostFp val = F.zero();
-      for (int j = 0; j < 4; ++j)
-        val = F.add(val, F.mul(F.mul(fe_from_bytes(L.poly[i * 4 + j].leaf), num[j]), F.mul(inv_den, quartic[j])));
-      if (!FieldHost::eq(val, fe_from_bytes(L.col[i].leaf))) return STARK_ERR_CHECK;  // assert_eq (fri.rs:337)
-    }
+    if (!row_ok[l]) return STARK_ERR_CHECK;          // a row's cubic disagrees with its column value
     memcpy(m_root, L.root2, 32);
     root = F.pow_u64(root, 4);
     max_deg_plus_1 /= 4;
@@ -526,42 +550,50 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
   for (uint64_t t = prec; t > 1; t /= 2)
     for (int l = 0; l < 4; ++l) pm1[l] = (pm1[l] >> 1) | (l < 3 ? pm1[l + 1] << 63 : 0);
   const HostFp g2 = F.pow(F.from_u64(7), pm1, 4);
-  // FRI on the linear combination (verify.rs:80-84).
-  stark_status st = verify_fri(pr.l_root, g2, pr.fri, prec / 4, (uint32_t)skips);
-  if (st != STARK_OK) return st;
-  clk.mark("FRI layers");
-  // Spot checks (verify.rs:86-118).
+  // FRI on the linear combination (verify.rs:80-84), then the spot checks' openings (verify.rs:86-118).
+  // Every Merkle path of both -- the FRI layers', the 320 main and 80 L openings -- is checked in one
+  // parallel pass inside verify_fri; the outcomes are reported in the reference's order.
   std::vector<size_t> positions, aug;
-  if (!sampler(pr.l_root, prec, 80, (uint32_t)skips, positions)) return STARK_ERR_CHECK;
-  for (size_t j : positions) {
-    aug.push_back(j);
-    aug.push_back((j + prec - skips) % prec);
-    aug.push_back((j + os / 3 * skips) % prec);
-    aug.push_back((j + os / 3 * 2 * skips) % prec);
-  }
-  if (pr.main.size() < aug.size() || pr.lcomb.size() < positions.size()) return STARK_ERR_CHECK;  // zip
-  {
-    std::vector<PathCheck> checks;
+  const bool sampled = sampler(pr.l_root, prec, 80, (uint32_t)skips, positions);
+  if (sampled)
+    for (size_t j : positions) {
+      aug.push_back(j);
+      aug.push_back((j + prec - skips) % prec);
+      aug.push_back((j + os / 3 * skips) % prec);
+      aug.push_back((j + os / 3 * 2 * skips) % prec);
+    }
+  // (zip: every index needs its opening)
+  const bool sized = sampled && pr.main.size() >= aug.size() && pr.lcomb.size() >= positions.size();
+  std::vector<PathCheck> checks;
+  if (sized) {
     for (size_t i = 0; i < aug.size(); ++i) checks.push_back({pr.m_root, aug[i], &pr.main[i]});
     for (size_t i = 0; i < positions.size(); ++i) checks.push_back({pr.l_root, positions[i], &pr.lcomb[i]});
-    if (!paths_valid(checks)) return STARK_ERR_CHECK;
   }
-  clk.mark("main + L Merkle paths");
-  for (size_t i = 0; i < aug.size(); ++i)
-    if (pr.main[i].leaf.size() < 256) return STARK_ERR_CHECK;  // m_branch[k] chunks (verify.rs:185-200)
   // K, F0-F2, IDX, PIDX at the positions: the circuit's extensions (K, F0-F2 stored as Montgomery
-  // images, IDX and PIDX canonical), gathered in one launch.
+  // images, IDX and PIDX canonical), gathered in one launch on the side thread while this one checks
+  // the paths and the FRI layers (the positions depend on l_root alone).
   const size_t n_pos = positions.size();
   std::vector<uint8_t> got(6 * n_pos * 32);
+  stark_status st_got = STARK_OK;
+  bool paths_ok = false;
+  stark_status st;
   {
-    stark_open_req req[6];
-    for (int k = 0; k < 6; ++k)
-      req[k] = stark_open_req{nullptr, (const uint8_t*)c.lde.ptr + (size_t)k * prec * 32, 32, prec,
-                              positions.data(), n_pos, got.data() + (size_t)k * n_pos * 32, nullptr};
-    st = stark_open_batch(ctx, req, 6, nullptr);
-    if (st != STARK_OK) return st;
+    HostTask gather([&] {
+      if (!sized) return;
+      stark_open_req req[6];
+      for (int k = 0; k < 6; ++k)
+        req[k] = stark_open_req{nullptr, (const uint8_t*)c.lde.ptr + (size_t)k * prec * 32, 32, prec,
+                                positions.data(), n_pos, got.data() + (size_t)k * n_pos * 32, nullptr};
+      st_got = stark_open_batch(ctx, req, 6, nullptr);
+    });
+    st = verify_fri(pr.l_root, g2, pr.fri, prec / 4, (uint32_t)skips, sized ? &checks : nullptr, &paths_ok);
   }
-  clk.mark("extension values gathered");
+  if (st != STARK_OK) return st;
+  clk.mark("FRI layers + main/L paths || gather");
+  if (!sized || !paths_ok) return STARK_ERR_CHECK;
+  for (size_t i = 0; i < aug.size(); ++i)
+    if (pr.main[i].leaf.size() < 256) return STARK_ERR_CHECK;  // m_branch[k] chunks (verify.rs:185-200)
+  if (st_got != STARK_OK) return st_got;
   auto col_val = [&](int k, size_t i) {
     HostFp v;
     memcpy(v.v, got.data() + ((size_t)k * n_pos + i) * 32, 32);

@@ -338,3 +338,39 @@ def test_cyclic_ntt_local_fused_twiddle(ctx, oracle, log_n, log_g, rank, inverse
         want.append(v * t % O.P)
         t = t * step % O.P
     assert got == want
+
+
+def _local_step_want(oracle, x, log_n, log_g, rank):
+    w = O.root_of_unity(log_n)
+    base = oracle.best_fft(x, pow(w, 1 << log_g, O.P), log_n - log_g, cpus=8)
+    step, want, t = pow(w, rank, O.P), [], 1
+    for v in O.from_limbs(base):
+        want.append(v * t % O.P)
+        t = t * step % O.P
+    return want
+
+
+@pytest.mark.parametrize("cap_units", [0, 1, 3])
+def test_cyclic_ntt_local_post_table_under_cache_cap(oracle, cap_units):
+    """the sender-side post table of G = 8 under a cache cap that cannot hold it
+    (0: built for the call and freed), or holds it or the last pass's full table but not both (1.5 and
+    3.5 x M x 32 B with other tables competing).  The table a transform is using is never evicted by
+    the full table that transform's last pass reserves; every result equals the oracle's."""
+    import stark_amd as S
+    log_n, log_g = 18, 3
+    M = 1 << (log_n - log_g)
+    c = S.Context(0)
+    try:
+        c.set_cache_limit(M * 32 * cap_units + M * 16)
+        for rank in (1, 6, 1):  # a second rank's table evicts (or replaces) the first's
+            x = O.random_elements(M, 0x5EED0900 + rank)
+            d = torch.from_numpy(x.view(np.int64).copy()).cuda()
+            torch.cuda.synchronize()
+            c.cyclic_ntt_local_dev(d.data_ptr(), log_n, log_g, rank, O.root_of_unity(log_n), stream=c.stream)
+            c.synchronize()
+            got = O.from_limbs(d.cpu().numpy().view(np.uint64).reshape(-1, 4))
+            assert got == _local_step_want(oracle, x, log_n, log_g, rank), (cap_units, rank)
+            m = c.memory()
+            assert m["cached"] <= m["cache_limit"], m
+    finally:
+        c.close()
