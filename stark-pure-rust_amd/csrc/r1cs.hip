@@ -99,6 +99,10 @@ struct Transcript {
   int err;
   // Digit-basis tables (fe_db.h) of L's constants: k0, k1, k2, k9, k10, then kx[t][c] at 5 + 3 t + c.
   uint32_t k_db[kLincombConsts][72];
+  // The constraint kernel's constants as digit-basis tables: r[1], r[2] (r1cs_r_kernel), and from the
+  // host (upload_constraint_tables) R^-1 (the x R^-1 scalings) and the partial-fraction coefficients a_k.
+  uint32_t r_db[2][72];
+  uint32_t c_db[33][72];  // R^-1 | a_0..a_7 | inv(Z) R^k at t = i mod 8, table 9 + 8 k + t (invz_m)
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -157,6 +161,12 @@ __global__ void r1cs_r_kernel(const uint32_t* __restrict__ a_root, uint32_t prec
   tr->r0 = r[0];
   tr->r1_m = fe_mul(r[1], r2);
   tr->r2_m = fe_mul(r[2], r2);
+  fe two32;  // canonical 2^32 -> its Montgomery image
+#pragma unroll
+  for (int i = 0; i < 8; ++i) two32.w[i] = i == 1;
+  const fe two32_m = fe_mul(two32, r2);
+  db_table_dev(r[1], two32_m, tr->r_db[0]);
+  db_table_dev(r[2], two32_m, tr->r_db[1]);
 #pragma unroll
   for (int i = 0; i < 8; ++i) tr->roots[0][i] = a_root[i];
 }
@@ -436,7 +446,20 @@ struct ConstraintArgs {
 // Q1/Q2/Q3 (utils.rs:181-248, 344-376) -> D1..D3 (utils.rs:379-418), I2/I3
 // evaluations (prove.rs:216-220), B2/B3 (utils.rs:477-524); one main-tree row
 // (prove.rs:235-258) per thread.
-__global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) {
+// (3 workgroups per CU: the digit-basis products need ~170 VGPRs; at 4 waves per SIMD they spill, at the
+// compiler's free choice of 180-217 VGPRs two waves per SIMD leave the loads uncovered:
+// 1.94 ms before the digit basis, 1.73 ms with it at this bound, 1.96-1.98 ms at the others,
+// profiles/r05_constraint_db_ab.txt)
+__global__ __launch_bounds__(256, 3) void r1cs_constraint_kernel(ConstraintArgs a) {
+  // The 24 inv(Z) R^k tables in LDS (a lane's t = i mod 8 picks its table): 76 words apart, so the 8
+  // tables a wave reads at once start on distinct 4-bank groups.
+  __shared__ __attribute__((aligned(16))) uint32_t izt[24 * 76];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&a.tr->c_db[9][0]);
+    for (uint32_t k = threadIdx.x; k < 24 * 18; k += blockDim.x)
+      reinterpret_cast<uint4*>(izt)[(k / 18) * 19 + k % 18] = src[k];
+    __syncthreads();
+  }
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.prec) return;
   const uint64_t n = a.prec, mask = n - 1;
@@ -451,7 +474,7 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   const fe* A = a.col[8];
   const uint64_t prev = (i + n - a.back) & mask;
   const uint64_t gi = a.g_add + (i << a.log_g);  // global evaluation point
-  const fe r0 = a.tr->r0, r1_m = a.tr->r1_m, r2_m = a.tr->r2_m;
+  const fe r0 = a.tr->r0;
   const fe p = fe_load(Pc + i), s = fe_load(S + i), av = fe_load(A + i);
   const fe p_prev = fe_load(Pc + prev), a_prev = fe_load(A + prev);
   const fe p2 = fe_load(Pc + ((i + a.shift1) & mask)), p3 = fe_load(Pc + ((i + a.shift2) & mask));
@@ -459,26 +482,30 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
   // formed at a scale R^-k and D = Q inv(Z) takes the inv(Z) R^k constant (zero tests are
   // scale-free).  Prepared circuits hold K, F0-F2 as Montgomery images: their products are exact.
   const bool mc = a.mont_cols != 0;
-  fe unit = fe_zero();
-  unit.w[0] = 1;                                  // canonical 1: fe_mul(x, unit) = x R^-1
+  // Products by the proof's constants (r1, r2, R^-1, the a_k below) by the digit basis from the
+  // transcript's tables (wave-uniform: scalar loads), each reduced once to canonical: the same values
+  // as the Montgomery products by their images, at about half the instructions.
+  const uint32_t* __restrict__ db_r1 = a.tr->r_db[0];
+  const uint32_t* __restrict__ db_r2 = a.tr->r_db[1];
+  const uint32_t* __restrict__ db_rinv = a.tr->c_db[0];
+  auto cmul = [](const fe& x, const uint32_t* __restrict__ w) {  // x w mod p, canonical (x < 4p)
+    fe y = fe_mul_db(x, w);
+    fe_reduce_once(y);
+    return y;
+  };
   const fe k_s = fe_mul(fe_load(K + i), s), f1_p = fe_mul(fe_load(F1 + i), p_prev);
-  const fe q1 = fe_mul(fe_load(F0 + i), fe_sub(fe_sub(mc ? p : fe_mul(p, unit), f1_p), k_s));  // R^-(mc ? 0 : 2)
-  const fe q2 = fe_mul(fe_load(F2 + i), fe_sub(fe_mul(p3, unit), fe_mul(p, p2)));            // R^-(mc ? 1 : 2)
-  const fe rs = fe_mul(s, r2_m);
-  const fe nmr = fe_add(fe_add(r0, fe_mul(fe_load(IDX + i), r1_m)), rs);
-  const fe dnm = fe_add(fe_add(r0, fe_mul(fe_load(PIDX + i), r1_m)), rs);
+  const fe q1 = fe_mul(fe_load(F0 + i), fe_sub(fe_sub(mc ? p : cmul(p, db_rinv), f1_p), k_s));  // R^-(mc ? 0 : 2)
+  const fe q2 = fe_mul(fe_load(F2 + i), fe_sub(cmul(p3, db_rinv), fe_mul(p, p2)));            // R^-(mc ? 1 : 2)
+  const fe rs = cmul(s, db_r2);
+  const fe nmr = fe_add(fe_add(r0, cmul(fe_load(IDX + i), db_r1)), rs);
+  const fe dnm = fe_add(fe_add(r0, cmul(fe_load(PIDX + i), db_r1)), rs);
   const fe q3 = fe_sub(fe_mul(av, dnm), fe_mul(a_prev, nmr));                                // R^-1
   const uint32_t t = (uint32_t)(gi & 7);
-  fe iz0 = a.invz_m[0][0], iz1 = a.invz_m[1][0], iz2 = a.invz_m[2][0];
-#pragma unroll
-  for (uint32_t k = 1; k < 8; ++k)
-    if (t == k) {
-      iz0 = a.invz_m[0][k];
-      iz1 = a.invz_m[1][k];
-      iz2 = a.invz_m[2][k];
-    }
   if (t == 0 && !(fe_is_zero(q1) && fe_is_zero(q2) && fe_is_zero(q3))) atomicOr(a.err, 1);
-  const fe d1 = fe_mul(q1, mc ? iz0 : iz2), d2 = fe_mul(q2, mc ? iz1 : iz2), d3 = fe_mul(q3, iz1);
+  auto iz = [&](uint32_t k) {  // the table of inv(Z) R^k at this t
+    return static_cast<const uint32_t*>(__builtin_assume_aligned(izt + 76 * (8 * k + t), 16));
+  };
+  const fe d1 = cmul(q1, iz(mc ? 0 : 2)), d2 = cmul(q2, iz(mc ? 1 : 2)), d3 = cmul(q3, iz(1));
   // I2 / I3 at x = g2^i (Horner; the interpolants are canonical).
   const fe x_m = pow_tab(a.lo, a.hi, a.kb, gi);
   // (Horner from the leading coefficient: the first step's 0 * x + c is c itself)
@@ -493,8 +520,11 @@ __global__ __launch_bounds__(256) void r1cs_constraint_kernel(ConstraintArgs a) 
     for (uint32_t k = 0; k < a.n_pf; ++k) {
       const uint64_t m = (i + n - a.pf_shift[k]) & mask;
       root = root || (m == 0 && a.g_add == 0);
-      izb2 = fe_add(izb2, fe_mul(a.pf_coef[k], fe_load(a.tinv + m)));
+      // a_k tinv (a Montgomery image times a canonical a_k: the image of the product), sum in [0, 2p)
+      izb2 = fe_add_raw(izb2, fe_mul_db(fe_load(a.tinv + m), a.tr->c_db[1 + k]));
+      fe_csub2p(izb2);
     }
+    fe_reduce_once(izb2);
     if (root) izb2 = fe_zero();
   } else {
     izb2 = fe_load(a.inv_zb + i);
@@ -904,6 +934,32 @@ static bool zb2_partial_fractions(const HostFp& g2, uint64_t prec, uint64_t skip
   return true;
 }
 
+// The host part of the transcript's c_db: R^-1, the partial-fraction coefficients a_k and the 24 inv(Z) R^k
+// constants (ca.pf_coef and ca.invz_m hold Montgomery images, which are the HostFp representation itself:
+// the tables are of the values the Montgomery products multiply by).  A pageable copy: the
+// runtime stages it before returning, so the table may live on this stack.
+static stark_status upload_constraint_tables(stark_ctx* ctx, Transcript* d_tr, const ConstraintArgs& ca,
+                                             hipStream_t s) {
+  const FieldHost& F = FieldHost::get();
+  uint32_t t[33][72];
+  db_table(F.inv(F.pow_u64(F.from_u64(2), 256)), t[0]);  // R^-1
+  const uint32_t n = ca.tinv ? ca.n_pf : 0;
+  for (uint32_t k = 0; k < 8; ++k) {
+    HostFp c;
+    if (k < n) memcpy(c.v, &ca.pf_coef[k], 32);
+    else c = F.zero();
+    db_table(c, t[1 + k]);
+  }
+  for (int k = 0; k < 3; ++k)
+    for (int u = 0; u < 8; ++u) {
+      HostFp c;
+      memcpy(c.v, &ca.invz_m[k][u], 32);
+      db_table(c, t[9 + 8 * k + u]);
+    }
+  STARK_HIP(ctx, hipMemcpyAsync(&d_tr->c_db[0][0], &t[0][0], sizeof t, hipMemcpyHostToDevice, s));
+  return STARK_OK;
+}
+
 static stark_status ext_index_column(stark_ctx* ctx, uint32_t log_steps, uint32_t log_prec, uint32_t log_g,
                                      uint32_t r, const Twiddles& tw_g1_inv, const Twiddles& tw_g2,
                                      const Twiddles& tw_h, hipStream_t s, const fe** out) {
@@ -1184,6 +1240,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   ca.tr = d_tr;
   set_inv_z(ca, g2, steps);
   ca.mont_cols = pre ? 1 : 0;
+  STARK_TRY(upload_constraint_tables(ctx, d_tr, ca, s));
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
   // Main tree over the 256-B rows (prove.rs:261-264), read as 8 column planes.
@@ -1663,6 +1720,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
       wt = F.mul(wt, w8);
     }
   }
+  STARK_TRY(upload_constraint_tables(ctx, d.d_tr, ca, s));
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(P)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
   // hc2 and the uploads above must outlive the copies: wait here (the caller
