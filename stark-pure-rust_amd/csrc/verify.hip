@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -29,9 +30,21 @@ namespace {
 
 // ---- the proof, as serde_json writes it (utils.rs:122-130, merkle_tree.rs:14-18, fri.rs:16-26) ----
 
+// Bytes held elsewhere: the proof text's arena (ProofIn::arena) or the caller's arrays.  A parsed proof
+// makes no allocation per opening (freeing ~3,600 small vectors written by 16 threads took ~0.27 ms of a
+// 1.35 ms pedersen verify, profiles/r05_verify_phases.txt).
+struct Bytes {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  const uint8_t* data() const { return p; }
+  size_t size() const { return n; }
+  const uint8_t* begin() const { return p; }
+  const uint8_t* end() const { return p + n; }
+};
+
 struct Branch {  // commitment::merkle_tree::Proof
-  std::vector<uint8_t> leaf;
-  std::vector<uint8_t> nodes;  // 32 B each, leaf -> root
+  Bytes leaf;
+  Bytes nodes;  // 32 B each, leaf -> root
 };
 
 struct FriIn {  // FriProof::Middle { root2, column_branches, poly_branches } | Last { last }
@@ -45,6 +58,9 @@ struct ProofIn {
   uint8_t m_root[32], l_root[32], a_root[32];
   std::vector<Branch> main, lcomb;
   std::vector<FriIn> fri;
+  // The openings' bytes: the opening whose text starts at offset t is written from arena + t / 2 (a
+  // number takes two characters at least, so openings never overlap).
+  std::unique_ptr<uint8_t[]> arena;
 };
 
 class Json;
@@ -63,8 +79,10 @@ struct PreBranches {
 // A reader for exactly this schema: objects with string keys, arrays, u8 numbers.
 class Json {
  public:
-  Json(const char* s, size_t n, PreBranches* pre = nullptr) : p_(s), e_(s + n), base_(s), pre_(pre) {}
-  Json(const char* base, size_t n, size_t at) : p_(base + at), e_(base + n), base_(base) {}
+  Json(const char* s, size_t n, PreBranches* pre = nullptr, uint8_t* arena = nullptr)
+      : p_(s), e_(s + n), base_(s), pre_(pre), arena_(arena) {}
+  Json(const char* base, size_t n, size_t at, uint8_t* arena)
+      : p_(base + at), e_(base + n), base_(base), arena_(arena) {}
   bool ok = true;
   size_t pos() const { return (size_t)(p_ - base_); }
 
@@ -88,10 +106,10 @@ class Json {
     expect(':');
     return k;
   }
-  // A u8 array.  Tight loop: serde_json writes no whitespace, so the separator is checked
-  // before falling back to the general whitespace skip.
-  void bytes(std::vector<uint8_t>& out) {
-    out.clear();
+  // A u8 array, each value handed to put (false: stop, malformed).  Tight loop: serde_json writes no
+  // whitespace, so the separator is checked before falling back to the general whitespace skip.
+  template <class Put>
+  void u8_array(Put put) {
     expect('[');
     if (!ok || accept(']')) return;
     ws();
@@ -102,11 +120,10 @@ class Json {
         v = 10 * v + (unsigned)(*p_++ - '0');
         ++nd;
       }
-      if (nd == 0 || v > 255) {
+      if (nd == 0 || v > 255 || !put((uint8_t)v)) {
         ok = false;
         return;
       }
-      out.push_back((uint8_t)v);
       if (p_ < e_ && *p_ == ',') {
         ++p_;
         if (p_ < e_ && (unsigned)(*p_ - '0') >= 10u) ws();
@@ -126,30 +143,52 @@ class Json {
       return;
     }
   }
+  void bytes(std::vector<uint8_t>& out) {
+    out.clear();
+    u8_array([&](uint8_t v) {
+      out.push_back(v);
+      return true;
+    });
+  }
+  // Into out[0..max): the count (a longer array is malformed).
+  size_t bytes_to(uint8_t* out, size_t max) {
+    size_t k = 0;
+    u8_array([&](uint8_t v) {
+      if (k == max) return false;
+      out[k++] = v;
+      return true;
+    });
+    return k;
+  }
   void digest(uint8_t out[32]) {
-    bytes(tmp_);  // reused buffer: no allocation per digest
-    if (tmp_.size() != 32) ok = false;
-    if (ok) memcpy(out, tmp_.data(), 32);
+    if (bytes_to(out, 32) != 32) ok = false;
   }
   void branch(Branch& b) {
+    if (!arena_) {
+      ok = false;
+      return;
+    }
+    uint8_t* w = arena_ + pos() / 2;  // this opening's part of the arena (ProofIn::arena)
     expect('{');
     bool has_leaf = false, has_nodes = false;
     do {
       const std::string k = key();
       if (k == "leaf") {
-        bytes(b.leaf);
+        const size_t n = bytes_to(w, (size_t)(e_ - p_) / 2 + 1);
+        b.leaf = Bytes{w, n};
+        w += n;
         has_leaf = true;
       } else if (k == "nodes") {
+        uint8_t* const n0 = w;
         expect('[');
         if (!accept(']')) {
-          b.nodes.reserve(32 * 32);
           do {
-            const size_t at = b.nodes.size();
-            b.nodes.resize(at + 32);
-            digest(b.nodes.data() + at);
+            digest(w);
+            w += 32;
           } while (ok && accept(','));
           expect(']');
         }
+        b.nodes = Bytes{n0, (size_t)(w - n0)};
         has_nodes = true;
       } else {
         ok = false;
@@ -260,11 +299,11 @@ class Json {
   const char* e_;
   const char* base_;
   PreBranches* pre_ = nullptr;
-  std::vector<uint8_t> tmp_;
+  uint8_t* arena_ = nullptr;
 };
 
 // Finds every Branch start and parses each from its offset on the host workers.
-void pre_parse_branches(const char* s, size_t n, PreBranches& P) {
+void pre_parse_branches(const char* s, size_t n, PreBranches& P, uint8_t* arena) {
   static const char kKey[] = "{\"leaf\":";
   const size_t klen = sizeof(kKey) - 1;
   const unsigned parts = n < ((size_t)1 << 18) ? 1u : host_threads();
@@ -289,7 +328,7 @@ void pre_parse_branches(const char* s, size_t n, PreBranches& P) {
   host_parallel(std::min<unsigned>(host_threads(), (unsigned)((k + 15) / 16)), [&](unsigned) {
     for (size_t c; (c = next.fetch_add(16)) < k;)
       for (size_t i = c; i < std::min(k, c + 16); ++i) {
-        Json j(s, n, P.off[i]);
+        Json j(s, n, P.off[i], arena);
         j.branch(P.br[i]);
         P.good[i] = j.ok;
         P.end[i] = j.pos();
@@ -300,14 +339,16 @@ void pre_parse_branches(const char* s, size_t n, PreBranches& P) {
 // ---- field helpers ----
 
 // T::from_bytes_le (ff_utils/src/fp.rs:70-77): the little-endian integer of the bytes mod p.
-HostFp fe_from_bytes(const std::vector<uint8_t>& b) {
+HostFp fe_from_bytes(const uint8_t* b, size_t n) {
   const FieldHost& F = FieldHost::get();
-  if (b.size() <= 32) return F.from_bytes_le(b.data(), b.size());
+  if (n <= 32) return F.from_bytes_le(b, n);
   HostFp acc = F.zero();
   const HostFp base = F.from_u64(256);
-  for (size_t i = b.size(); i-- > 0;) acc = F.add(F.mul(acc, base), F.from_u64(b[i]));
+  for (size_t i = n; i-- > 0;) acc = F.add(F.mul(acc, base), F.from_u64(b[i]));
   return acc;
 }
+HostFp fe_from_bytes(const std::vector<uint8_t>& b) { return fe_from_bytes(b.data(), b.size()); }
+HostFp fe_from_bytes(const Bytes& b) { return fe_from_bytes(b.data(), b.size()); }
 
 HostFp eval_poly(const std::vector<HostFp>& poly, const HostFp& x) {  // eval_poly_at, poly_utils.rs:93-102
   const FieldHost& F = FieldHost::get();
@@ -640,9 +681,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
   auto spot = [&](size_t i) -> bool {
     const HostFp x = F.pow_u64(g2, positions[i]);
     auto leaf = [&](int b, int chunk) {
-      std::vector<uint8_t> v(pr.main[4 * i + b].leaf.begin() + 32 * chunk,
-                             pr.main[4 * i + b].leaf.begin() + 32 * chunk + 32);
-      return fe_from_bytes(v);
+      return fe_from_bytes(pr.main[4 * i + b].leaf.data() + 32 * chunk, 32);
     };
     const HostFp p_x = leaf(0, 0), p_prev = leaf(1, 0), p_w = leaf(2, 0), p_2w = leaf(3, 0);
     const HostFp a_x = leaf(0, 1), a_prev = leaf(1, 1), s_x = leaf(0, 2), d1 = leaf(0, 3), d2 = leaf(0, 4),
@@ -713,9 +752,9 @@ stark_status stark_verify_low_degree_proof(const uint8_t merkle_root[32], const 
       std::vector<Branch>& out = which ? proof[l].poly : proof[l].col;
       if (B.k && (!B.leaves || (B.depth && !B.nodes))) return STARK_ERR_BAD_ARG;
       for (size_t i = 0; i < B.k; ++i) {
-        Branch b;
-        b.leaf.assign(B.leaves + i * B.leaf_len, B.leaves + (i + 1) * B.leaf_len);
-        b.nodes.assign(B.nodes + i * B.depth * 32, B.nodes + (i + 1) * B.depth * 32);
+        Branch b;  // (views into the caller's arrays, which outlive the call)
+        b.leaf = Bytes{B.leaves + i * B.leaf_len, B.leaf_len};
+        b.nodes = Bytes{B.depth ? B.nodes + i * B.depth * 32 : nullptr, B.depth * 32};
         out.push_back(std::move(b));
       }
     }
@@ -733,9 +772,10 @@ namespace stark {
 static bool read_proof(const char* proof_json, size_t json_len, ProofIn& pr) {
   PhaseClock clk("verify: read proof");
   PreBranches pre;
-  pre_parse_branches(proof_json, json_len, pre);
+  pr.arena.reset(new uint8_t[json_len / 2 + 64]);
+  pre_parse_branches(proof_json, json_len, pre, pr.arena.get());
   clk.mark("openings parsed (parallel)");
-  Json j(proof_json, json_len, &pre);
+  Json j(proof_json, json_len, &pre, pr.arena.get());
   j.stark_proof(pr);
   clk.mark("StarkProof JSON parsed");
   return j.ok;
@@ -770,16 +810,20 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
   PhaseClock clk("verify: circuit");
   // The proof is read on the side thread while this one builds the circuit (mostly device work and
   // its synchronisations): the two do not depend on each other.
-  ProofIn pr;
+  auto pr = std::make_unique<ProofIn>();
   bool parsed = false;
   stark_status st;
   {
-    HostTask read([&] { parsed = read_proof(proof_json, json_len, pr); });
+    HostTask read([&] { parsed = read_proof(proof_json, json_len, *pr); });
     st = circuit_build(ctx, r1cs, r1cs_len, circ.c);
     clk.mark("circuit build (proof read beside it)");
   }
+  clk.mark("proof read joined");
   if (st == STARK_OK && !parsed) st = STARK_ERR_BAD_ARG;  // serde_json::from_reader fails (run.rs:579)
-  if (st == STARK_OK) st = verify_r1cs(ctx, circ.c, public_wires, n_public, pr);
+  if (st == STARK_OK) st = verify_r1cs(ctx, circ.c, public_wires, n_public, *pr);
+  clk.mark("verify_r1cs returned");
+  pr.reset();
+  clk.mark("proof freed");
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
   return st;
