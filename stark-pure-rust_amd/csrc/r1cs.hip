@@ -121,54 +121,64 @@ __device__ __forceinline__ void b2s_short(const uint32_t* w, uint32_t extra_byte
 
 // The digit-basis table of a canonical constant c: limb j of c 2^(32 i) mod p at 9 i + j (two32_m = the
 // Montgomery image of 2^32, so fe_mul(c, two32_m) = c 2^32 mod p).
+__device__ __forceinline__ void db_limbs(const fe& c, uint32_t* __restrict__ out) {  // 9 x 29-bit limbs of c
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int bit = 29 * j, w = bit >> 5, sh = bit & 31;
+    uint32_t v = c.w[w] >> sh;
+    if (sh > 3 && w < 7) v |= c.w[w + 1] << (32 - sh);
+    out[j] = v & STARK_DB_M29;
+  }
+}
 __device__ void db_table_dev(fe c, const fe& two32_m, uint32_t* __restrict__ out) {
   for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int bit = 29 * j, w = bit >> 5, sh = bit & 31;
-      uint32_t v = c.w[w] >> sh;
-      if (sh > 3 && w < 7) v |= c.w[w + 1] << (32 - sh);
-      out[9 * i + j] = v & STARK_DB_M29;
-    }
+    db_limbs(c, out + 9 * i);
     c = fe_mul(c, two32_m);
   }
 }
+
+// Montgomery images of 2^(32 i) mod p, i < 8: a digit-basis table's rows as independent products.
+struct Pow32 {
+  fe m[8];
+};
 
 // r = get_random_ff_values(a_root, precision, 3, 0) (utils.rs:272-290):
 // get_pseudorandom_indices(seed, precision, 24, 0) (fri/src/utils.rs:82-109)
 // expands seed || B(seed) || B(B(seed)), reads 24 big-endian words mod
 // precision; each group of 8 is written as big-endian bytes and read back
 // with from_bytes_le (mod p).
-__global__ void r1cs_r_kernel(const uint32_t* __restrict__ a_root, uint32_t prec_mask, fe r2,
+__global__ void r1cs_r_kernel(const uint32_t* __restrict__ a_root, uint32_t prec_mask, fe r2, Pow32 p32,
                               Transcript* __restrict__ tr) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t data[24];
+  __shared__ fe rs[2];
+  if (threadIdx.x == 0) {
+    uint32_t data[24];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) data[i] = a_root[i];
-  b2s_short(data, 0, 32, data + 8);
-  b2s_short(data + 8, 0, 32, data + 16);
-  fe r[3];
+    for (int i = 0; i < 8; ++i) data[i] = a_root[i];
+    b2s_short(data, 0, 32, data + 8);
+    b2s_short(data + 8, 0, 32, data + 16);
+    fe r[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < 3; ++c) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t v = bswap32(data[8 * c + i]) & prec_mask;  // BE word mod 2^k
-      r[c].w[i] = bswap32(v);                                  // BE bytes read as LE words
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t v = bswap32(data[8 * c + i]) & prec_mask;  // BE word mod 2^k
+        r[c].w[i] = bswap32(v);                                  // BE bytes read as LE words
+      }
+#pragma unroll
+      for (int k = 0; k < 5; ++k) fe_reduce_once(r[c]);
     }
+    tr->r0 = r[0];
+    tr->r1_m = fe_mul(r[1], r2);
+    tr->r2_m = fe_mul(r[2], r2);
+    rs[0] = r[1];
+    rs[1] = r[2];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) fe_reduce_once(r[c]);
+    for (int i = 0; i < 8; ++i) tr->roots[0][i] = a_root[i];
   }
-  tr->r0 = r[0];
-  tr->r1_m = fe_mul(r[1], r2);
-  tr->r2_m = fe_mul(r[2], r2);
-  fe two32;  // canonical 2^32 -> its Montgomery image
-#pragma unroll
-  for (int i = 0; i < 8; ++i) two32.w[i] = i == 1;
-  const fe two32_m = fe_mul(two32, r2);
-  db_table_dev(r[1], two32_m, tr->r_db[0]);
-  db_table_dev(r[2], two32_m, tr->r_db[1]);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) tr->roots[0][i] = a_root[i];
+  __syncthreads();
+  // The digit-basis tables of r[1], r[2] (the constraint kernel's): one row r 2^(32 i) per thread.
+  const uint32_t t = threadIdx.x;
+  if (t < 16) db_limbs(fe_mul(rs[t >> 3], p32.m[t & 7]), tr->r_db[t >> 3] + 9 * (t & 7));
 }
 
 // (g2^steps)^t, t < 8: the x^steps factor of L at the points i = t mod 8 (prove.rs:287-291).
@@ -938,6 +948,18 @@ static bool zb2_partial_fractions(const HostFp& g2, uint64_t prec, uint64_t skip
 // constants (ca.pf_coef and ca.invz_m hold Montgomery images, which are the HostFp representation itself:
 // the tables are of the values the Montgomery products multiply by).  A pageable copy: the
 // runtime stages it before returning, so the table may live on this stack.
+static Pow32 pow32() {
+  const FieldHost& F = FieldHost::get();
+  Pow32 p;
+  HostFp x = F.one();
+  const HostFp t = F.from_u64((uint64_t)1 << 32);
+  for (int i = 0; i < 8; ++i) {
+    p.m[i] = to_dev(x);
+    x = F.mul(x, t);
+  }
+  return p;
+}
+
 static stark_status upload_constraint_tables(stark_ctx* ctx, Transcript* d_tr, const ConstraintArgs& ca,
                                              hipStream_t s) {
   const FieldHost& F = FieldHost::get();
@@ -1161,24 +1183,29 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(ctx_tree(ctx, 3, &m_tree));
   STARK_TRY(ctx_tree(ctx, 4, &l_tree));
   STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
-  if (pre)  // S and P only: K, the flags, IDX and PIDX are the circuit's
-    STARK_TRY(lde(ctx, raw + 4 * steps, 2, cols + 4 * prec, log_steps, log_prec, *tw1i, *tw2, s));
-  else if (f0_ext)  // K (in F0's slot) F1 F2 S P PIDX
-    STARK_TRY(lde(ctx, raw + steps, 6, cols + prec, log_steps, log_prec, *tw1i, *tw2, s));
-  else  // K F0 F1 F2 S P PIDX
-    STARK_TRY(lde(ctx, raw, 7, cols, log_steps, log_prec, *tw1i, *tw2, s));
-  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(acc_tree),
-                     (uint32_t)(prec - 1), mc.r2, d_tr);
+  // A (utils.rs:293-339, prove.rs:183-184): r from a_root, the running products of the numerators and
+  // denominators over the steps, their batch inverse (whose top level is the proof's one mid-pipeline host
+  // round trip) and A = nmr / dnm.  It reads the trace and a_root only (IDX and PIDX at the step points
+  // are i and the permutation), so when no Zb inverse shares its round trip it runs on the aux stream
+  // beside the main LDE, which the host enqueues before it waits.
+  const bool a_aside = pre || ca.tinv;
+  if (!ctx->ev_aux) STARK_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_aux, hipEventDisableTiming));
+  if (!ctx->aux) STARK_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  hipStream_t sa = s;
+  if (a_aside) {
+    sa = ctx->aux;
+    STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, s));  // the trace columns, the transcript's zero fill, a_root
+    STARK_HIP(ctx, hipStreamWaitEvent(sa, ctx->ev_aux, 0));
+  }
+  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, sa, (const uint32_t*)merkle_root_dev(acc_tree),
+                     (uint32_t)(prec - 1), mc.r2, pow32(), d_tr);
   STARK_HIP(ctx, hipGetLastError());
-  // A (utils.rs:293-339, prove.rs:183-184).
-  const fe* ext_idx = pre ? pre + 4 * prec : idx_ext;
-  const fe* ext_pidx = pre ? pre + 5 * prec : cols + 6 * prec;
-  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)ext_idx,
-                     (const fe*)ext_pidx, (const uint64_t*)nullptr, (uint64_t)0, (const fe*)wcopy, steps,
+  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, sa, (const fe*)nullptr,
+                     (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
                      (const Transcript*)d_tr, mc.r2, nmr, dnm);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
-  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
+  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, sa));
+  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, sa));
   // The cold proof's two batch inverses (the A denominators over the steps; Zb2, Zb3 over the precision
   // domain, which prepared circuits carry) share one host round trip: both up passes, one
   // synchronisation, both top levels on the host, then the down passes.
@@ -1187,7 +1214,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   fe* const top_z = multi_inv_h_top(ctx, 1);
   if (!top_d || !top_z) return STARK_ERR_OOM;
   // (io2's guard covers the pinned top arrays too: multi_inv_device on another stream uses both)
-  STARK_TRY(buf_acquire(ctx, ctx->io2, s));
+  STARK_TRY(buf_acquire(ctx, ctx->io2, sa));
   if (!pre && !ca.tinv) {
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, prec,
                        (uint64_t)0, (uint32_t)0, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
@@ -1195,17 +1222,30 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     STARK_HIP(ctx, hipGetLastError());
     STARK_TRY(multi_inv_up(ctx, zb, inv_zb, izb3 ? prec : 2 * prec, s, ctx->io2, top_z, inv_z));
   }
-  STARK_TRY(multi_inv_up(ctx, dnm_c, inv_dnm, steps, s, ctx->inv_tmp, top_d, inv_d));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
+  STARK_TRY(multi_inv_up(ctx, dnm_c, inv_dnm, steps, sa, ctx->inv_tmp, top_d, inv_d));
+  if (pre)  // S and P only: K, the flags, IDX and PIDX are the circuit's
+    STARK_TRY(lde(ctx, raw + 4 * steps, 2, cols + 4 * prec, log_steps, log_prec, *tw1i, *tw2, s));
+  else if (f0_ext)  // K (in F0's slot) F1 F2 S P PIDX
+    STARK_TRY(lde(ctx, raw + steps, 6, cols + prec, log_steps, log_prec, *tw1i, *tw2, s));
+  else  // K F0 F1 F2 S P PIDX
+    STARK_TRY(lde(ctx, raw, 7, cols, log_steps, log_prec, *tw1i, *tw2, s));
+  STARK_HIP(ctx, hipStreamSynchronize(sa));
   multi_inv_top(inv_d);
   multi_inv_top(inv_z);
-  STARK_TRY(multi_inv_down(ctx, inv_d, s));
-  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
-                     (const fe*)inv_dnm, steps, raw);
+  STARK_TRY(multi_inv_down(ctx, inv_d, sa));
+  // A = nmr / dnm into dnm (free after its scan's canonical copy)
+  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, sa, (const fe*)nmr,
+                     (const fe*)inv_dnm, steps, dnm);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(lde(ctx, raw, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
+  STARK_TRY(buf_release(ctx, ctx->io2, sa));
+  if (a_aside) {
+    STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, sa));
+    STARK_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_aux, 0));
+  }
+  STARK_TRY(lde(ctx, dnm, 1, cols + 7 * prec, log_steps, log_prec, *tw1i, *tw2, s));  // A in slot 7
   STARK_TRY(multi_inv_down(ctx, inv_z, s));  // (empty plan with a prepared circuit)
-  STARK_TRY(buf_release(ctx, ctx->io2, s));
+  const fe* ext_idx = pre ? pre + 4 * prec : idx_ext;
+  const fe* ext_pidx = pre ? pre + 5 * prec : cols + 6 * prec;
 
   // Constraint kernel.
   for (int c = 0; c < 6; ++c) ca.col[c] = cols + (size_t)c * prec;
@@ -1659,7 +1699,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   else  // K F0 F1 F2 S P PIDX
     STARK_TRY(lde_coset(d, raw, 7, cols, *tw1i, *tw2, *twh));
   hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
-                     (uint32_t)(prec - 1), mc.r2, d.d_tr);
+                     (uint32_t)(prec - 1), mc.r2, pow32(), d.d_tr);
   STARK_HIP(ctx, hipGetLastError());
   // A (utils.rs:293-339): step-domain scans on every rank, then this rank's coset.
   hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nullptr,
