@@ -1692,27 +1692,45 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
   STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
   STARK_TRY(merkle_build(ctx, d.acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
+  // A (utils.rs:293-339): step-domain scans on every rank, then this rank's coset.  As on one GPU, the
+  // chain (r, the scans, their batch inverse with its host round trip, A = nmr / dnm) runs on the
+  // context's aux stream beside the coset LDE, which the host enqueues before it waits.
+  if (!ctx->ev_aux) STARK_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_aux, hipEventDisableTiming));
+  if (!ctx->aux) STARK_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  hipStream_t sa = ctx->aux;
+  STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, s));  // the trace columns, the transcript's zero fill, a_root
+  STARK_HIP(ctx, hipStreamWaitEvent(sa, ctx->ev_aux, 0));
+  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, sa, (const uint32_t*)merkle_root_dev(d.acc_tree),
+                     (uint32_t)(prec - 1), mc.r2, pow32(), d.d_tr);
+  STARK_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, sa, (const fe*)nullptr,
+                     (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
+                     (const Transcript*)d.d_tr, mc.r2, nmr, dnm);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, sa));
+  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, sa));
+  InvPlan inv_d;
+  fe* const top_d = multi_inv_h_top(ctx, 0);
+  if (!top_d) return STARK_ERR_OOM;
+  STARK_TRY(buf_acquire(ctx, ctx->io2, sa));  // (io2's guard covers the pinned top arrays too)
+  STARK_TRY(multi_inv_up(ctx, dnm_c, inv_dnm, steps, sa, ctx->io2, top_d, inv_d));
   if (pre)
     STARK_TRY(lde_coset(d, raw + 4 * steps, 2, cols + 4 * P, *tw1i, *tw2, *twh));
   else if (f0_ext)  // K (in F0's slot) F1 F2 S P PIDX
     STARK_TRY(lde_coset(d, raw + steps, 6, cols + P, *tw1i, *tw2, *twh));
   else  // K F0 F1 F2 S P PIDX
     STARK_TRY(lde_coset(d, raw, 7, cols, *tw1i, *tw2, *twh));
-  hipLaunchKernelGGL(r1cs_r_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(d.acc_tree),
-                     (uint32_t)(prec - 1), mc.r2, pow32(), d.d_tr);
+  STARK_HIP(ctx, hipStreamSynchronize(sa));
+  multi_inv_top(inv_d);
+  STARK_TRY(multi_inv_down(ctx, inv_d, sa));
+  // A = nmr / dnm into dnm (free after its scan's canonical copy; raw may still be read by the LDE)
+  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, sa, (const fe*)nmr,
+                     (const fe*)inv_dnm, steps, dnm);
   STARK_HIP(ctx, hipGetLastError());
-  // A (utils.rs:293-339): step-domain scans on every rank, then this rank's coset.
-  hipLaunchKernelGGL(r1cs_a_vals_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nullptr,
-                     (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
-                     (const Transcript*)d.d_tr, mc.r2, nmr, dnm);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, s));
-  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, s));
-  STARK_TRY(multi_inv_device(ctx, dnm_c, inv_dnm, steps, s));
-  hipLaunchKernelGGL(r1cs_a_mini_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const fe*)nmr,
-                     (const fe*)inv_dnm, steps, raw);
-  STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(lde_coset(d, raw, 1, cols + 7 * P, *tw1i, *tw2, *twh));  // A in slot 7
+  STARK_TRY(buf_release(ctx, ctx->io2, sa));
+  STARK_HIP(ctx, hipEventRecord(ctx->ev_aux, sa));
+  STARK_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_aux, 0));
+  STARK_TRY(lde_coset(d, dnm, 1, cols + 7 * P, *tw1i, *tw2, *twh));  // A in slot 7
   if (!pre && !ca.tinv) {  // Zb2 / Zb3 at this rank's points and their inverses
     hipLaunchKernelGGL(r1cs_zb_kernel, dim3(blocks_for(P)), dim3(256), 0, s, tw2->d_lo, tw2->d_hi, tw2->kb, P,
                        (uint64_t)rank, d.log_g, (const fe*)consts, (uint32_t)n_pfi, to_dev(x_last), mc.rinv, mc.one,
