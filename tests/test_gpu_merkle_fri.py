@@ -99,7 +99,8 @@ def test_golden_fri(ctx, oracle):
         assert hashlib.sha256(js.encode()).hexdigest() == v["json_sha256"]
 
 
-@pytest.mark.parametrize("log_n,excl,deg_div", [(7, 8, 4), (12, 8, 4), (14, 0, 4), (16, 8, 8), (13, 8, 4096)])
+@pytest.mark.parametrize("log_n,excl,deg_div", [(7, 8, 4), (12, 8, 4), (14, 0, 4), (16, 8, 8), (13, 8, 4096),
+                                                  (11, 3, 4), (10, 2, 4)])
 def test_fri_vs_oracle(ctx, oracle, log_n, excl, deg_div):
     n = 1 << log_n
     w = O.root_of_unity(log_n)

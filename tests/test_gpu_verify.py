@@ -127,6 +127,42 @@ def test_malformed_json_raises(ctx, proofs):
             verify_with_wtns(ctx, r1, wt, bad)
 
 
+def test_json_reader_arena_edges(ctx, proofs):
+    """The proof reader writes every opening's bytes into one arena sized from the text (a number takes
+    two characters at least).  Whitespace anywhere serde_json allows it still verifies (the reader
+    accepts it as serde_json does); adversarial texts -- truncations at many points, short and long
+    digests, over-long leaves of one-digit numbers, 4-digit numbers -- are refused (StarkError or
+    AssertionError), never a crash or an acceptance."""
+    from stark_amd import StarkError
+    from stark_amd.verify import verify_with_wtns
+    r1, wt, js = proofs["pedersen_test"]
+    spaced = js.replace(",", ", ").replace(":", " : ").replace("[", "[ ")
+    assert verify_with_wtns(ctx, r1, wt, spaced)
+    q = json.loads(js)
+    bad = []
+    for cut in range(7, len(js), max(1, len(js) // 23)):
+        bad.append(js[:cut])
+    b = json.loads(js)
+    b["main_branches"][3]["nodes"][2] = [1]  # a short digest
+    bad.append(json.dumps(b, separators=(",", ":")))
+    b = json.loads(js)
+    b["main_branches"][5]["nodes"][0] = list(range(33))  # a long digest
+    bad.append(json.dumps(b, separators=(",", ":")))
+    b = json.loads(js)
+    b["linear_comb_branches"][1]["leaf"] = [1] * 5000  # a long leaf of one-digit numbers
+    bad.append(json.dumps(b, separators=(",", ":")))
+    b = json.loads(js)
+    b["fri_proof"][0]["Middle"]["poly_branches"][7]["nodes"] = [[1] * 32] * 4000  # many nodes
+    bad.append(json.dumps(b, separators=(",", ":")))
+    bad.append(js.replace("[", "[0255,", 1))
+    bad.append(js.replace("]]", "],[]]", 3))
+    assert q["main_branches"]  # (the fixture is a full proof)
+    for t in bad:
+        with pytest.raises((StarkError, AssertionError)):
+            verify_with_wtns(ctx, r1, wt, t)
+    assert verify_with_wtns(ctx, r1, wt, js)  # the context is still good
+
+
 def test_prepared_circuit_verifies_many(ctx):
     """R1csCircuit + verify_circuit on a synthetic 2^13-step circuit, two witnesses."""
     import synth_r1cs

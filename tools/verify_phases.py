@@ -1,5 +1,6 @@
 """Host phase times of the cold verifier (STARK_PROFILE=1 prints the library's phase clock on stderr):
-prove pedersen_test once, then verify_with_wtns N times, printing each call's wall-clock."""
+prove a fixture (or `synthK`, the synthetic 2^K-step circuit) once, then verify_with_wtns N times, printing
+each call's wall-clock.   python tools/verify_phases.py [pedersen_test | synth20] [N]"""
 import os
 import sys
 import time
@@ -15,9 +16,14 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "pedersen_test"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     ctx = S.Context(0)
-    fix = os.path.join(ROOT, "tests", "golden", "r1cs")
-    r1 = open(os.path.join(fix, f"{name}.r1cs"), "rb").read()
-    wt = open(os.path.join(fix, f"{name}.wtns"), "rb").read()
+    if name.startswith("synth"):  # synthK: the synthetic 2^K-step circuit (tools/synth_r1cs.py)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import synth_r1cs
+        r1, wt = synth_r1cs.for_steps(int(name[5:]))
+    else:
+        fix = os.path.join(ROOT, "tests", "golden", "r1cs")
+        r1 = open(os.path.join(fix, f"{name}.r1cs"), "rb").read()
+        wt = open(os.path.join(fix, f"{name}.wtns"), "rb").read()
     js = prove_with_witness(ctx, r1, wt).to_json().encode()
     for i in range(reps):
         t = time.perf_counter()
