@@ -360,7 +360,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // which reads only the first six and evaluates Zb2 / Zb3 at its spot positions): 6 x P, no inverses.
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s, bool with_zb = true);
+                         hipStream_t s, bool with_zb = true, const fe** colp = nullptr);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                     size_t os, const uint64_t* public_wires, size_t n_public,
@@ -382,6 +382,9 @@ struct PreparedCircuit {
   uint32_t n_c = 0;
   uint32_t world = 1, rank = 0;  // the points rank + world j of the precision domain (distributed prover)
   bool with_zb = true;           // false: lde holds K F0 F1 F2 IDX PIDX only (the verifier's cold build)
+  // Where the six columns K F0 F1 F2 IDX PIDX are (slots of lde, or for the verifier's cold build
+  // K's slot 1 and the shared F0 / IDX extensions); K F0-F2 are Montgomery images iff with_zb.
+  const fe* col[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   uint64_t a_len = 0;
   std::vector<size_t> pfi;
   const uint32_t* base = nullptr;

@@ -1426,8 +1426,13 @@ __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, 
 // are the device trace builder's circuit columns (os slots).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s, bool with_zb) {
+                         hipStream_t s, bool with_zb, const fe** colp) {
   const FieldHost& F = FieldHost::get();
+  // with_zb = false (the verifier's cold build, which gathers six values per spot position): the columns
+  // stay where they are made -- K's extension in slot 1, F0's and IDX's in their shared entries -- with
+  // no slot copies and no Montgomery images (colp tells the caller where each one is).
+  const bool verify_only = !with_zb;
+  const fe* col[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
     return STARK_ERR_BAD_ARG;
   uint32_t log_g = 0;
@@ -1470,17 +1475,26 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
         st = STARK_ERR_HIP;
       if (st == STARK_OK)
         st = coset_lde(ctx, raw + steps, 3, o + P, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
-      if (st == STARK_OK && (hipMemcpyAsync(o, o + P, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess ||
-                             hipMemcpyAsync(o + P, f0_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess))
+      if (st == STARK_OK && !verify_only &&
+          (hipMemcpyAsync(o, o + P, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+           hipMemcpyAsync(o + P, f0_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess))
         st = STARK_ERR_HIP;
+      col[0] = verify_only ? o + P : o;
+      col[1] = verify_only ? f0_ext : o + P;
     } else if (st == STARK_OK) {
       st = coset_lde(ctx, raw, 4, o, log_steps, log_prec, log_g, rank, *tw1i, *tw2, *twh, s);
+      col[0] = o;
+      col[1] = o + P;
     }
+    col[2] = o + 2 * P;
+    col[3] = o + 3 * P;
+    col[4] = verify_only ? idx_ext : o + 4 * P;
+    col[5] = o + 5 * P;
     if (st == STARK_OK)
       st = coset_lde(ctx, raw + 5 * steps, 1, (fe*)out.ptr + 5 * P, log_steps, log_prec, log_g, rank, *tw1i, *tw2,
                      *twh, s);
-    if (st == STARK_OK && hipMemcpyAsync((fe*)out.ptr + 4 * P, idx_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) !=
-                              hipSuccess)
+    if (st == STARK_OK && !verify_only &&
+        hipMemcpyAsync((fe*)out.ptr + 4 * P, idx_ext, P * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess)
       st = STARK_ERR_HIP;
     // Zb2 = prod_k (x - x_k), Zb3 = x - x_last (utils.rs:438-474) and their inverses (0 -> 0).
     const uint64_t skips = prec / steps;
@@ -1498,13 +1512,15 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                          to_dev(F.pow_u64(g2, prec - skips)), mc.rinv, mc.one, zb, zb + P);
       st = multi_inv_device(ctx, zb, (fe*)out.ptr + 6 * P, 2 * P, s);
     }
-    if (st == STARK_OK) {  // K, F0-F2 as Montgomery images (ConstraintArgs::mont_cols; the Zb inverses are)
+    if (st == STARK_OK && !verify_only) {  // K, F0-F2 as Montgomery images (ConstraintArgs::mont_cols; the Zb inverses are)
       hipLaunchKernelGGL(to_mont_kernel, dim3(blocks_for(4 * P)), dim3(256), 0, s, o, 4 * P, mc.r2);
       if (hipGetLastError() != hipSuccess) st = STARK_ERR_HIP;
     }
     if (st == STARK_OK && hipStreamSynchronize(s) != hipSuccess) st = STARK_ERR_HIP;
   }
   hipStreamSynchronize(s);  // tmp (a context buffer) is free for the next call
+  if (colp)
+    for (int k = 0; k < 6; ++k) colp[k] = col[k];
   return st;
 }
 

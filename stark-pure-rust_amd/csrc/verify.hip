@@ -610,9 +610,10 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     for (size_t i = 0; i < aug.size(); ++i) checks.push_back({pr.m_root, aug[i], &pr.main[i]});
     for (size_t i = 0; i < positions.size(); ++i) checks.push_back({pr.l_root, positions[i], &pr.lcomb[i]});
   }
-  // K, F0-F2, IDX, PIDX at the positions: the circuit's extensions (K, F0-F2 stored as Montgomery
-  // images, IDX and PIDX canonical), gathered in one launch on the side thread while this one checks
-  // the paths and the FRI layers (the positions depend on l_root alone).
+  // K, F0-F2, IDX, PIDX at the positions: the circuit's extensions (K, F0-F2 as Montgomery images in a
+  // prover's prepared circuit, canonical in the verifier's cold build; IDX and PIDX canonical), gathered
+  // in one launch on the side thread while this one checks the paths and the FRI layers (the positions
+  // depend on l_root alone).
   const size_t n_pos = positions.size();
   std::vector<uint8_t> got(6 * n_pos * 32);
   stark_status st_got = STARK_OK;
@@ -623,8 +624,8 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
       if (!sized) return;
       stark_open_req req[6];
       for (int k = 0; k < 6; ++k)
-        req[k] = stark_open_req{nullptr, (const uint8_t*)c.lde.ptr + (size_t)k * prec * 32, 32, prec,
-                                positions.data(), n_pos, got.data() + (size_t)k * n_pos * 32, nullptr};
+        req[k] = stark_open_req{nullptr, (const uint8_t*)c.col[k], 32, prec, positions.data(), n_pos,
+                              got.data() + (size_t)k * n_pos * 32, nullptr};
       st_got = stark_open_batch(ctx, req, 6, nullptr);
     });
     st = verify_fri(pr.l_root, g2, pr.fri, prec / 4, (uint32_t)skips, sized ? &checks : nullptr, &paths_ok);
@@ -639,7 +640,7 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
     HostFp v;
     memcpy(v.v, got.data() + ((size_t)k * n_pos + i) * 32, 32);
     while (FieldHost::ge_p(v.v)) FieldHost::sub_p_in_place(v.v);
-    return k < 4 ? v : F.from_canonical(v.v);  // a Montgomery image's bits are the HostFp itself
+    return k < 4 && c.with_zb ? v : F.from_canonical(v.v);  // a Montgomery image's bits are the HostFp itself
   };
   // Boundary interpolants (verify.rs:151-155, utils.rs:421-474) and Zb2's points.
   std::vector<HostFp> bx, by;
