@@ -182,3 +182,33 @@ def test_prepared_circuit_verifies_many(ctx):
         q["linear_comb_branches"][0]["leaf"][1] ^= 1
         with pytest.raises(AssertionError):
             verify_circuit(ctx, c, pub, q)
+
+
+def test_cold_verify_under_cache_caps(proofs):
+    """The cold verifier gathers K, F0 and IDX at the spot positions from where their extensions are made
+    (csrc/r1cs.hip circuit_lde, verify_only): F0's and IDX's from the context's shared cache when it holds
+    them, F0 from its own slot and IDX from the per-context buffer when the cap refuses them (cap 0), or
+    when each reservation evicts the previous column (cap of one column).  Every case accepts the golden
+    proof and rejects a tampered one; the prover's digest is unchanged afterwards."""
+    import stark_amd as S
+    from stark_amd.r1cs import prove_with_witness
+    from stark_amd.verify import verify_with_wtns
+    r1, wt, js = proofs["compute"]
+    col = 128 * 32  # one extension: os = 15 -> 16 steps -> precision 128
+    bad = json.loads(js)
+    bad["linear_comb_branches"][0]["leaf"][1] ^= 1
+    for cap in (None, 0, col):
+        c = S.Context(0)
+        try:
+            if cap is not None:
+                c.set_cache_limit(cap)
+            for _ in range(2):  # the second call finds whatever the first one cached
+                assert verify_with_wtns(c, r1, wt, js), cap
+                with pytest.raises(AssertionError):
+                    verify_with_wtns(c, r1, wt, bad)
+            if cap is not None:
+                assert c.memory()["cached"] <= cap
+            js2 = prove_with_witness(c, r1, wt).to_json()
+            assert hashlib.sha256(js2.encode()).hexdigest() == GOLDEN["compute"]["json_sha256"], cap
+        finally:
+            c.close()
