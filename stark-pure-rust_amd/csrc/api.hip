@@ -486,7 +486,7 @@ void stark_ctx_destroy(stark_ctx* ctx) {
   if (ctx->aux) hipStreamDestroy(ctx->aux);
   ctx->fri_trees.clear();
   for (DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->inv_tmp, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena, &ctx->trace_raw, &ctx->fri_misc,
-                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp}) {
+                     &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde, &ctx->ext_idx_tmp, &ctx->spot}) {
     if (b->ptr) hipFree(b->ptr);
     if (b->ev) hipEventDestroy(b->ev);
   }
@@ -512,7 +512,7 @@ stark_status stark_ctx_memory(const stark_ctx* ctx, size_t* cached_bytes, size_t
   for (const auto& kv : ctx->tw) total += kv.second->base_bytes;
   for (const DevBuf* b : {&ctx->scratch, &ctx->io, &ctx->io2, &ctx->inv_tmp, &ctx->fri_cols, &ctx->r1cs_arena, &ctx->trace_arena,
                           &ctx->trace_raw, &ctx->fri_misc, &ctx->lde_tmp, &ctx->verify_arena, &ctx->verify_lde,
-                          &ctx->ext_idx_tmp})
+                          &ctx->ext_idx_tmp, &ctx->spot})
     total += b->ptr ? b->bytes : 0;
   for (const stark_merkle_tree* t : ctx->trees) total += merkle_device_bytes(t);
   for (const stark_merkle_tree* t : ctx->fri_trees) total += merkle_device_bytes(t);

@@ -127,6 +127,7 @@ struct stark_ctx {
   stark::DevBuf verify_arena, verify_lde;  // the verifier's circuit, kept for the next call
   stark::DevBuf ext_idx_tmp;  // an IDX extension too large for the cache cap (this proof only)
   stark::DevBuf inv_tmp;      // the scratch of a second batch inverse sharing a host round trip (r1cs.hip)
+  stark::DevBuf spot;         // circuit_spot_values' tables and sums (r1cs.hip)
   // Merkle trees reused across calls: [0, 1] FRI layer ping-pong, [2..4] the
   // accumulator, main and linear-combination trees of mk_r1cs_proof.
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -265,6 +266,12 @@ uint32_t ntt_first_log_r(uint32_t log_n);  // log2 of the first pass's radix
 stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* d_data, uint32_t log_n,
                              uint32_t batch, const Twiddles& tw, bool inverse, hipStream_t stream,
                              const fe* post = nullptr);
+// The forward transform's first pass alone over src's zero-extended columns (as ntt_device_from), stored
+// transposed and canonical: out[c][t A + j] = sum_r src[c][j + r A] w_T^(r t), T = 2^*log_t (the plan's
+// first radix), A = n / T, w_T = w^A.  Then X[c][i] = sum_j w^(i j) out[c][(i mod T) A + j]: one output of
+// the whole transform is a dot product of length A over a contiguous run (the verifier's spot values).
+stark_status ntt_first_pass_tmajor(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* out, uint32_t log_n,
+                                   uint32_t batch, const Twiddles& tw, hipStream_t stream, uint32_t* log_t);
 
 // First pass of a transform whose input is zero beyond its first n >> zero_log elements (best_fft's
 // zero padding): skip = the number of leading radix-2 stages that are plain copies (<= zero_log,
@@ -360,7 +367,8 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // which reads only the first six and evaluates Zb2 / Zb3 at its spot positions): 6 x P, no inverses.
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s, bool with_zb = true, const fe** colp = nullptr);
+                         hipStream_t s, bool with_zb = true, const fe** colp = nullptr,
+                         uint32_t* spot_log_t = nullptr);
 // mk_r1cs_proof with those columns given (only S, P and A are extended).
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,
                                     size_t os, const uint64_t* public_wires, size_t n_public,
@@ -376,6 +384,11 @@ stark_status dprove_begin_prepared(stark_ctx* ctx, uint32_t world, uint32_t rank
                                    void* stream, stark_dprove** out);
 // A circuit prepared for many proofs (r1cs_trace_dev.hip): everything of a proof that depends on
 // the .r1cs alone.  lde = circuit_lde's columns for (world, rank).
+struct PreparedCircuit;
+// The six circuit columns K F0 F1 F2 IDX PIDX at n positions of the precision domain (a spot build):
+// out[(k n + i) 32 ..] = column k at g2^positions[i], canonical little-endian.
+stark_status circuit_spot_values(stark_ctx* ctx, const PreparedCircuit& c, const size_t* positions, size_t n,
+                                 uint8_t* out, hipStream_t s);
 struct PreparedCircuit {
   DevBuf arena, lde;
   size_t os = 0, n_wires = 0, n_public = 0;
@@ -385,6 +398,10 @@ struct PreparedCircuit {
   // Where the six columns K F0 F1 F2 IDX PIDX are (slots of lde, or for the verifier's cold build
   // K's slot 1 and the shared F0 / IDX extensions); K F0-F2 are Montgomery images iff with_zb.
   const fe* col[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // spot: the verifier's cold build holds no extensions, only the columns' first forward passes
+  // (circuit_spot_values; first radix 2^spot_log_t).
+  bool spot = false;
+  uint32_t spot_log_t = 0;
   uint64_t a_len = 0;
   std::vector<size_t> pfi;
   const uint32_t* base = nullptr;

@@ -1094,4 +1094,33 @@ stark_status ntt_device_from(stark_ctx* ctx, const fe* src, uint32_t zero_log, f
   return STARK_OK;
 }
 
+// Pass 0 launched as if it were the transform's last pass (Ns = A = n / T): the store's
+// out[(j / Ns) Ns R + (j mod Ns) + r Ns] is then out[j + r A] (every column j < A), reduced to canonical,
+// and the pass has no column twiddle whatever its Ns (kColNone / kColSparse read none).
+stark_status ntt_first_pass_tmajor(stark_ctx* ctx, const fe* src, uint32_t zero_log, fe* out, uint32_t log_n,
+                                   uint32_t batch, const Twiddles& tw, hipStream_t stream, uint32_t* log_t) {
+  if (!src || log_n < 2 || zero_log == 0 || batch == 0 || tw.log_n != log_n) return STARK_ERR_BAD_ARG;
+  if (((uint64_t)batch << log_n) > ((uint64_t)1 << 34)) return STARK_ERR_BAD_ARG;
+  const uint32_t lr = plan_passes(log_n).log_r[0];
+  if (zero_log > lr) return STARK_ERR_BAD_ARG;  // (the LDEs here: zero_log 3 <= every plan's first radix)
+  uint32_t k = zero_log;
+  if ((k & 1) != (lr & 1)) --k;
+  const Sparse sp{k, zero_log, log_n - zero_log};
+  const uint32_t lb = choose_log_b_impl(log_n, lr, kTileLog);
+  const uint32_t elems = 1u << (lr + lb);
+  const uint32_t threads = elems / 4 < 64 ? 64 : elems / 4;
+  const uint32_t log_tiles = log_n - lr - lb;
+  const uint64_t total = (uint64_t)batch << log_tiles;
+  const int col = sp.skip ? kColSparse : kColNone;
+  const ColTw ct{tw.d_t16, tw.d_lo, tw.d_hi, nullptr, tw.l16, tw.kb, nullptr};
+  const size_t image = std::max((size_t)elems, db_full_fe(lr, col));
+  const size_t lds = (image + db_lds_fe(lr, col)) * sizeof(fe);
+  hipLaunchKernelGGL(pass_kernel(lr, col), dim3((unsigned)total), dim3(threads), lds, stream, src, out, log_n,
+                     log_n - lr, lb, ct, tw.d_small + tw.small_off[lr], tw.d_db + tw.db_off[lr], to_dev(tw.inv_n), 0,
+                     log_tiles, (uint32_t)total, sp);
+  STARK_HIP(ctx, hipGetLastError());
+  *log_t = lr;
+  return STARK_OK;
+}
+
 }  // namespace stark

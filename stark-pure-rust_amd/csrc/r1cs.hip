@@ -1426,12 +1426,14 @@ __global__ void r1cs_idx_kernel(const uint64_t* __restrict__ perm, uint64_t os, 
 // are the device trace builder's circuit columns (os slots).
 stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_bytes, const uint64_t* perm, size_t os,
                          const size_t* public_first_indices, size_t n_pfi, uint32_t world, uint32_t rank, DevBuf& out,
-                         hipStream_t s, bool with_zb, const fe** colp) {
+                         hipStream_t s, bool with_zb, const fe** colp, uint32_t* spot_log_t) {
   const FieldHost& F = FieldHost::get();
-  // with_zb = false (the verifier's cold build, which gathers six values per spot position): the columns
+  // with_zb = false (the verifier's cold build, which needs six values per spot position): the columns
   // stay where they are made -- K's extension in slot 1, F0's and IDX's in their shared entries -- with
-  // no slot copies and no Montgomery images (colp tells the caller where each one is).
+  // no slot copies and no Montgomery images (colp tells the caller where each one is).  With spot_log_t
+  // no extension is made at all: out holds the six columns' first forward passes (circuit_spot_values).
   const bool verify_only = !with_zb;
+  if (spot_log_t && (with_zb || world != 1)) return STARK_ERR_BAD_ARG;
   const fe* col[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (world == 0 || world > (uint32_t)kExtensionFactor || (world & (world - 1)) || rank >= world)
     return STARK_ERR_BAD_ARG;
@@ -1460,6 +1462,18 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
                        raw + steps);
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
+    if (spot_log_t) {
+      // The six step columns' coefficients (inv_best_fft, one batch), then only the first pass of their
+      // forward transforms over the precision domain, transposed (ntt_first_pass_tmajor).
+      fe* const o = (fe*)out.ptr;
+      st = ntt_device(ctx, raw, log_steps, 6, *tw1i, true, s);
+      if (st == STARK_OK) st = ntt_first_pass_tmajor(ctx, raw, log_prec - log_steps, o, log_prec, 6, *tw2, s, spot_log_t);
+      for (int k = 0; k < 6; ++k) col[k] = o + (uint64_t)k * P;
+      if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
+      if (colp)
+        for (int k = 0; k < 6; ++k) colp[k] = col[k];
+      return st;
+    }
     // K F0 F1 F2, then PIDX; IDX and F0 (1 on the os rows: the flags are circuit_build's calc_flags)
     // are the shared extensions (ext_const_column), copied into their slots.  With F0's: K is moved
     // over F0's step column, K F1 F2 are extended into slots 1-3, and K then copied to slot 0.
@@ -1522,6 +1536,122 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
   if (colp)
     for (int k = 0; k < 6; ++k) colp[k] = col[k];
   return st;
+}
+
+// ---- the verifier's spot values (circuit_lde's spot mode) -------------------------------------------
+//
+// Y = the six step columns' first forward passes, T-major (column k at Y + k P, Y[t A + j], T = 2^log_t,
+// A = P / T): column k at x = g2^e is sum_{j < A} x^j Y_k[(e mod T) A + j] (ntt_first_pass_tmajor), a
+// contiguous run of A values per column and position instead of the two further passes of its extension.
+// Workgroup (b, i) takes position i's j = g + S l (g = 256 b + thread < S, l < A / S): Horner over l with
+// the constant x^S (its digit-basis table, spot_setup_kernel), then one product by x^g (the two-level
+// table of g2), summed over the workgroup; spot_sum_kernel adds position i's workgroups.
+constexpr uint32_t kSpotMax = 128;
+struct SpotPos {
+  uint64_t e[kSpotMax];
+};
+
+__global__ void spot_setup_kernel(SpotPos pos, uint32_t n, uint32_t log_s, uint64_t P, const fe* __restrict__ lo,
+                                  const fe* __restrict__ hi, uint32_t kb, fe two32_m, uint32_t* __restrict__ tabs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe unit = fe_zero();
+  unit.w[0] = 1;
+  const fe xs = fe_mul(pow_tab(lo, hi, kb, (pos.e[i] << log_s) & (P - 1)), unit);  // x^S, canonical
+  db_table_dev(xs, two32_m, tabs + 72 * i);
+}
+
+__global__ __launch_bounds__(256) void spot_eval_kernel(const fe* __restrict__ y, uint64_t P, uint32_t log_t,
+                                                        uint32_t log_s, SpotPos pos, const uint32_t* __restrict__ tabs,
+                                                        const fe* __restrict__ lo, const fe* __restrict__ hi,
+                                                        uint32_t kb, fe* __restrict__ partial) {
+  __shared__ fe red[256];
+  const uint32_t i = blockIdx.y;
+  const uint64_t e = pos.e[i];
+  const uint64_t T = (uint64_t)1 << log_t, A = P >> log_t, S = (uint64_t)1 << log_s, nl = A >> log_s;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool on = g < S;
+  const uint32_t* W = tabs + 72 * i;  // (uniform: scalar loads)
+  const fe xg = on ? pow_tab(lo, hi, kb, (e * g) & (P - 1)) : fe_zero();  // Montgomery image of x^g
+  const fe* base = y + (e & (T - 1)) * A + g;
+  fe sum[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    fe acc = fe_zero();
+    if (on) {
+      const fe* c = base + (uint64_t)k * P;
+      acc = fe_load(c + (nl - 1) * S);
+#pragma unroll 4
+      for (uint64_t l = nl - 1; l-- > 0;) {
+        const fe v = fe_load(c + l * S);
+        acc = fe_add_raw(fe_mul_db(acc, W), v);  // [0, 2p) + [0, p): below 3p, a digit-basis input
+      }
+      acc = fe_mul(acc, xg);  // canonical
+    }
+    sum[k] = acc;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    red[threadIdx.x] = sum[k];
+    __syncthreads();
+    for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + w]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) fe_store(partial + ((uint64_t)i * gridDim.x + blockIdx.x) * 6 + k, red[0]);
+    __syncthreads();
+  }
+}
+
+__global__ void spot_sum_kernel(const fe* __restrict__ partial, uint32_t bp, uint32_t n, fe* __restrict__ out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;  // position q / 6, column q % 6
+  if (q >= 6 * n) return;
+  const uint32_t i = q / 6, k = q % 6;
+  fe s = fe_zero();
+  for (uint32_t b = 0; b < bp; ++b) s = fe_add(s, fe_load(partial + ((uint64_t)i * bp + b) * 6 + k));
+  fe_store(out + (uint64_t)k * n + i, s);
+}
+
+stark_status circuit_spot_values(stark_ctx* ctx, const PreparedCircuit& c, const size_t* positions, size_t n,
+                                 uint8_t* out, hipStream_t s) {
+  if (!c.spot || !c.col[0] || n == 0 || n > kSpotMax || !positions || !out) return STARK_ERR_BAD_ARG;
+  const FieldHost& F = FieldHost::get();
+  const uint32_t log_steps = log2_ceil_ref(c.os - 1), log_prec = log_steps + kLogExtensionFactor;
+  const uint64_t P = (uint64_t)1 << log_prec;
+  if (c.spot_log_t == 0 || c.spot_log_t > log_prec) return STARK_ERR_BAD_ARG;
+  ProofRoots roots;
+  STARK_TRY(proof_roots(ctx, log_steps, log_prec, 1, roots));
+  const Twiddles& tw = *roots.tw2;
+  // j's per thread: 16 where the positions' threads fill the chip (A = 2^16 at 2^20 steps: 80 x 16
+  // workgroups), 4 below (a few hundred workgroups, each short)
+  const uint32_t log_a = log_prec - c.spot_log_t;
+  const uint32_t log_nl = std::min<uint32_t>(log_a, log_a >= 16 ? 4 : log_a >= 14 ? log_a - 12 : 2);
+  const uint32_t log_s = log_a - log_nl;
+  const uint32_t bp = log_s > 8 ? 1u << (log_s - 8) : 1u;
+  SpotPos sp;
+  for (size_t i = 0; i < n; ++i) {
+    if (positions[i] >= P) return STARK_ERR_BAD_ARG;
+    sp.e[i] = positions[i];
+  }
+  const size_t tab_bytes = (n * 72 * 4 + 255) & ~(size_t)255, part_bytes = n * bp * 6 * sizeof(fe);
+  STARK_TRY(ensure_buf(ctx, ctx->spot, tab_bytes + part_bytes + 6 * n * sizeof(fe)));
+  uint8_t* d = (uint8_t*)ctx->spot.ptr;
+  uint32_t* tabs = (uint32_t*)d;
+  fe* partial = (fe*)(d + tab_bytes);
+  fe* vals = (fe*)(d + tab_bytes + part_bytes);
+  uint8_t* host = nullptr;
+  STARK_TRY(ctx_pinned(ctx, 0, 6 * n * sizeof(fe), (void**)&host));
+  hipLaunchKernelGGL(spot_setup_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, (uint32_t)n, log_s, P,
+                     tw.d_lo, tw.d_hi, tw.kb, to_dev(F.from_u64((uint64_t)1 << 32)), tabs);
+  hipLaunchKernelGGL(spot_eval_kernel, dim3(bp, (unsigned)n), dim3(256), 0, s, (const fe*)c.col[0], P, c.spot_log_t,
+                     log_s, sp, (const uint32_t*)tabs, tw.d_lo, tw.d_hi, tw.kb, partial);
+  hipLaunchKernelGGL(spot_sum_kernel, dim3((unsigned)((6 * n + 255) / 256)), dim3(256), 0, s, (const fe*)partial, bp,
+                     (uint32_t)n, vals);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_HIP(ctx, hipMemcpyAsync(host, vals, 6 * n * sizeof(fe), hipMemcpyDeviceToHost, s));
+  STARK_HIP(ctx, hipStreamSynchronize(s));
+  memcpy(out, host, 6 * n * sizeof(fe));
+  return STARK_OK;
 }
 
 stark_status mk_r1cs_proof_prepared(stark_ctx* ctx, const uint64_t* witness_trace, const uint64_t* computational_trace,

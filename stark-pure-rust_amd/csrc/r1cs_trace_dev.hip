@@ -607,7 +607,7 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   c.perm = (const uint64_t*)(A + o_perm);
   c.slot_wire = (const uint32_t*)(A + o_sw);
   return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s,
-                     c.with_zb, c.col);
+                     c.with_zb, c.col, c.spot ? &c.spot_log_t : nullptr);
 }
 
 // The witness of one proof: decode, then S and P from the circuit's slot wires.

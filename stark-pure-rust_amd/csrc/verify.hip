@@ -622,6 +622,10 @@ static stark_status verify_r1cs(stark_ctx* ctx, const PreparedCircuit& c, const 
   {
     HostTask gather([&] {
       if (!sized) return;
+      if (c.spot) {  // the cold build's first passes: the six values per position evaluated from them
+        st_got = circuit_spot_values(ctx, c, positions.data(), n_pos, got.data(), ctx->stream);
+        return;
+      }
       stark_open_req req[6];
       for (int k = 0; k < 6; ++k)
         req[k] = stark_open_req{nullptr, (const uint8_t*)c.col[k], 32, prec, positions.data(), n_pos,
@@ -808,6 +812,7 @@ stark_status stark_verify_r1cs_bytes(stark_ctx* ctx, const uint8_t* r1cs, size_t
   std::swap(circ.c.arena, ctx->verify_arena);
   std::swap(circ.c.lde, ctx->verify_lde);
   circ.c.with_zb = false;  // verify_r1cs evaluates Zb2 / Zb3 at its spot positions on the host
+  circ.c.spot = true;      // and the six circuit columns there from their first forward passes
   PhaseClock clk("verify: circuit");
   // The proof is read on the side thread while this one builds the circuit (mostly device work and
   // its synchronisations): the two do not depend on each other.

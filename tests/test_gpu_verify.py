@@ -185,11 +185,11 @@ def test_prepared_circuit_verifies_many(ctx):
 
 
 def test_cold_verify_under_cache_caps(proofs):
-    """The cold verifier gathers K, F0 and IDX at the spot positions from where their extensions are made
-    (csrc/r1cs.hip circuit_lde, verify_only): F0's and IDX's from the context's shared cache when it holds
-    them, F0 from its own slot and IDX from the per-context buffer when the cap refuses them (cap 0), or
-    when each reservation evicts the previous column (cap of one column).  Every case accepts the golden
-    proof and rejects a tampered one; the prover's digest is unchanged afterwards."""
+    """The cold verifier makes no extension: it evaluates K, F0-F2, IDX and PIDX at its spot positions from
+    their first forward passes (csrc/r1cs.hip circuit_spot_values), outside the context's capped cache.
+    Under the default cap, cap 0 and a cap of one column it accepts the golden proof and rejects a
+    tampered one, twice per context, and the prover beside it (which does use the cache: its shared F0 /
+    IDX / 1/Zb3 columns) still gives the golden digest."""
     import stark_amd as S
     from stark_amd.r1cs import prove_with_witness
     from stark_amd.verify import verify_with_wtns
@@ -212,3 +212,23 @@ def test_cold_verify_under_cache_caps(proofs):
             assert hashlib.sha256(js2.encode()).hexdigest() == GOLDEN["compute"]["json_sha256"], cap
         finally:
             c.close()
+
+
+@pytest.mark.parametrize("log_steps", [16, 20])
+def test_cold_verify_synthetic_spot_sizes(ctx, log_steps):
+    """Cold verify_with_wtns of synthetic 2^16- and 2^20-step proofs: first passes of radix 2^6 / 2^7 with
+    runs of A = 2^13 / 2^16 values per column and position, split over 8 / 16 workgroups per position
+    (circuit_spot_values).  Accepts the prover's proof; a flipped main-branch leaf byte (P at a spot
+    position) and a flipped L leaf are rejected."""
+    import synth_r1cs
+    from stark_amd.r1cs import prove_with_witness
+    from stark_amd.verify import verify_with_wtns
+    r1, wt = synth_r1cs.for_steps(log_steps)
+    js = prove_with_witness(ctx, r1, wt).to_json()
+    assert verify_with_wtns(ctx, r1, wt, js)
+    p = json.loads(js)
+    for path in (("main_branches", 1, 5), ("linear_comb_branches", 7, 30)):
+        q = copy.deepcopy(p)
+        q[path[0]][path[1]]["leaf"][path[2]] ^= 1
+        with pytest.raises(AssertionError):
+            verify_with_wtns(ctx, r1, wt, q)
