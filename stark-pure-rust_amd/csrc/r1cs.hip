@@ -817,11 +817,15 @@ __global__ void const_column_kernel(fe* __restrict__ out, uint64_t n, uint64_t t
 // Call before the proof enqueues work on `s`: a first call synchronises s.  An IDX extension larger
 // than the cache cap lives in a per-context buffer for this proof only; the others are not built
 // when they cannot be cached (*out = nullptr: the caller computes them as part of the proof).
-enum : uint32_t { kExtIdx = 0, kExtF0 = 1, kInvZb3 = 2, kInvXm1 = 3 };
+//   kSpotF0 / kSpotIdx: F0's / IDX's first forward pass, transposed (ntt_first_pass_tmajor: the verifier's
+//            cold build, circuit_spot_values; world 1), not built when it cannot be cached.
+enum : uint32_t { kExtIdx = 0, kExtF0 = 1, kInvZb3 = 2, kInvXm1 = 3, kSpotF0 = 4, kSpotIdx = 5 };
 static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os, uint32_t log_steps,
                                      uint32_t log_prec, uint32_t log_g, uint32_t r, const Twiddles& tw_g1_inv,
                                      const Twiddles& tw_g2, const Twiddles& tw_h, hipStream_t s, const fe** out) {
-  const uint64_t tag = kind == kExtF0 ? os : 0;
+  const bool spot = kind == kSpotF0 || kind == kSpotIdx;
+  if (spot && (log_g || r)) return STARK_ERR_BAD_ARG;
+  const uint64_t tag = (kind == kExtF0 || kind == kSpotF0) ? os : 0;
   const auto key = std::make_tuple(kind, log_steps, log_prec, log_g, r, tag);
   auto it = ctx->ext_idx.find(key);
   if (it != ctx->ext_idx.end()) {
@@ -877,8 +881,14 @@ static stark_status ext_const_column(stark_ctx* ctx, uint32_t kind, uint64_t os,
   } else {
     hipLaunchKernelGGL(const_column_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (fe*)coef, steps, tag);
     st = hipGetLastError() == hipSuccess ? STARK_OK : STARK_ERR_HIP;
-    if (st == STARK_OK)
+    if (st == STARK_OK && spot) {
+      uint32_t log_t = 0;
+      st = ntt_device(ctx, (fe*)coef, log_steps, 1, tw_g1_inv, true, s);
+      if (st == STARK_OK)
+        st = ntt_first_pass_tmajor(ctx, (fe*)coef, log_prec - log_steps, (fe*)col, log_prec, 1, tw_g2, s, &log_t);
+    } else if (st == STARK_OK) {
       st = coset_lde(ctx, (fe*)coef, 1, (fe*)col, log_steps, log_prec, log_g, r, tw_g1_inv, tw_g2, tw_h, s);
+    }
   }
   if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
   hipFree(coef);
@@ -1463,12 +1473,36 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
     hipLaunchKernelGGL(r1cs_idx_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, perm, (uint64_t)os, steps,
                        raw + 4 * steps, raw + 5 * steps);
     if (spot_log_t) {
-      // The six step columns' coefficients (inv_best_fft, one batch), then only the first pass of their
-      // forward transforms over the precision domain, transposed (ntt_first_pass_tmajor).
+      // The step columns' coefficients (inv_best_fft, one batch), then only the first pass of their
+      // forward transforms over the precision domain, transposed (ntt_first_pass_tmajor).  F0's and
+      // IDX's depend on the size alone: from the context's cache when it holds them (K moved over F0's
+      // step column and PIDX over IDX's, K F1 F2 PIDX are then one batch of four), else in the batch.
       fe* const o = (fe*)out.ptr;
-      st = ntt_device(ctx, raw, log_steps, 6, *tw1i, true, s);
-      if (st == STARK_OK) st = ntt_first_pass_tmajor(ctx, raw, log_prec - log_steps, o, log_prec, 6, *tw2, s, spot_log_t);
-      for (int k = 0; k < 6; ++k) col[k] = o + (uint64_t)k * P;
+      const fe *yf0 = nullptr, *yidx = nullptr;
+      st = ext_const_column(ctx, kSpotF0, os, log_steps, log_prec, 0, 0, *tw1i, *tw2, *twh, s, &yf0);
+      if (st == STARK_OK) st = ext_const_column(ctx, kSpotIdx, 0, log_steps, log_prec, 0, 0, *tw1i, *tw2, *twh, s, &yidx);
+      auto live = [&](uint32_t kind, uint64_t tag) {  // (a later reservation may evict an earlier column)
+        return ctx->ext_idx.count(std::make_tuple(kind, log_steps, log_prec, 0u, 0u, tag)) != 0;
+      };
+      if (yf0 && !live(kSpotF0, os)) yf0 = nullptr;
+      if (yidx && !live(kSpotIdx, 0)) yidx = nullptr;
+      const bool shared = yf0 && yidx;
+      if (st == STARK_OK && shared &&
+          (hipMemcpyAsync(raw + steps, raw, steps * sizeof(fe), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+           hipMemcpyAsync(raw + 4 * steps, raw + 5 * steps, steps * sizeof(fe), hipMemcpyDeviceToDevice, s) !=
+               hipSuccess))
+        st = STARK_ERR_HIP;
+      fe* const first = shared ? raw + steps : raw;
+      const uint32_t batch = shared ? 4 : 6;
+      if (st == STARK_OK) st = ntt_device(ctx, first, log_steps, batch, *tw1i, true, s);
+      if (st == STARK_OK)
+        st = ntt_first_pass_tmajor(ctx, first, log_prec - log_steps, o, log_prec, batch, *tw2, s, spot_log_t);
+      if (shared) {
+        const fe* c6[6] = {o, yf0, o + P, o + 2 * P, yidx, o + 3 * P};
+        for (int k = 0; k < 6; ++k) col[k] = c6[k];
+      } else {
+        for (int k = 0; k < 6; ++k) col[k] = o + (uint64_t)k * P;
+      }
       if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
       if (colp)
         for (int k = 0; k < 6; ++k) colp[k] = col[k];
@@ -1540,7 +1574,7 @@ stark_status circuit_lde(stark_ctx* ctx, const fe* coef, const uint8_t* flag_byt
 
 // ---- the verifier's spot values (circuit_lde's spot mode) -------------------------------------------
 //
-// Y = the six step columns' first forward passes, T-major (column k at Y + k P, Y[t A + j], T = 2^log_t,
+// Y = the six step columns' first forward passes, T-major (column k at c.col[k], Y[t A + j], T = 2^log_t,
 // A = P / T): column k at x = g2^e is sum_{j < A} x^j Y_k[(e mod T) A + j] (ntt_first_pass_tmajor), a
 // contiguous run of A values per column and position instead of the two further passes of its extension.
 // Workgroup (b, i) takes position i's j = g + S l (g = 256 b + thread < S, l < A / S): Horner over l with
@@ -1561,7 +1595,11 @@ __global__ void spot_setup_kernel(SpotPos pos, uint32_t n, uint32_t log_s, uint6
   db_table_dev(xs, two32_m, tabs + 72 * i);
 }
 
-__global__ __launch_bounds__(256) void spot_eval_kernel(const fe* __restrict__ y, uint64_t P, uint32_t log_t,
+struct SpotCols {
+  const fe* c[6];
+};
+
+__global__ __launch_bounds__(256) void spot_eval_kernel(SpotCols y, uint64_t P, uint32_t log_t,
                                                         uint32_t log_s, SpotPos pos, const uint32_t* __restrict__ tabs,
                                                         const fe* __restrict__ lo, const fe* __restrict__ hi,
                                                         uint32_t kb, fe* __restrict__ partial) {
@@ -1573,13 +1611,13 @@ __global__ __launch_bounds__(256) void spot_eval_kernel(const fe* __restrict__ y
   const bool on = g < S;
   const uint32_t* W = tabs + 72 * i;  // (uniform: scalar loads)
   const fe xg = on ? pow_tab(lo, hi, kb, (e * g) & (P - 1)) : fe_zero();  // Montgomery image of x^g
-  const fe* base = y + (e & (T - 1)) * A + g;
+  const uint64_t off = (e & (T - 1)) * A + g;
   fe sum[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     fe acc = fe_zero();
     if (on) {
-      const fe* c = base + (uint64_t)k * P;
+      const fe* c = y.c[k] + off;
       acc = fe_load(c + (nl - 1) * S);
 #pragma unroll 4
       for (uint64_t l = nl - 1; l-- > 0;) {
@@ -1643,7 +1681,12 @@ stark_status circuit_spot_values(stark_ctx* ctx, const PreparedCircuit& c, const
   STARK_TRY(ctx_pinned(ctx, 0, 6 * n * sizeof(fe), (void**)&host));
   hipLaunchKernelGGL(spot_setup_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, (uint32_t)n, log_s, P,
                      tw.d_lo, tw.d_hi, tw.kb, to_dev(F.from_u64((uint64_t)1 << 32)), tabs);
-  hipLaunchKernelGGL(spot_eval_kernel, dim3(bp, (unsigned)n), dim3(256), 0, s, (const fe*)c.col[0], P, c.spot_log_t,
+  SpotCols cols;
+  for (int k = 0; k < 6; ++k) {
+    if (!c.col[k]) return STARK_ERR_BAD_ARG;
+    cols.c[k] = c.col[k];
+  }
+  hipLaunchKernelGGL(spot_eval_kernel, dim3(bp, (unsigned)n), dim3(256), 0, s, cols, P, c.spot_log_t,
                      log_s, sp, (const uint32_t*)tabs, tw.d_lo, tw.d_hi, tw.kb, partial);
   hipLaunchKernelGGL(spot_sum_kernel, dim3((unsigned)((6 * n + 255) / 256)), dim3(256), 0, s, (const fe*)partial, bp,
                      (uint32_t)n, vals);

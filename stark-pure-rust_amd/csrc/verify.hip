@@ -24,6 +24,7 @@
 
 #include "internal.h"
 #include "blake2s.h"
+#include "host_b2s.h"
 
 namespace stark {
 namespace {
@@ -357,22 +358,6 @@ HostFp eval_poly(const std::vector<HostFp>& poly, const HostFp& x) {  // eval_po
   return acc;
 }
 
-// Proof::validate (merkle_tree.rs:25-43) for each (index, proof) pair; verify_multi_branch
-// (:46-58) zips, so every index needs its proof.
-bool branch_valid(const uint8_t root[32], size_t index, const Branch& b) {
-  uint8_t cur[32], msg[64];
-  b2s_host(b.leaf.data(), b.leaf.size(), cur);
-  size_t pos = index;
-  for (size_t d = 0; d < b.nodes.size() / 32; ++d) {
-    const uint8_t* sib = b.nodes.data() + 32 * d;
-    memcpy(msg, pos % 2 == 0 ? cur : sib, 32);
-    memcpy(msg + 32, pos % 2 == 0 ? sib : cur, 32);
-    b2s_host(msg, 64, cur);
-    pos /= 2;
-  }
-  return memcmp(cur, root, 32) == 0;
-}
-
 // Proof::validate (merkle_tree.rs:25-43) for many (root, index, opening) triples of different trees
 // in one pass over the host workers, split by node count (verify_multi_branch, :46-58, zips indices
 // and openings: the callers check that every index has one).
@@ -381,16 +366,26 @@ struct PathCheck {
   size_t index;
   const Branch* b;
 };
-// ok[i] = check i's path leads to its root.
+// ok[i] = check i's path leads to its root: b2s_paths (host_b2s.h), a SIMD register of paths of one
+// shape per compression (the checks come in runs of equal leaf length and depth), split by compression
+// count over the host workers.
 void paths_check(const std::vector<PathCheck>& v, std::vector<uint8_t>& ok) {
   ok.assign(v.size(), 0);
+  std::vector<PathJob> jobs(v.size());
   std::vector<size_t> cost(v.size() + 1, 0);
-  for (size_t i = 0; i < v.size(); ++i) cost[i + 1] = cost[i] + 1 + v[i].b->nodes.size() / 32;
-  const unsigned parts = std::max(1u, (unsigned)std::min<size_t>(host_threads(), (v.size() + 31) / 32));
+  for (size_t i = 0; i < v.size(); ++i) {
+    const Branch& b = *v[i].b;
+    jobs[i] = PathJob{v[i].root, (uint64_t)v[i].index, b.leaf.data(), b.nodes.data(), (uint32_t)b.leaf.size(),
+                      (uint32_t)(b.nodes.size() / 32)};
+    cost[i + 1] = cost[i] + (b.leaf.size() + 63) / 64 + jobs[i].depth + 1;
+  }
+  const size_t per_part = 48 * (size_t)b2s_paths_width();  // compressions per part at least
+  const unsigned parts =
+      std::max(1u, (unsigned)std::min<size_t>(host_threads(), cost.back() / per_part));
   host_parallel(parts, [&](unsigned t) {
     const size_t lo = std::lower_bound(cost.begin(), cost.end(), cost.back() * t / parts) - cost.begin();
     const size_t hi = std::lower_bound(cost.begin(), cost.end(), cost.back() * (t + 1) / parts) - cost.begin();
-    for (size_t i = lo; i < hi && i < v.size(); ++i) ok[i] = branch_valid(v[i].root, v[i].index, *v[i].b);
+    if (lo < hi && lo < v.size()) b2s_paths(jobs.data() + lo, std::min(hi, v.size()) - lo, ok.data() + lo);
   });
 }
 bool sampler(const uint8_t seed[32], size_t modulus, uint32_t count, uint32_t excl, std::vector<size_t>& out) {

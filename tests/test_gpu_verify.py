@@ -186,10 +186,11 @@ def test_prepared_circuit_verifies_many(ctx):
 
 def test_cold_verify_under_cache_caps(proofs):
     """The cold verifier makes no extension: it evaluates K, F0-F2, IDX and PIDX at its spot positions from
-    their first forward passes (csrc/r1cs.hip circuit_spot_values), outside the context's capped cache.
-    Under the default cap, cap 0 and a cap of one column it accepts the golden proof and rejects a
-    tampered one, twice per context, and the prover beside it (which does use the cache: its shared F0 /
-    IDX / 1/Zb3 columns) still gives the golden digest."""
+    their first forward passes (csrc/r1cs.hip circuit_spot_values), F0's and IDX's from the context's
+    capped cache when it holds them (default cap), else computed with the others (cap 0; a cap of one
+    column, where IDX's reservation evicts F0's).  Each case accepts the golden proof and rejects a
+    tampered one, twice per context, and the prover beside it (whose shared F0 / IDX / 1/Zb3 columns use
+    the same cache) still gives the golden digest."""
     import stark_amd as S
     from stark_amd.r1cs import prove_with_witness
     from stark_amd.verify import verify_with_wtns
