@@ -38,6 +38,10 @@ extern "C" {
 #define STARK_ABI_VERSION 2u
 /* The ABI version the loaded library implements (no reference counterpart: a linking check). */
 uint32_t stark_abi_version(void);
+/* Paths per SIMD register of the verifier's host Merkle path checks on this CPU (16 AVX-512, 8 AVX2,
+ * 4 SSE2; the environment variable STARK_B2S_WIDTH=4|8 narrows it).  A diagnostic with no reference
+ * counterpart (Proof::validate, commitment/src/merkle_tree.rs:25-43, is what those checks restate). */
+uint32_t stark_verify_simd_width(void);
 
 typedef enum {
   STARK_OK = 0,

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include "internal.h"
+#include "host_b2s.h"
 #include "blake2s.h"
 
 namespace stark {
@@ -436,6 +437,7 @@ const char* stark_status_str(stark_status s) {
 }
 
 uint32_t stark_abi_version(void) { return STARK_ABI_VERSION; }
+uint32_t stark_verify_simd_width(void) { return (uint32_t)b2s_paths_width(); }
 
 stark_status stark_ctx_create(int device, stark_ctx** out) {
   if (!out) return STARK_ERR_BAD_ARG;

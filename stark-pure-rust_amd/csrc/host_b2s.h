@@ -20,7 +20,8 @@ struct PathJob {
 // registers; any mix is accepted.
 void b2s_paths(const PathJob* jobs, size_t n, uint8_t* ok);
 
-// The vector width b2s_paths uses on this CPU (16: AVX-512, 8: AVX2, 4: SSE2).
+// The vector width b2s_paths uses on this CPU (16: AVX-512, 8: AVX2, 4: SSE2; STARK_B2S_WIDTH may
+// narrow it).
 int b2s_paths_width();
 
 }  // namespace stark

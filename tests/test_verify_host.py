@@ -68,3 +68,43 @@ def test_malformed_raises(oracle):
         verify_low_degree_proof(root, w, proof[:-1], md, 8)        # no Last layer
     with pytest.raises(S.StarkError):
         verify_low_degree_proof(root, 5, proof, md, 8)             # not a root of unity of 2-power order
+
+
+@pytest.mark.parametrize("width", [4, 8])
+def test_path_checks_at_every_vector_width(oracle, tmp_path, width):
+    """The Merkle path checks run W paths per SIMD register (csrc/host_b2s*.cpp), W picked once per
+    process from the CPU; STARK_B2S_WIDTH narrows it, so a child process checks the AVX2 and SSE2 widths
+    on this host too: the oracle's proof is accepted, a flipped leaf and a flipped sibling are rejected."""
+    import os
+    import subprocess
+    import sys
+    root, w, proof, md = _proof(oracle, 12, 8)
+    bad_leaf = copy.deepcopy(proof)
+    bad_leaf[1]["Middle"]["poly_branches"][17]["leaf"][3] ^= 1
+    bad_node = copy.deepcopy(proof)
+    bad_node[0]["Middle"]["column_branches"][9]["nodes"][2][0] ^= 0x80
+    f = tmp_path / "p.json"
+    f.write_text(json.dumps({"root": root.hex(), "w": w, "md": md,
+                             "proofs": [proof, bad_leaf, bad_node]}))
+    here = os.path.dirname(os.path.abspath(__file__))
+    child = (
+        "import json, sys\n"
+        "from stark_amd.verify import verify_low_degree_proof\n"
+        "import stark_amd as S\n"
+        f"d = json.load(open({str(f)!r}))\n"
+        "root = bytes.fromhex(d['root'])\n"
+        "out = []\n"
+        "for p in d['proofs']:\n"
+        "    try:\n"
+        "        out.append(bool(verify_low_degree_proof(root, d['w'], p, d['md'], 8)))\n"
+        "    except AssertionError:\n"
+        "        out.append(False)\n"
+        "print(json.dumps({'width': S.load_library().stark_verify_simd_width(), 'results': out}))\n")
+    env = dict(os.environ, STARK_B2S_WIDTH=str(width))
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(os.path.dirname(here), "stark-pure-rust_amd"),
+                                         env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["width"] <= width
+    assert got["results"] == [True, False, False]
