@@ -1653,6 +1653,7 @@ __global__ void spot_sum_kernel(const fe* __restrict__ partial, uint32_t bp, uin
 stark_status circuit_spot_values(stark_ctx* ctx, const PreparedCircuit& c, const size_t* positions, size_t n,
                                  uint8_t* out, hipStream_t s) {
   if (!c.spot || !c.col[0] || n == 0 || n > kSpotMax || !positions || !out) return STARK_ERR_BAD_ARG;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));  // (the verifier calls this from its side thread)
   const FieldHost& F = FieldHost::get();
   const uint32_t log_steps = log2_ceil_ref(c.os - 1), log_prec = log_steps + kLogExtensionFactor;
   const uint64_t P = (uint64_t)1 << log_prec;

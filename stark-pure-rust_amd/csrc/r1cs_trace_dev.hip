@@ -312,6 +312,12 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
       beside();
       return;
     }
+    // (a worker's current device is whatever it last ran for: the context's, for its copies)
+    if (t > 1 && hipSetDevice(ctx->device) != hipSuccess) {
+      int ok = (int)hipSuccess;
+      failed.compare_exchange_strong(ok, (int)hipErrorInvalidDevice);
+      return;
+    }
     for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
       if (failed.load(std::memory_order_relaxed) != (int)hipSuccess) break;
       const Piece& p = pieces[i];
