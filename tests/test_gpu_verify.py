@@ -215,12 +215,13 @@ def test_cold_verify_under_cache_caps(proofs):
             c.close()
 
 
-@pytest.mark.parametrize("log_steps", [16, 20])
+@pytest.mark.parametrize("log_steps", [16, 17, 20])
 def test_cold_verify_synthetic_spot_sizes(ctx, log_steps):
-    """Cold verify_with_wtns of synthetic 2^16- and 2^20-step proofs: first passes of radix 2^6 / 2^7 with
-    runs of A = 2^13 / 2^16 values per column and position, split over 8 / 16 workgroups per position
-    (circuit_spot_values).  Accepts the prover's proof; a flipped main-branch leaf byte (P at a spot
-    position) and a flipped L leaf are rejected."""
+    """Cold verify_with_wtns of synthetic 2^16-, 2^17- and 2^20-step proofs: first passes of radix 2^6, 2^8
+    (the 16 x 16 kernel, sparse, of 2^20's (8, 4, 8) plan) and 2^7, with runs of A = 2^13, 2^12 and 2^16
+    values per column and position split over 8, 4 and 16 workgroups per position (circuit_spot_values).
+    Accepts the prover's proof; a flipped main-branch leaf byte (P at a spot position) and a flipped L
+    leaf are rejected."""
     import synth_r1cs
     from stark_amd.r1cs import prove_with_witness
     from stark_amd.verify import verify_with_wtns
