@@ -369,45 +369,51 @@ struct ByteText {
   }
 };
 
-// Writes "[b0,...]" at w (at most 2 + 4 n bytes; the 4-byte stores may touch 2 bytes past the
-// returned end, inside that bound) and returns the end.
+// Writes "[b0,...]" at w and returns the end; nothing past the end is written (the last byte's digits
+// are stored exactly, every earlier 4-byte store is overwritten by the bytes after it).
 static char* json_bytes_at(char* w, const uint8_t* p, size_t n) {
   static const ByteText T;
   *w++ = '[';
-  for (size_t i = 0; i < n; ++i) {
-    const uint8_t b = p[i];
-    memcpy(w, &T.s[b], 4);
-    w += T.len[b];
+  if (n) {
+    for (size_t i = 0; i + 1 < n; ++i) {
+      const uint8_t b = p[i];
+      memcpy(w, &T.s[b], 4);
+      w += T.len[b];
+    }
+    const uint8_t b = p[n - 1];
+    const char* d = reinterpret_cast<const char*>(&T.s[b]);
+    for (uint32_t k = 0; k + 1 < T.len[b]; ++k) *w++ = d[k];
   }
-  if (n) --w;  // the last comma
   *w++ = ']';
   return w;
 }
 
+// Its exact length: 2 + the digits + n - 1 commas.
+static size_t json_bytes_len(const uint8_t* p, size_t n) {
+  size_t d = 0;
+  for (size_t i = 0; i < n; ++i) d += 1 + (p[i] >= 10) + (p[i] >= 100);
+  return 2 + d + (n ? n - 1 : 0);
+}
+
 void json_bytes(std::string& o, const uint8_t* p, size_t n) {
   const size_t at = o.size();
-  o.resize(at + 2 + 4 * n);  // upper bound: 3 digits + comma per byte
-  char* w = json_bytes_at(&o[at], p, n);
-  o.resize((size_t)(w - &o[0]));
+  o.resize(at + json_bytes_len(p, n));
+  json_bytes_at(&o[at], p, n);
 }
 
 // Proofs [i0, i1) of a serde_json Vec<Proof<Vec<u8>, BlakeDigest>>
 // (commitment/src/merkle_tree.rs:14-18), each preceded by a comma unless it is
-// proof 0; the caller writes the brackets.  Rendered into one buffer sized for the worst case.
-static void json_branch_range(std::string& o, const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes,
-                              size_t i0, size_t i1, size_t depth) {
-  static const char kLeaf[] = "{\"leaf\":", kNodes[] = ",\"nodes\":[";
-  const size_t per = 1 + (sizeof kLeaf - 1) + (2 + 4 * leaf_len) + (sizeof kNodes - 1) + depth * (1 + 2 + 4 * 32) + 2;
-  const size_t at = o.size();
-  o.resize(at + (i1 - i0) * per + 8);
-  char* w = &o[at];
+// proof 0; the caller writes the brackets.
+static const char kLeafKey[] = "{\"leaf\":", kNodesKey[] = ",\"nodes\":[";
+static char* json_branch_range_at(char* w, const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes, size_t i0,
+                                  size_t i1, size_t depth) {
   for (size_t i = i0; i < i1; ++i) {
     if (i) *w++ = ',';
-    memcpy(w, kLeaf, sizeof kLeaf - 1);
-    w += sizeof kLeaf - 1;
+    memcpy(w, kLeafKey, sizeof kLeafKey - 1);
+    w += sizeof kLeafKey - 1;
     w = json_bytes_at(w, leaves + leaf_len * i, leaf_len);
-    memcpy(w, kNodes, sizeof kNodes - 1);
-    w += sizeof kNodes - 1;
+    memcpy(w, kNodesKey, sizeof kNodesKey - 1);
+    w += sizeof kNodesKey - 1;
     for (size_t d = 0; d < depth; ++d) {
       if (d) *w++ = ',';
       w = json_bytes_at(w, nodes + (i * depth + d) * 32, 32);
@@ -415,22 +421,60 @@ static void json_branch_range(std::string& o, const uint8_t* leaves, size_t leaf
     *w++ = ']';
     *w++ = '}';
   }
-  o.resize((size_t)(w - &o[0]));
+  return w;
+}
+static size_t json_branch_range_len(const uint8_t* leaves, size_t leaf_len, const uint8_t* nodes, size_t i0,
+                                    size_t i1, size_t depth) {
+  size_t t = 0;
+  for (size_t i = i0; i < i1; ++i) {
+    t += (i ? 1 : 0) + (sizeof kLeafKey - 1) + json_bytes_len(leaves + leaf_len * i, leaf_len) +
+         (sizeof kNodesKey - 1) + (depth ? depth - 1 : 0) + 2;
+    for (size_t d = 0; d < depth; ++d) t += json_bytes_len(nodes + (i * depth + d) * 32, 32);
+  }
+  return t;
 }
 
 void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t leaf_len,
                    const std::vector<uint8_t>& nodes, size_t k, size_t depth) {
-  o.push_back('[');
-  json_branch_range(o, leaves.data(), leaf_len, nodes.data(), 0, k, depth);
-  o.push_back(']');
+  const size_t at = o.size();
+  o.resize(at + 2 + json_branch_range_len(leaves.data(), leaf_len, nodes.data(), 0, k, depth));
+  char* w = &o[at];
+  *w++ = '[';
+  w = json_branch_range_at(w, leaves.data(), leaf_len, nodes.data(), 0, k, depth);
+  *w = ']';
 }
 
 void JsonPieces::text(const std::string& s) {
-  fns.push_back([s](std::string& o) { o += s; });
+  if (!pieces.empty() && !pieces.back().size && pieces.back().text.size() < 4096) {
+    pieces.back().text += s;  // adjacent short fixed texts are one piece (a prerendered one is not grown)
+    return;
+  }
+  pieces.push_back(Piece{s, nullptr, nullptr});
 }
 
 void JsonPieces::bytes(const uint8_t* p, size_t n) {
-  fns.push_back([p, n](std::string& o) { json_bytes(o, p, n); });
+  pieces.push_back(Piece{std::string(), [p, n] { return json_bytes_len(p, n); },
+                         [p, n](char* w) { return json_bytes_at(w, p, n); }});
+}
+
+void JsonPieces::byte_rows(const uint8_t* p, size_t rows, size_t row_len) {
+  constexpr size_t per = 256;  // rows per piece
+  for (size_t r0 = 0; r0 < rows; r0 += per) {
+    const size_t r1 = r0 + per < rows ? r0 + per : rows;
+    pieces.push_back(Piece{std::string(),
+                           [=] {
+                             size_t t = 0;
+                             for (size_t r = r0; r < r1; ++r) t += (r ? 1 : 0) + json_bytes_len(p + r * row_len, row_len);
+                             return t;
+                           },
+                           [=](char* w) {
+                             for (size_t r = r0; r < r1; ++r) {
+                               if (r) *w++ = ',';
+                               w = json_bytes_at(w, p + r * row_len, row_len);
+                             }
+                             return w;
+                           }});
+  }
 }
 
 void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes,
@@ -441,68 +485,67 @@ void JsonPieces::branches(const std::vector<uint8_t>& leaves, size_t leaf_len, c
     const size_t i1 = i0 + per < k ? i0 + per : k;
     const uint8_t* lp = leaves.data();
     const uint8_t* np = nodes.data();
-    fns.push_back([=](std::string& o) { json_branch_range(o, lp, leaf_len, np, i0, i1, depth); });
+    pieces.push_back(Piece{std::string(), [=] { return json_branch_range_len(lp, leaf_len, np, i0, i1, depth); },
+                           [=](char* w) { return json_branch_range_at(w, lp, leaf_len, np, i0, i1, depth); }});
   }
   text("]");
 }
 
-// Renders every piece into its own string on the host workers.
-static void render_pieces(std::vector<std::function<void(std::string&)>>& fns, std::vector<std::string>& out,
-                          unsigned max_threads = 16) {
-  out.assign(fns.size(), std::string());
+// The pieces' lengths (computed ones on the host workers) and their offsets in the text.
+static std::vector<size_t> piece_offsets(std::vector<JsonPieces::Piece>& pieces, unsigned max_threads) {
+  const size_t k = pieces.size();
+  std::vector<size_t> len(k, 0);
   std::atomic<size_t> next{0};
   unsigned nt = host_threads();
   if (nt > max_threads) nt = max_threads;
-  if (fns.size() < 8) nt = 1;
+  if (k < 8) nt = 1;
   host_parallel(nt, [&](unsigned) {
-    for (size_t i; (i = next.fetch_add(1)) < fns.size();) fns[i](out[i]);
+    for (size_t i; (i = next.fetch_add(1)) < k;) len[i] = pieces[i].size ? pieces[i].size() : pieces[i].text.size();
   });
-  fns.clear();
+  std::vector<size_t> off(k + 1, 0);
+  for (size_t i = 0; i < k; ++i) off[i + 1] = off[i] + len[i];
+  return off;
 }
 
-static void prepend_done(std::vector<std::string>& done, std::vector<std::string>& out) {
-  if (done.empty()) return;
-  out.insert(out.begin(), std::make_move_iterator(done.begin()), std::make_move_iterator(done.end()));
-  done.clear();
+// Every piece written at its offset in dst (the host workers take pieces in order of claim).
+static void write_pieces(std::vector<JsonPieces::Piece>& pieces, const std::vector<size_t>& off, char* dst,
+                         unsigned max_threads) {
+  std::atomic<size_t> next{0};
+  unsigned nt = host_threads();
+  if (nt > max_threads) nt = max_threads;
+  if (pieces.size() < 8 || off.back() < ((size_t)1 << 16)) nt = 1;
+  host_parallel(nt, [&](unsigned) {
+    for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+      const JsonPieces::Piece& q = pieces[i];
+      if (q.size) q.write(dst + off[i]);
+      else memcpy(dst + off[i], q.text.data(), q.text.size());
+    }
+  });
 }
 
 void JsonPieces::prerender(unsigned max_threads) {
-  std::vector<std::string> out;
-  render_pieces(fns, out, max_threads);
-  for (std::string& x : out) done.push_back(std::move(x));
+  std::vector<size_t> off = piece_offsets(pieces, max_threads);
+  std::string all(off.back(), '\0');
+  write_pieces(pieces, off, &all[0], max_threads);
+  pieces.clear();
+  pieces.push_back(Piece{std::move(all), nullptr, nullptr});
 }
 
 void JsonPieces::render(std::string& o) {
-  std::vector<std::string> out;
-  render_pieces(fns, out);
-  prepend_done(done, out);
-  size_t total = o.size();
-  for (const std::string& x : out) total += x.size();
-  o.reserve(total);
-  for (const std::string& x : out) o += x;
+  std::vector<size_t> off = piece_offsets(pieces, 16);
+  const size_t at = o.size();
+  o.resize(at + off.back());
+  write_pieces(pieces, off, &o[at], 16);
+  pieces.clear();
 }
 
 void JsonPieces::render(JsonText& o) {
-  std::vector<std::string> out;
-  render_pieces(fns, out);
-  prepend_done(done, out);
-  std::vector<size_t> off(out.size() + 1, 0);
-  for (size_t i = 0; i < out.size(); ++i) off[i + 1] = off[i] + out[i].size();
+  std::vector<size_t> off = piece_offsets(pieces, 16);
   o.n = off.back();
-  o.p.reset(new char[o.n + 1]);  // uninitialised; its pages fault in on the threads that copy
+  o.p.reset(new char[o.n + 1]);  // uninitialised; its pages fault in on the threads that write them
   o.p[o.n] = 0;
-  char* dst = o.p.get();
-  // contiguous runs of pieces of about equal bytes per worker
-  unsigned nt = host_threads();
-  if (nt > 16) nt = 16;
-  if (o.n < ((size_t)1 << 20)) nt = 1;
-  host_parallel(nt, [&](unsigned t) {
-    const size_t lo = o.n * t / nt, hi = o.n * (t + 1) / nt;
-    for (size_t i = std::upper_bound(off.begin(), off.end(), lo) - off.begin() - 1; i < out.size() && off[i] < hi; ++i) {
-      const size_t a = std::max(off[i], lo), b = std::min(off[i + 1], hi);
-      if (b > a) memcpy(dst + a, out[i].data() + (a - off[i]), b - a);
-    }
-  });
+  write_pieces(pieces, off, o.p.get(), 16);
+  pieces.clear();
 }
 
 // serde_json of Vec<FriProof<BlakeDigest>> (fri.rs:16-26) as pieces.
@@ -513,14 +556,7 @@ void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j) {
     if (l) j.text(",");
     if (L.last) {
       j.text("{\"Last\":{\"last\":[");
-      const uint8_t* v = L.last_values.data();
-      const size_t m = L.last_values.size() / 32;
-      j.fns.push_back([v, m](std::string& o) {
-        for (size_t i = 0; i < m; ++i) {
-          if (i) o.push_back(',');
-          json_bytes(o, v + 32 * i, 32);
-        }
-      });
+      j.byte_rows(L.last_values.data(), L.last_values.size() / 32, 32);
       j.text("]}}");
     } else {
       j.text("{\"Middle\":{\"root2\":");

@@ -313,18 +313,25 @@ struct JsonText {
   size_t size() const { return n; }
 };
 
-// serde_json text rendered in pieces on a few host threads, then
-// concatenated in order (fri.hip).
+// serde_json text in pieces: fixed text, or a piece whose exact length is known before it is rendered
+// (size) and which renders straight into its place (write: returns the end, writes nothing past it), so
+// the whole text is sized once and its pieces written in parallel at their offsets (fri.hip).
 struct JsonPieces {
-  std::vector<std::function<void(std::string&)>> fns;
-  std::vector<std::string> done;  // pieces already rendered (prerender), in order before fns
+  struct Piece {
+    std::string text;                    // fixed (or prerendered) text when size is empty
+    std::function<size_t()> size;
+    std::function<char*(char*)> write;
+  };
+  std::vector<Piece> pieces;
   void text(const std::string& s);
   void bytes(const uint8_t* p, size_t n);  // p must outlive render()
+  // rows of row_len bytes, "[..],[..]" (the caller writes the brackets)
+  void byte_rows(const uint8_t* p, size_t rows, size_t row_len);
   void branches(const std::vector<uint8_t>& leaves, size_t leaf_len, const std::vector<uint8_t>& nodes, size_t k,
                 size_t depth);
   void render(std::string& o);
-  void render(JsonText& o);  // pieces rendered and copied to their offsets on the host workers
-  // renders the pieces added so far now (e.g. while the GPU still works), on up to max_threads host threads
+  void render(JsonText& o);  // sized, then every piece written at its offset on the host workers
+  // renders the pieces added so far into fixed text now (e.g. while the GPU still works)
   void prerender(unsigned max_threads = 16);
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
