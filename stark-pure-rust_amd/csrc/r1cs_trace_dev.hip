@@ -36,9 +36,11 @@ __device__ __forceinline__ fe reduce_any(fe v) {  // any 256-bit value < 5.3 p -
 }
 
 // from_bytes_le of witness values of `words` 32-bit words (run.rs:354-357).
+// (err, when given: the trace's wire-id flag, cleared here for slot_fill_kernel's atomicOr.)
 __global__ void wit_decode_kernel(const uint32_t* __restrict__ w, uint32_t words, uint64_t n, fe r2,
-                                  fe* __restrict__ wcan, fe* __restrict__ wmont) {
+                                  fe* __restrict__ wcan, fe* __restrict__ wmont, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && err) *err = 0;
   if (i >= n) return;
   fe v = fe_zero();
   for (uint32_t k = 0; k < words; ++k) v.w[k] = w[i * words + k];
@@ -60,6 +62,11 @@ struct FillArgs {
   uint32_t *keys, *vals;
   uint32_t* slot_wire;  // optional: the wire of every slot (prepared circuits)
   uint32_t* err;
+  // initialised here for the kernels behind (flags_kernel, perm_kernel): flag0 = flag1 = 1, flag2 = 0 on
+  // the 3 a_len trace rows, and the public wires' first uses "not found"
+  uint8_t* flags;
+  uint64_t* pf;
+  uint32_t n_public;
 };
 
 // The constraint whose slots contain slot j of a third: the last ci with base[ci] <= j (empty
@@ -81,7 +88,14 @@ __device__ __forceinline__ uint32_t owner_of(const uint32_t* __restrict__ base, 
 // (a factor may hold a thousand terms: bits.r1cs).
 __global__ void slot_fill_kernel(FillArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < a.n_public) a.pf[t] = ~0ull;
   if (t >= 3 * a.a_len) return;
+  {
+    const uint64_t os = 3 * a.a_len;
+    a.flags[t] = 1;
+    a.flags[os + t] = 1;
+    a.flags[2 * os + t] = 0;
+  }
   const uint32_t f = (uint32_t)(t / a.a_len), j = (uint32_t)(t - (uint64_t)f * a.a_len);
   const uint32_t ci = owner_of(a.base, a.n_constraints, j);
   const uint32_t b0 = a.base[ci], n_coeff = a.base[ci + 1] - b0, i = j - b0;
@@ -422,16 +436,15 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
   STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac, fac_n * 4, hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base, base_n * 4, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
-  STARK_HIP(ctx, hipMemsetAsync(A + o_pf, 0xFF, n_public * 8, s));
   fe* wcan = (fe*)(A + o_wcan);
   fe* wmont = (fe*)(A + o_wmont);
   uint32_t* err = (uint32_t*)(A + o_err);
   {
     uint64_t one_r[4];  // Montgomery image of R = R^2 mod p
     memcpy(one_r, F.one().v, 32);
-    hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(RAW + o_raw_w),
-                       wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), wcan, wmont);
+    hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(std::max<uint64_t>(n_wit, 1))), dim3(256), 0, s,
+                       (const uint32_t*)(RAW + o_raw_w), wh.field_size / 4, (uint64_t)n_wit,
+                       to_dev(F.from_canonical(one_r)), wcan, wmont, err);
   }
   FillArgs fa;
   fa.cons = RAW;
@@ -450,13 +463,14 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   fa.vals = (uint32_t*)(A + o_v);
   fa.slot_wire = nullptr;
   fa.err = err;
-  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * a_len)), dim3(256), 0, s, fa);
+  uint8_t* flags = A + o_flags;
+  fa.flags = flags;
+  fa.pf = (uint64_t*)(A + o_pf);
+  fa.n_public = (uint32_t)n_public;
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(std::max<uint64_t>(3 * a_len, n_public))), dim3(256), 0, s, fa);
   if (fa.wmont)
     hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
                        fa.comp);
-  uint8_t* flags = A + o_flags;
-  STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));  // flag0, flag1 = 1
-  STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
   hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
                      flags + os, flags + 2 * os);
   STARK_HIP(ctx, hipGetLastError());
@@ -552,7 +566,6 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac.data(), fac.size() * 4, hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base.data(), base.size() * 4, hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
-  STARK_HIP(ctx, hipMemsetAsync(A + o_pf, 0xFF, n_public * 8, s));
   FillArgs fa;
   fa.cons = A + o_cons;
   fa.fac_rec = (const uint32_t*)(A + o_fac);
@@ -570,13 +583,14 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   fa.vals = (uint32_t*)(A + o_v);
   fa.slot_wire = (uint32_t*)(A + o_sw);
   fa.err = (uint32_t*)(A + o_err);
-  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(3 * a_len)), dim3(256), 0, s, fa);
+  fa.flags = A + o_flags;
+  fa.pf = (uint64_t*)(A + o_pf);
+  fa.n_public = (uint32_t)n_public;
+  hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(std::max<uint64_t>(3 * a_len, n_public))), dim3(256), 0, s, fa);
   if (fa.wmont)
     hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
                        fa.comp);
   uint8_t* flags = A + o_flags;
-  STARK_HIP(ctx, hipMemsetAsync(flags, 1, 2 * os, s));
-  STARK_HIP(ctx, hipMemsetAsync(flags + 2 * os, 0, os, s));
   hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
                      flags + os, flags + 2 * os);
   STARK_HIP(ctx, hipGetLastError());
@@ -653,7 +667,7 @@ static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, co
   memcpy(one_r, F.one().v, 32);
   hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
                      wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), (fe*)(A + o_wcan),
-                     (fe*)(A + o_wmont));
+                     (fe*)(A + o_wmont), (uint32_t*)nullptr);
   hipLaunchKernelGGL(wit_fill_kernel, dim3(blocks(3 * c.a_len)), dim3(256), 0, s, 3 * c.a_len, c.slot_wire, c.coef,
                      (const fe*)(A + o_wcan), (const fe*)(A + o_wmont), (fe*)(A + o_wit), (fe*)(A + o_comp));
   hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)c.n_c)), dim3(256), 0, s, c.base, c.n_c, c.a_len,
