@@ -67,6 +67,7 @@ struct FillArgs {
   uint8_t* flags;
   uint64_t* pf;
   uint32_t n_public;
+  uint32_t* long_count;  // running_sum_kernel's long-factor counter, cleared here (or null)
 };
 
 // The constraint whose slots contain slot j of a third: the last ci with base[ci] <= j (empty
@@ -89,6 +90,7 @@ __device__ __forceinline__ uint32_t owner_of(const uint32_t* __restrict__ base, 
 __global__ void slot_fill_kernel(FillArgs a) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < a.n_public) a.pf[t] = ~0ull;
+  if (t == 0 && a.long_count) *a.long_count = 0;
   if (t >= 3 * a.a_len) return;
   {
     const uint64_t os = 3 * a.a_len;
@@ -127,15 +129,21 @@ __global__ void slot_fill_kernel(FillArgs a) {
   a.vals[push] = (uint32_t)slot;
 }
 
-// comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels).  The
-// terms are loaded sixteen at a time ahead of their additions, so a long factor (hundreds of terms in
-// pedersen_test, a thousand in bits.r1cs) waits for one memory latency per sixteen terms, not per term.
+// comp[slot] <- the factor's running sum up to slot (its terms were written by the fill kernels), one
+// thread per factor for factors of up to kLongFactor slots.  The terms are loaded sixteen at a time ahead
+// of their additions.  A longer factor (hundreds of terms in pedersen_test, a thousand in bits.r1cs) is
+// listed instead (list / count, the order of no consequence) for running_sum_long_kernel.
+constexpr uint32_t kLongFactor = 32;
 __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n_constraints, uint64_t a_len,
-                                   fe* __restrict__ comp) {
+                                   fe* __restrict__ comp, uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 3 * (uint64_t)n_constraints) return;
   const uint32_t ci = (uint32_t)(t / 3), f = (uint32_t)(t - 3 * (uint64_t)ci);
   const uint32_t b0 = base[ci], n_coeff = base[ci + 1] - b0;
+  if (n_coeff > kLongFactor) {
+    if (f == 0) list[atomicAdd(count, 1u)] = ci;
+    return;
+  }
   fe* c = comp + (uint64_t)f * a_len + b0;
   fe acc = fe_zero();
   constexpr uint32_t kAhead = 16;
@@ -152,6 +160,40 @@ __global__ void running_sum_kernel(const uint32_t* __restrict__ base, uint32_t n
       }
   }
 }
+
+// The listed long factors, one wave per factor (the grid's waves stride over the 3 count factors): 64
+// slots at a time, an inclusive scan across the wave (six shifted additions), plus the running total of
+// the slots before.  Field addition is associative, so the sums are the sequential ones.
+__global__ __launch_bounds__(256) void running_sum_long_kernel(const uint32_t* __restrict__ base,
+                                                               const uint32_t* __restrict__ list,
+                                                               const uint32_t* __restrict__ count, uint64_t a_len,
+                                                               fe* __restrict__ comp) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t items = 3 * *count;
+  for (uint32_t it = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; it < items; it += nw) {
+    const uint32_t ci = list[it / 3], f = it % 3;
+    const uint32_t b0 = base[ci], n = base[ci + 1] - b0;
+    fe* c = comp + (uint64_t)f * a_len + b0;
+    fe carry = fe_zero();
+    for (uint32_t o = 0; o < n; o += 64) {
+      const uint32_t i = o + lane;
+      fe x = i < n ? fe_load(c + i) : fe_zero();
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        fe y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y.w[k] = (uint32_t)__shfl_up((int)x.w[k], d, 64);
+        if (lane >= d) x = fe_add(x, y);
+      }
+      x = fe_add(x, carry);
+      if (i < n) fe_store(c + i, x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) carry.w[k] = (uint32_t)__shfl((int)x.w[k], 63, 64);
+    }
+  }
+}
+constexpr unsigned kLongSumBlocks = 256;
 
 // calc_flags (run.rs:283-308): flag1 = 0 at (last slot + 1) mod a_len in every
 // third, flag2 = 1 at each constraint's last slot (first third).
@@ -430,7 +472,8 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
                o_wmont = take((size_t)n_wit * 32), o_coef = take(os * 32), o_wit = take(os * 32),
                o_comp = take(os * 32), o_flags = take(3 * os), o_perm = take(os * 8), o_k = take(os * 4),
                o_v = take(os * 4), o_k2 = take(os * 4), o_v2 = take(os * 4), o_last = take((size_t)n_wires * 4),
-               o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp);
+               o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp), o_long = take((size_t)n_c * 4),
+               o_cnt = take(4);
   st = ensure_buf(ctx, ctx->trace_arena, off);
   if (st != STARK_OK) return st;
   uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
@@ -467,10 +510,14 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   fa.flags = flags;
   fa.pf = (uint64_t*)(A + o_pf);
   fa.n_public = (uint32_t)n_public;
+  uint32_t* long_list = (uint32_t*)(A + o_long);
+  uint32_t* long_cnt = (uint32_t*)(A + o_cnt);
+  fa.long_count = long_cnt;
   hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(std::max<uint64_t>(3 * a_len, n_public))), dim3(256), 0, s, fa);
-  if (fa.wmont)
-    hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
-                       fa.comp);
+  hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
+                     fa.comp, long_list, long_cnt);
+  hipLaunchKernelGGL(running_sum_long_kernel, dim3(kLongSumBlocks), dim3(256), 0, s, fa.base,
+                     (const uint32_t*)long_list, (const uint32_t*)long_cnt, a_len, fa.comp);
   hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
                      flags + os, flags + 2 * os);
   STARK_HIP(ctx, hipGetLastError());
@@ -586,10 +633,8 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   fa.flags = A + o_flags;
   fa.pf = (uint64_t*)(A + o_pf);
   fa.n_public = (uint32_t)n_public;
+  fa.long_count = nullptr;  // (circuit columns only: no running sums here)
   hipLaunchKernelGGL(slot_fill_kernel, dim3(blocks(std::max<uint64_t>(3 * a_len, n_public))), dim3(256), 0, s, fa);
-  if (fa.wmont)
-    hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)n_c)), dim3(256), 0, s, fa.base, n_c, a_len,
-                       fa.comp);
   uint8_t* flags = A + o_flags;
   hipLaunchKernelGGL(flags_kernel, dim3(blocks(n_c)), dim3(256), 0, s, (const uint32_t*)(A + o_base), n_c, a_len,
                      flags + os, flags + 2 * os);
@@ -657,7 +702,7 @@ static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, co
     return o;
   };
   const size_t o_w = take(wbytes), o_wcan = take((size_t)n_wit * 32), o_wmont = take((size_t)n_wit * 32),
-               o_wit = take(c.os * 32), o_comp = take(c.os * 32);
+               o_wit = take(c.os * 32), o_comp = take(c.os * 32), o_long = take((size_t)c.n_c * 4), o_cnt = take(4);
   st = ensure_buf(ctx, ctx->trace_arena, off);
   if (st != STARK_OK) return st;
   uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
@@ -667,11 +712,13 @@ static stark_status circuit_witness(stark_ctx* ctx, const PreparedCircuit& c, co
   memcpy(one_r, F.one().v, 32);
   hipLaunchKernelGGL(wit_decode_kernel, dim3(blocks(n_wit)), dim3(256), 0, s, (const uint32_t*)(A + o_w),
                      wh.field_size / 4, (uint64_t)n_wit, to_dev(F.from_canonical(one_r)), (fe*)(A + o_wcan),
-                     (fe*)(A + o_wmont), (uint32_t*)nullptr);
+                     (fe*)(A + o_wmont), (uint32_t*)(A + o_cnt));  // (clears the long-factor counter)
   hipLaunchKernelGGL(wit_fill_kernel, dim3(blocks(3 * c.a_len)), dim3(256), 0, s, 3 * c.a_len, c.slot_wire, c.coef,
                      (const fe*)(A + o_wcan), (const fe*)(A + o_wmont), (fe*)(A + o_wit), (fe*)(A + o_comp));
   hipLaunchKernelGGL(running_sum_kernel, dim3(blocks(3 * (uint64_t)c.n_c)), dim3(256), 0, s, c.base, c.n_c, c.a_len,
-                     (fe*)(A + o_comp));
+                     (fe*)(A + o_comp), (uint32_t*)(A + o_long), (uint32_t*)(A + o_cnt));
+  hipLaunchKernelGGL(running_sum_long_kernel, dim3(kLongSumBlocks), dim3(256), 0, s, c.base,
+                     (const uint32_t*)(A + o_long), (const uint32_t*)(A + o_cnt), c.a_len, (fe*)(A + o_comp));
   STARK_HIP(ctx, hipGetLastError());
   out->os = c.os;
   out->n_constraints = c.n_c;
