@@ -108,7 +108,9 @@ class Json {
     return k;
   }
   // A u8 array, each value handed to put (false: stop, malformed).  Tight loop: serde_json writes no
-  // whitespace, so the separator is checked before falling back to the general whitespace skip.
+  // whitespace, so the separator is checked before falling back to the general whitespace skip.  A number
+  // is read from its first four bytes without branching on its length (1-3 digits); like serde_json the
+  // reader refuses a leading zero ("05"), four or more digits and values above 255.
   template <class Put>
   void u8_array(Put put) {
     expect('[');
@@ -116,12 +118,27 @@ class Json {
     ws();
     for (;;) {
       unsigned v = 0;
-      int nd = 0;
-      while (p_ < e_ && (unsigned)(*p_ - '0') < 10u && nd < 4) {
-        v = 10 * v + (unsigned)(*p_++ - '0');
-        ++nd;
+      bool bad;
+      if (e_ - p_ >= 4) {
+        const unsigned b0 = (unsigned)(unsigned char)p_[0] - '0', b1 = (unsigned)(unsigned char)p_[1] - '0',
+                       b2 = (unsigned)(unsigned char)p_[2] - '0', b3 = (unsigned)(unsigned char)p_[3] - '0';
+        const unsigned d1 = b1 < 10u, d2 = d1 & (b2 < 10u), d3 = d2 & (b3 < 10u);
+        bad = b0 >= 10u || d3 || (b0 == 0 && d1);
+        v = b0;
+        v = d1 ? 10 * v + b1 : v;
+        v = d2 ? 10 * v + b2 : v;
+        p_ += 1 + d1 + d2;
+      } else {
+        int nd = 0;
+        unsigned first = 0;
+        while (p_ < e_ && (unsigned)(*p_ - '0') < 10u && nd < 4) {
+          if (nd == 0) first = (unsigned)(*p_ - '0');
+          v = 10 * v + (unsigned)(*p_++ - '0');
+          ++nd;
+        }
+        bad = nd == 0 || nd > 3 || (first == 0 && nd > 1);
       }
-      if (nd == 0 || v > 255 || !put((uint8_t)v)) {
+      if (bad || v > 255 || !put((uint8_t)v)) {
         ok = false;
         return;
       }

@@ -156,6 +156,10 @@ def test_json_reader_arena_edges(ctx, proofs):
     bad.append(json.dumps(b, separators=(",", ":")))
     bad.append(js.replace("[", "[0255,", 1))
     bad.append(js.replace("]]", "],[]]", 3))
+    # a leading zero on a leaf value, the array otherwise intact: serde_json refuses "07" (no value changes,
+    # so only the reader can reject it)
+    at = js.index('"leaf":[') + len('"leaf":[')
+    bad.append(js[:at] + "0" + js[at:])
     assert q["main_branches"]  # (the fixture is a full proof)
     for t in bad:
         with pytest.raises((StarkError, AssertionError)):
