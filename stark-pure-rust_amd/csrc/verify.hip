@@ -79,6 +79,8 @@ struct PreBranches {
 
 // A reader for exactly this schema: objects with string keys, arrays, u8 numbers.
 class Json {
+  static constexpr int kBranchDepth = 6;  // a Proof object's nesting in a StarkProof (at most; FRI branches)
+
  public:
   Json(const char* s, size_t n, PreBranches* pre = nullptr, uint8_t* arena = nullptr)
       : p_(s), e_(s + n), base_(s), pre_(pre), arena_(arena) {}
@@ -98,14 +100,120 @@ class Json {
   void expect(char c) {
     if (!accept(c)) ok = false;
   }
+  // A member name, unescaped (serde_json matches field names after decoding "\u0061" and the like).
   std::string key() {
     std::string k;
-    expect('"');
-    while (ok && p_ < e_ && *p_ != '"') k.push_back(*p_++);
-    if (p_ >= e_) ok = false;
-    ++p_;
+    ws();
+    if (!str(&k)) ok = false;
     expect(':');
     return k;
+  }
+  // A JSON string at p_ (serde_json's rules: escapes \" \\ \/ \b \f \n \r \t \uXXXX with surrogate pairs,
+  // no raw control characters, valid UTF-8), decoded into out when given.
+  bool str(std::string* out) {
+    if (p_ >= e_ || *p_ != '"') return false;
+    ++p_;
+    for (;;) {
+      if (p_ >= e_) return false;
+      const unsigned char c = (unsigned char)*p_++;
+      if (c == '"') return true;
+      if (c < 0x20) return false;
+      if (c == '\\') {
+        if (p_ >= e_) return false;
+        const char x = *p_++;
+        uint32_t cp;
+        switch (x) {
+          case '"': cp = '"'; break;
+          case '\\': cp = '\\'; break;
+          case '/': cp = '/'; break;
+          case 'b': cp = 8; break;
+          case 'f': cp = 12; break;
+          case 'n': cp = 10; break;
+          case 'r': cp = 13; break;
+          case 't': cp = 9; break;
+          case 'u': {
+            if (!hex4(&cp)) return false;
+            if (cp >= 0xDC00 && cp <= 0xDFFF) return false;  // a lone trailing surrogate
+            if (cp >= 0xD800 && cp <= 0xDBFF) {                // a leading one: its pair must follow
+              uint32_t lo;
+              if (e_ - p_ < 2 || p_[0] != '\\' || p_[1] != 'u') return false;
+              p_ += 2;
+              if (!hex4(&lo) || lo < 0xDC00 || lo > 0xDFFF) return false;
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            }
+            break;
+          }
+          default:
+            return false;
+        }
+        if (out) utf8(cp, *out);
+        continue;
+      }
+      if (c < 0x80) {
+        if (out) out->push_back((char)c);
+        continue;
+      }
+      // a multi-byte UTF-8 sequence: lead byte, continuation bytes, no overlong / surrogate / > U+10FFFF forms
+      const int n = c >= 0xF0 ? 3 : c >= 0xE0 ? 2 : c >= 0xC2 ? 1 : -1;
+      if (n < 0 || c > 0xF4 || e_ - p_ < n) return false;
+      uint32_t cp = c & (0x3F >> n);
+      for (int i = 0; i < n; ++i) {
+        const unsigned char d = (unsigned char)p_[i];
+        if ((d & 0xC0) != 0x80) return false;
+        cp = (cp << 6) | (d & 0x3F);
+      }
+      if ((n == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (n == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
+        return false;
+      if (out) out->append(p_ - 1, (size_t)n + 1);
+      p_ += n;
+    }
+  }
+  // Any JSON value, skipped: serde_json ignores the members of a struct that it does not know (no
+  // deny_unknown_fields on StarkProof, Proof or FriProof's variants).  depth: containers already open.
+  bool skip_value(int depth) {
+    ws();
+    if (p_ >= e_ || depth > 128) return false;  // (serde_json's recursion limit)
+    const char c = *p_;
+    if (c == '{' || c == '[') {
+      const char close = c == '{' ? '}' : ']';
+      ++p_;
+      if (accept(close)) return true;
+      do {
+        if (c == '{') {
+          ws();
+          if (!str(nullptr) || !accept(':')) return false;
+        }
+        if (!skip_value(depth + 1)) return false;
+      } while (accept(','));
+      return accept(close);
+    }
+    if (c == '"') return str(nullptr);
+    for (const char* lit : {"true", "false", "null"}) {
+      const size_t n = strlen(lit);
+      if ((size_t)(e_ - p_) >= n && memcmp(p_, lit, n) == 0) {
+        p_ += n;
+        return true;
+      }
+    }
+    // a number: -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+    auto digit = [&] { return p_ < e_ && (unsigned)(*p_ - '0') < 10u; };
+    if (p_ < e_ && *p_ == '-') ++p_;
+    if (!digit()) return false;
+    if (*p_ == '0') ++p_;
+    else
+      while (digit()) ++p_;
+    if (p_ < e_ && *p_ == '.') {
+      ++p_;
+      if (!digit()) return false;
+      while (digit()) ++p_;
+    }
+    if (p_ < e_ && (*p_ == 'e' || *p_ == 'E')) {
+      ++p_;
+      if (p_ < e_ && (*p_ == '+' || *p_ == '-')) ++p_;
+      if (!digit()) return false;
+      while (digit()) ++p_;
+    }
+    return true;
   }
   // A u8 array, each value handed to put (false: stop, malformed).  Tight loop: serde_json writes no
   // whitespace, so the separator is checked before falling back to the general whitespace skip.  A number
@@ -191,7 +299,9 @@ class Json {
     bool has_leaf = false, has_nodes = false;
     do {
       const std::string k = key();
-      if (k == "leaf") {
+      if ((k == "leaf" && has_leaf) || (k == "nodes" && has_nodes)) {
+        ok = false;  // serde_json: duplicate field
+      } else if (k == "leaf") {
         const size_t n = bytes_to(w, (size_t)(e_ - p_) / 2 + 1);
         b.leaf = Bytes{w, n};
         w += n;
@@ -208,7 +318,7 @@ class Json {
         }
         b.nodes = Bytes{n0, (size_t)(w - n0)};
         has_nodes = true;
-      } else {
+      } else if (ok && !skip_value(kBranchDepth)) {
         ok = false;
       }
     } while (ok && accept(','));
@@ -232,7 +342,9 @@ class Json {
       bool r = false, c = false, q = false;
       do {
         const std::string k = key();
-        if (k == "root2") {
+        if ((k == "root2" && r) || (k == "column_branches" && c) || (k == "poly_branches" && q)) {
+          ok = false;  // duplicate field
+        } else if (k == "root2") {
           digest(f.root2);
           r = true;
         } else if (k == "column_branches") {
@@ -241,22 +353,33 @@ class Json {
         } else if (k == "poly_branches") {
           branches(f.poly);
           q = true;
-        } else {
+        } else if (ok && !skip_value(4)) {
           ok = false;
         }
       } while (ok && accept(','));
       if (!(r && c && q)) ok = false;
     } else if (tag == "Last") {
       f.last = true;
-      if (key() != "last") ok = false;
-      expect('[');
-      if (ok && !accept(']')) {
-        do {
-          f.last_vals.emplace_back();
-          bytes(f.last_vals.back());
-        } while (ok && accept(','));
-        expect(']');
-      }
+      bool l = false;
+      do {
+        const std::string k = key();
+        if (k == "last" && l) {
+          ok = false;  // duplicate field
+        } else if (k == "last") {
+          l = true;
+          expect('[');
+          if (ok && !accept(']')) {
+            do {
+              f.last_vals.emplace_back();
+              bytes(f.last_vals.back());
+            } while (ok && accept(','));
+            expect(']');
+          }
+        } else if (ok && !skip_value(4)) {
+          ok = false;
+        }
+      } while (ok && accept(','));
+      if (!l) ok = false;
     } else {
       ok = false;
     }
@@ -268,12 +391,12 @@ class Json {
     int seen = 0;
     do {
       const std::string k = key();
-      if (k == "m_root") digest(pr.m_root), seen |= 1;
-      else if (k == "l_root") digest(pr.l_root), seen |= 2;
-      else if (k == "a_root") digest(pr.a_root), seen |= 4;
-      else if (k == "main_branches") branches(pr.main), seen |= 8;
-      else if (k == "linear_comb_branches") branches(pr.lcomb), seen |= 16;
-      else if (k == "fri_proof") {
+      if (k == "m_root" && !(seen & 1)) digest(pr.m_root), seen |= 1;
+      else if (k == "l_root" && !(seen & 2)) digest(pr.l_root), seen |= 2;
+      else if (k == "a_root" && !(seen & 4)) digest(pr.a_root), seen |= 4;
+      else if (k == "main_branches" && !(seen & 8)) branches(pr.main), seen |= 8;
+      else if (k == "linear_comb_branches" && !(seen & 16)) branches(pr.lcomb), seen |= 16;
+      else if (k == "fri_proof" && !(seen & 32)) {
         expect('[');
         if (!accept(']')) {
           do {
@@ -283,8 +406,9 @@ class Json {
           expect(']');
         }
         seen |= 32;
-      } else {
-        ok = false;
+      } else if (k == "m_root" || k == "l_root" || k == "a_root" || k == "main_branches" ||
+                 k == "linear_comb_branches" || k == "fri_proof" || !skip_value(1)) {
+        ok = false;  // a duplicate field (the first five arms above take only a first occurrence), or no value
       }
     } while (ok && accept(','));
     expect('}');
@@ -295,6 +419,35 @@ class Json {
  private:
   void ws() {
     while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_;
+  }
+  bool hex4(uint32_t* v) {
+    if (e_ - p_ < 4) return false;
+    uint32_t x = 0;
+    for (int i = 0; i < 4; ++i) {
+      const char c = *p_++;
+      const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+      if (d < 0) return false;
+      x = 16 * x + (uint32_t)d;
+    }
+    *v = x;
+    return true;
+  }
+  static void utf8(uint32_t cp, std::string& o) {
+    if (cp < 0x80) {
+      o.push_back((char)cp);
+    } else if (cp < 0x800) {
+      o.push_back((char)(0xC0 | (cp >> 6)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      o.push_back((char)(0xE0 | (cp >> 12)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      o.push_back((char)(0xF0 | (cp >> 18)));
+      o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
   }
   // The pre-parsed Branch starting exactly here, if any (offsets ascend with the reader).
   bool take_pre(Branch& b) {

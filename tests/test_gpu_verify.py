@@ -238,3 +238,38 @@ def test_cold_verify_synthetic_spot_sizes(ctx, log_steps):
         q[path[0]][path[1]]["leaf"][path[2]] ^= 1
         with pytest.raises(AssertionError):
             verify_with_wtns(ctx, r1, wt, q)
+
+
+
+def test_json_reader_follows_serde_on_fields(ctx, proofs):
+    """serde_json (run.rs:579, no deny_unknown_fields on StarkProof / Proof / FriProof) ignores members it
+    does not know -- any JSON value, escapes and nesting included -- matches member names after
+    unescaping, and refuses a duplicate field.  The reader does the same: extra members at every level
+    and reordered, escaped names still verify; duplicates, a bad escape and a leading zero inside an
+    ignored member are refused (StarkError)."""
+    from stark_amd import StarkError
+    from stark_amd.verify import verify_with_wtns
+    r1, wt, js = proofs["compute"]
+    p = json.loads(js)
+    junk = {"a": [1, -2.5e3, {"b": None, "c": [True, False, [], {}]}], "s": 'q"é\U0001F600 \x00/'}
+    q = {"extra": junk}
+    q.update(p)
+    q["zzz"] = 0
+    m0 = q["main_branches"][0]
+    q["main_branches"][0] = {"nodes": m0["nodes"], "x": junk, "leaf": m0["leaf"]}
+    q["linear_comb_branches"][1]["y"] = "z"
+    q["fri_proof"][0]["Middle"]["extra"] = [junk, 7]
+    q["fri_proof"][-1]["Last"]["e"] = {"k": junk}
+    text = json.dumps(q, separators=(",", ":"))
+    assert "\\u00e9" in text and "\\ud83d\\ude00" in text
+    text = text.replace('"root2"', '"root\\u0032"', 1)
+    assert verify_with_wtns(ctx, r1, wt, text)
+    dup_top = js[:-1] + ',"a_root":' + json.dumps(p["a_root"], separators=(",", ":")) + "}"
+    leaf = json.dumps(p["main_branches"][2]["leaf"], separators=(",", ":"))
+    dup_leaf = js.replace('{"leaf":' + leaf, '{"leaf":' + leaf + ',"leaf":' + leaf, 1)
+    assert dup_leaf != js
+    bad_escape = text.replace("\\u00e9", "\\x00e9", 1)
+    lead_zero = js.replace("{", '{"u":01,', 1)
+    for t in (dup_top, dup_leaf, bad_escape, lead_zero):
+        with pytest.raises(StarkError):
+            verify_with_wtns(ctx, r1, wt, t)
