@@ -42,6 +42,10 @@ uint32_t stark_abi_version(void);
  * 4 SSE2; the environment variable STARK_B2S_WIDTH=4|8 narrows it).  A diagnostic with no reference
  * counterpart (Proof::validate, commitment/src/merkle_tree.rs:25-43, is what those checks restate). */
 uint32_t stark_verify_simd_width(void);
+/* Bytes per SIMD register of the proof JSON writer's byte-array digits on this CPU (64 with AVX-512
+ * VBMI2, else 1: one table store per byte; STARK_JSON_SIMD=0 forces 1).  A diagnostic: the text is the
+ * same either way (serde_json's, utils.rs:122-130 / fri.rs:16-26). */
+uint32_t stark_json_simd_width(void);
 
 typedef enum {
   STARK_OK = 0,

@@ -6,10 +6,15 @@ sys.path[:0] = [os.path.join(R, "stark-pure-rust_amd"), os.path.join(R, "tools")
 import stark_amd as S
 from stark_amd.r1cs import prove_with_witness
 import synth_r1cs
-r, w = synth_r1cs.for_steps(20)
+FX = os.environ.get("FIXTURE", "")
+if FX:
+    d = os.path.join(R, "tests", "golden", "r1cs")
+    r, w = open(f"{d}/{FX}.r1cs", "rb").read(), open(f"{d}/{FX}.wtns", "rb").read()
+else:
+    r, w = synth_r1cs.for_steps(20)
 ctx = S.Context(0)
 p = None
-for i in range(5):
+for i in range(int(os.environ.get("REPS", "5"))):
     t0 = time.perf_counter()
     p = None
     t1 = time.perf_counter()

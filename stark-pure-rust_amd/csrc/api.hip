@@ -10,6 +10,7 @@
 
 #include "internal.h"
 #include "host_b2s.h"
+#include "host_json.h"
 #include "blake2s.h"
 
 namespace stark {
@@ -335,6 +336,23 @@ void HostTask::wait() {
 unsigned host_threads() { return HostWorkers::get().threads(); }
 void host_parallel(unsigned n, const std::function<void(unsigned)>& fn) { HostWorkers::get().run(n, fn); }
 
+void host_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPiece = (size_t)256 << 10;
+  if (n < ((size_t)1 << 20)) {
+    memcpy(dst, src, n);
+    return;
+  }
+  const size_t pieces = (n + kPiece - 1) / kPiece;
+  std::atomic<size_t> next{0};
+  const unsigned nt = (unsigned)std::min<size_t>(host_threads(), pieces);
+  host_parallel(nt, [&](unsigned) {
+    for (size_t i; (i = next.fetch_add(1)) < pieces;) {
+      const size_t o = i * kPiece;
+      memcpy((char*)dst + o, (const char*)src + o, std::min(kPiece, n - o));
+    }
+  });
+}
+
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out) {
   if (ctx->pinned_bytes[slot] < bytes) {
     if (ctx->pinned[slot]) {
@@ -438,6 +456,7 @@ const char* stark_status_str(stark_status s) {
 
 uint32_t stark_abi_version(void) { return STARK_ABI_VERSION; }
 uint32_t stark_verify_simd_width(void) { return (uint32_t)b2s_paths_width(); }
+uint32_t stark_json_simd_width(void) { return (uint32_t)json_simd_width(); }
 
 stark_status stark_ctx_create(int device, stark_ctx** out) {
   if (!out) return STARK_ERR_BAD_ARG;

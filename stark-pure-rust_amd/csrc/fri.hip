@@ -27,6 +27,7 @@
 
 #include "internal.h"
 #include "blake2s.h"
+#include "host_json.h"
 
 
 struct stark_fri_layer {
@@ -375,7 +376,18 @@ static char* json_bytes_at(char* w, const uint8_t* p, size_t n) {
   static const ByteText T;
   *w++ = '[';
   if (n) {
-    for (size_t i = 0; i + 1 < n; ++i) {
+    size_t i = 0;
+    if (n >= 16 && json_simd_width() == 64) {
+      // 16 items at a time, each with its comma; when they cover every byte the last comma is the ']'
+      const size_t k = n / 16;
+      w = json_items16_v512(w, p, k);
+      i = 16 * k;
+      if (i == n) {
+        w[-1] = ']';
+        return w;
+      }
+    }
+    for (; i + 1 < n; ++i) {
       const uint8_t b = p[i];
       memcpy(w, &T.s[b], 4);
       w += T.len[b];
@@ -391,7 +403,9 @@ static char* json_bytes_at(char* w, const uint8_t* p, size_t n) {
 // Its exact length: 2 + the digits + n - 1 commas.
 static size_t json_bytes_len(const uint8_t* p, size_t n) {
   size_t d = 0;
-  for (size_t i = 0; i < n; ++i) d += 1 + (p[i] >= 10) + (p[i] >= 100);
+  if (json_simd_width() == 64) d = json_digits_v512(p, n);
+  else
+    for (size_t i = 0; i < n; ++i) d += 1 + (p[i] >= 10) + (p[i] >= 100);
   return 2 + d + (n ? n - 1 : 0);
 }
 
@@ -683,6 +697,8 @@ stark_status stark_r1cs_proof_json_from_parts(const uint8_t m_root[32], const ui
   const std::vector<uint8_t> ml = vec(mb.leaves, mb.k * mb.leaf_len), mn = vec(mb.nodes, mb.k * mb.depth * 32);
   const std::vector<uint8_t> ll = vec(lb.leaves, lb.k * lb.leaf_len), ln = vec(lb.nodes, lb.k * lb.depth * 32);
   stark_fri_proof fri;
+  for (size_t l = 0; l < n_layers; ++l)  // FRI leaves are field elements (fri.rs:16-26): 32 B each
+    if (layers[l].column.leaf_len != 32 || layers[l].poly.leaf_len != 32) return STARK_ERR_BAD_ARG;
   for (size_t l = 0; l < n_layers; ++l) {
     const stark_fri_layer_parts& P = layers[l];
     stark_fri_layer L;

@@ -232,6 +232,8 @@ stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_
 // millisecond-scale work it splits).  host_threads() = workers + 1 (<= 16).
 unsigned host_threads();
 void host_parallel(unsigned n, const std::function<void(unsigned)>& fn);
+// memcpy, split over the host workers from 1 MB on (a multi-MB proof text into caller memory).
+void host_memcpy(void* dst, const void* src, size_t n);
 // A task run on the process's side thread while the caller goes on (the caller waits for it with
 // wait() or the destructor, so the task may use the caller's locals).  When the side thread is busy
 // with another caller's task, the task runs inline in the constructor.

@@ -2008,7 +2008,7 @@ stark_status stark_r1cs_proof_json(const stark_r1cs_proof* proof, char* buf, siz
   *len = proof->json.size();
   if (buf && cap) {
     const size_t k = proof->json.size() < cap ? proof->json.size() : cap;
-    memcpy(buf, proof->json.data(), k);
+    host_memcpy(buf, proof->json.data(), k);
     if (k < cap) buf[k] = 0;
   }
   return STARK_OK;

@@ -47,6 +47,7 @@ _vp = ctypes.c_void_p
 _SIGNATURES = {
     "stark_abi_version": ([], ctypes.c_uint32),
     "stark_verify_simd_width": ([], ctypes.c_uint32),
+    "stark_json_simd_width": ([], ctypes.c_uint32),
     "stark_ctx_create": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_ctx_destroy": ([_vp], None),
     "stark_status_str": ([ctypes.c_int], ctypes.c_char_p),

@@ -12,6 +12,7 @@ Everything runs in libstark_hip.so; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import sys
 
 import numpy as np
 
@@ -26,6 +27,29 @@ _decode_ascii.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_char_p]
 def ascii_at(ptr: int, n: int) -> str:
     """The n ASCII bytes at address ptr as a str (UnicodeDecodeError on a non-ASCII byte)."""
     return _decode_ascii(ptr, n, None) if n else ""
+
+
+# PyUnicode_New(n, 127): a compact ASCII str whose n + 1 data bytes follow the object header, filled by
+# the library in place (stark_r1cs_proof_json copies a multi-MB text on its host workers) instead of
+# one decode pass on this thread.  The header size is checked once against a known string; when the
+# layout is not the expected one, to_json decodes instead.
+_unicode_new = ctypes.pythonapi.PyUnicode_New
+_unicode_new.restype = ctypes.py_object
+_unicode_new.argtypes = [ctypes.c_ssize_t, ctypes.c_uint32]
+
+
+def _ascii_header():
+    try:
+        h = sys.getsizeof("") - 1
+        probe = "".join(["stark", "-ascii-", "probe"])
+        if ctypes.string_at(id(probe) + h, len(probe) + 1) == probe.encode() + b"\0":
+            return h
+    except Exception:
+        pass
+    return None
+
+
+_ASCII_HEADER = _ascii_header()
 
 
 class StarkProof:
@@ -48,7 +72,15 @@ class StarkProof:
         p = ctypes.c_void_p()
         n = ctypes.c_size_t(0)
         self.lib.stark_r1cs_proof_json_view(self.h, ctypes.byref(p), ctypes.byref(n))
-        return ascii_at(p.value, n.value)
+        if _ASCII_HEADER is None or n.value < (1 << 20):
+            return ascii_at(p.value, n.value)
+        s = _unicode_new(n.value, 127)
+        got = ctypes.c_size_t(0)
+        dst = ctypes.cast(id(s) + _ASCII_HEADER, ctypes.c_char_p)
+        rc = self.lib.stark_r1cs_proof_json(self.h, dst, n.value + 1, ctypes.byref(got))
+        if rc != 0 or got.value != n.value:
+            raise StarkError(rc, "stark_r1cs_proof_json", f"{got.value} of {n.value} bytes")
+        return s
 
     def roots(self) -> dict:
         m, l, a = (ctypes.create_string_buffer(32) for _ in range(3))
