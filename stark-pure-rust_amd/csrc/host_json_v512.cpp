@@ -38,6 +38,8 @@ struct Digits {
   }
 };
 
+// full: store all 64 bytes (the caller's next group overwrites what lies past this one's end)
+template <bool full>
 inline char* items16(char* w, const uint8_t* p, const Digits& D) {
   const __m512i in = _mm512_castsi128_si512(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p)));
   const __m512i b = _mm512_permutexvar_epi8(D.spread, in);  // byte i/4 in every lane of slot i/4
@@ -58,7 +60,8 @@ inline char* items16(char* w, const uint8_t* p, const Digits& D) {
   const __mmask64 keep = (ge100 & D.p0) | (ge10 & D.p1) | D.p2 | D.p3;
   const __m512i out = _mm512_maskz_compress_epi8(keep, t);
   const unsigned len = (unsigned)_mm_popcnt_u64((unsigned long long)keep);
-  _mm512_mask_storeu_epi8(w, (__mmask64)(len == 64 ? ~0ull : ((1ull << len) - 1)), out);
+  if (full) _mm512_storeu_si512(w, out);
+  else _mm512_mask_storeu_epi8(w, (__mmask64)(len == 64 ? ~0ull : ((1ull << len) - 1)), out);
   return w + len;
 }
 
@@ -66,8 +69,9 @@ inline char* items16(char* w, const uint8_t* p, const Digits& D) {
 
 char* json_items16_v512(char* w, const uint8_t* p, size_t k) {
   static const Digits D;
-  for (size_t i = 0; i < k; ++i) w = items16(w, p + 16 * i, D);
-  return w;
+  if (!k) return w;
+  for (size_t i = 0; i + 1 < k; ++i) w = items16<true>(w, p + 16 * i, D);
+  return items16<false>(w, p + 16 * (k - 1), D);  // the last group writes nothing past its end
 }
 
 size_t json_digits_v512(const uint8_t* p, size_t n) {
