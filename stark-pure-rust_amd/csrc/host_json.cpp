@@ -7,7 +7,9 @@ namespace stark {
 
 static int pick_json_width() {
   const bool have = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
-                    __builtin_cpu_supports("avx512vbmi") && __builtin_cpu_supports("avx512vbmi2");
+                    __builtin_cpu_supports("avx512vl") && __builtin_cpu_supports("avx512vbmi") &&
+                    __builtin_cpu_supports("avx512vbmi2") && __builtin_cpu_supports("bmi") &&
+                    __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("popcnt");
   const char* e = getenv("STARK_JSON_SIMD");
   const bool want = !(e && e[0] == '0');
   return have && want ? 64 : 1;

@@ -10,6 +10,10 @@ namespace stark {
 // Writes "b," for each of the 16 k bytes at p (every item followed by its comma) and returns the end;
 // nothing past the end is written.
 char* json_items16_v512(char* w, const uint8_t* p, size_t k);
+// The reader's side: the numbers of a compact u8 array whose text starts after its '[' at p, written to
+// out[0..max), their count in *count and the end (past ']') returned; nullptr when the text is anything
+// but "d,d,...,d]" with serde_json's canonical numbers 0..255 (the scalar reader then decides it).
+const char* json_u8s_v512(const char* p, const char* e, uint8_t* out, size_t max, size_t* count);
 // Number of decimal digits of the n bytes at p.
 size_t json_digits_v512(const uint8_t* p, size_t n);
 

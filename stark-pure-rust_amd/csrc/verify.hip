@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "host_json.h"
 #include "blake2s.h"
 #include "host_b2s.h"
 
@@ -278,6 +279,14 @@ class Json {
   }
   // Into out[0..max): the count (a longer array is malformed).
   size_t bytes_to(uint8_t* out, size_t max) {
+    if (p_ < e_ && *p_ == '[' && json_simd_width() == 64) {
+      // the compact form in AVX-512 registers; any other text is re-read by the scalar loop below
+      size_t n = 0;
+      if (const char* r = json_u8s_v512(p_ + 1, e_, out, max, &n)) {
+        p_ = r;
+        return n;
+      }
+    }
     size_t k = 0;
     u8_array([&](uint8_t v) {
       if (k == max) return false;
