@@ -491,12 +491,14 @@ void pre_parse_branches(const char* s, size_t n, PreBranches& P, uint8_t* arena)
   host_parallel(parts, [&](unsigned t) {
     const size_t lo = n * t / parts, hi = n * (t + 1) / parts;  // starts in [lo, hi)
     const char* p = s + lo;
-    const char* end = s + std::min(n, hi + klen - 1);
-    while (p < end) {
-      const void* q = memmem(p, (size_t)(end - p), kKey, klen);
+    // every '{' by memchr (vectorised; in serde's text '{' opens objects only, most of them branches),
+    // then the key compared in place
+    const char* const stop = s + std::min(n, hi);  // (a match starting before hi may end past it)
+    while (p < stop) {
+      const char* q = (const char*)memchr(p, '{', (size_t)(stop - p));
       if (!q) break;
-      found[t].push_back((size_t)((const char*)q - s));
-      p = (const char*)q + 1;
+      if ((size_t)(s + n - q) >= klen && memcmp(q, kKey, klen) == 0) found[t].push_back((size_t)(q - s));
+      p = q + 1;
     }
   });
   for (auto& f : found) P.off.insert(P.off.end(), f.begin(), f.end());
