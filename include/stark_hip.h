@@ -34,8 +34,9 @@
 extern "C" {
 #endif
 
-/* 2: stark_r1cs_proof_branches takes leaves_cap / nodes_cap (round 4). */
-#define STARK_ABI_VERSION 2u
+/* 2: stark_r1cs_proof_branches takes leaves_cap / nodes_cap (round 4).
+ * 3: device groups, stark_group_* (round 6). */
+#define STARK_ABI_VERSION 3u
 /* The ABI version the loaded library implements (no reference counterpart: a linking check). */
 uint32_t stark_abi_version(void);
 /* Paths per SIMD register of the verifier's host Merkle path checks on this CPU (16 AVX-512, 8 AVX2,
@@ -441,6 +442,65 @@ stark_status stark_dprove_lincomb(stark_dprove* h, const uint8_t m_root[32], uin
 /* Same with m_root in device memory (4-B aligned): asynchronous on the stream given at begin. */
 stark_status stark_dprove_lincomb_dev(stark_dprove* h, const uint8_t* d_m_root, uint64_t** l_dev);
 void stark_dprove_free(stark_dprove* h);
+
+/* ---- device groups: one call over G GPUs (SURVEY.md 8(b) "Multi-GPU is a ctx group created once", 8(e))
+ * The reference parallelises a call over the thread pool the call builds (Worker::new inside best_fft,
+ * fri/src/fft.rs:332; commitment/src/multicore.rs:43-45).  A group is that pool with GPUs as its workers:
+ * created once from a device list (a device may repeat: G contexts on one GPU run the same code), then
+ * passed to the group entry points, which keep the reference's signatures and return what the
+ * single-context calls return, bit for bit.  The members exchange data by peer copies on their own
+ * streams (xGMI between devices); no collective library and no process per GPU is needed.  A group is
+ * not shared between threads (it runs its members on threads of its own). */
+typedef struct stark_group stark_group;
+typedef struct stark_group_tree stark_group_tree;
+/* g = 1, 2, 4 or 8 members on devices[0..g). */
+stark_status stark_group_create(const int* devices, uint32_t g, stark_group** out);
+void stark_group_destroy(stark_group* group);
+uint32_t stark_group_size(const stark_group* group);
+/* Member i's context (owned by the group): for _dev calls and device memory on that member. */
+stark_ctx* stark_group_ctx(stark_group* group, uint32_t i);
+const char* stark_group_last_error(const stark_group* group);
+stark_status stark_group_synchronize(stark_group* group);
+/* best_fft / inv_best_fft (fft.rs:327-379) with the group as the worker pool: the one-exchange cyclic
+ * NTT (member r transforms x[r + G j], one all-to-all, G-point DFTs across the received chunks);
+ * transforms smaller than 2^(2 log2 G) run on member 0.  Same arguments and output as stark_best_fft. */
+stark_status stark_group_best_fft(stark_group* group, const uint64_t* coeffs, size_t len, const uint64_t root[4],
+                                  uint32_t log_n, uint64_t* out);
+stark_status stark_group_inv_best_fft(stark_group* group, const uint64_t* evals, size_t len, const uint64_t root[4],
+                                      uint32_t log_n, uint64_t* out);
+/* Device-resident form: member r's d_shards[r] holds x[r + G j], j < M = 2^log_n / G (destroyed);
+ * d_out[r] receives X[r c + i + M k1] at k1 c + i, k1 < G, i < c = M / G.  log_n >= 2 log2 G.
+ * Asynchronous on the member contexts' streams (stark_group_synchronize). */
+stark_status stark_group_ntt_dev(stark_group* group, uint64_t* const* d_shards, uint64_t* const* d_out,
+                                 uint32_t log_n, const uint64_t root[4], int inverse);
+/* MerkleTree<Vec<u8>, BlakeDigest> (merkle_tree.rs:60-73) over the group: member r hashes leaves
+ * [r m, (r+1) m), m = n / G (n >= G; smaller trees live on member 0), its subtree root goes to
+ * member 0, which hashes the top log2 G levels -- the reference's own subtree + top-tree split
+ * (merkle_proof_in_place.rs:106-206), so roots and paths equal the single tree's. */
+stark_status stark_group_merkle_new(stark_group* group, stark_group_tree** out);
+void stark_group_merkle_free(stark_group_tree* tree);
+/* update(leaves) (merkle_proof_in_place.rs:37-42): n (a power of two) leaves of leaf_len bytes. */
+stark_status stark_group_merkle_update(stark_group_tree* tree, const uint8_t* leaves, size_t n, size_t leaf_len);
+/* Same with the leaves in device memory: d_blocks[r] = member r's block of m leaves (d_blocks[0] = all n
+ * leaves when n < G). */
+stark_status stark_group_merkle_update_dev(stark_group_tree* tree, const uint8_t* const* d_blocks, size_t n,
+                                           size_t leaf_len);
+size_t stark_group_merkle_width(const stark_group_tree* tree);
+/* get_root() / gen_proofs(indices) as stark_merkle_get_root / stark_merkle_gen_proofs. */
+stark_status stark_group_merkle_get_root(const stark_group_tree* tree, uint8_t root[32], size_t* root_len);
+stark_status stark_group_merkle_gen_proofs(stark_group_tree* tree, const size_t* indices, size_t k,
+                                           uint8_t* leaves_out, uint8_t* nodes_out);
+/* prove_with_witness (run.rs:310-452) with one proof shared by the group: member r owns
+ * the precision-domain points r + G j; coset LDEs, constraints and FRI folds are local, each Merkle tree
+ * is one digest all-to-all; the proof equals stark_prove_r1cs_bytes' byte for byte. */
+stark_status stark_group_prove_r1cs_bytes(stark_group* group, const uint8_t* r1cs, size_t r1cs_len,
+                                          const uint8_t* wtns, size_t wtns_len, stark_r1cs_proof** out);
+/* The .r1cs-only work of that proof done once per member (circuits[r] on member r, G handles, freed with
+ * stark_r1cs_circuit_free), and a proof of one witness with it (as stark_r1cs_circuit_new / _prove). */
+stark_status stark_group_circuit_new(stark_group* group, const uint8_t* r1cs, size_t r1cs_len,
+                                     stark_r1cs_circuit** circuits);
+stark_status stark_group_prove_r1cs_circuit(stark_group* group, stark_r1cs_circuit* const* circuits,
+                                            const uint8_t* wtns, size_t wtns_len, stark_r1cs_proof** out);
 
 /* ---- device memory helpers (for callers without their own allocator) ------ */
 stark_status stark_dev_alloc(stark_ctx* ctx, size_t bytes, void** d_ptr);

@@ -30,20 +30,6 @@
 #include "host_json.h"
 
 
-struct stark_fri_layer {
-  bool last = false;
-  uint8_t root2[32];
-  size_t col_depth = 0, poly_depth = 0;
-  std::vector<size_t> col_idx, poly_idx;
-  std::vector<uint8_t> col_leaves, col_nodes;    // 32 B leaves, depth*32 B paths
-  std::vector<uint8_t> poly_leaves, poly_nodes;
-  std::vector<uint8_t> last_values;              // n * 32 B
-};
-
-struct stark_fri_proof {
-  std::vector<stark_fri_layer> layers;
-};
-
 namespace stark {
 
 // special_x = T::from_bytes_le(m_root) (fri.rs:135) computed on the device from

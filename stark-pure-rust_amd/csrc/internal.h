@@ -17,6 +17,7 @@
 #include "stark_hip.h"
 #include "fp_dev.h"
 #include "fp_host.h"
+#include "host_pool.h"
 
 namespace stark {
 
@@ -226,28 +227,6 @@ stark_status multi_inv_down(stark_ctx* ctx, const InvPlan& plan, hipStream_t s);
 fe* multi_inv_h_top(stark_ctx* ctx, int k);  // top array k < 2 in pinned slot 1 (null: no pinned memory)
 stark_status multi_inv_device(stark_ctx* ctx, const fe* d_in, fe* d_out, uint64_t n, hipStream_t s);
 
-// Host worker threads shared by the host-side stages (trace build, proof
-// JSON): host_parallel(n, fn) runs fn(0) .. fn(n-1), fn(0) on the caller, the
-// rest on persistent workers (spawning threads per call costs more than the
-// millisecond-scale work it splits).  host_threads() = workers + 1 (<= 16).
-unsigned host_threads();
-void host_parallel(unsigned n, const std::function<void(unsigned)>& fn);
-// memcpy, split over the host workers from 1 MB on (a multi-MB proof text into caller memory).
-void host_memcpy(void* dst, const void* src, size_t n);
-// A task run on the process's side thread while the caller goes on (the caller waits for it with
-// wait() or the destructor, so the task may use the caller's locals).  When the side thread is busy
-// with another caller's task, the task runs inline in the constructor.
-class HostTask {
- public:
-  explicit HostTask(std::function<void()> fn);
-  ~HostTask() { wait(); }
-  void wait();
-  HostTask(const HostTask&) = delete;
-  HostTask& operator=(const HostTask&) = delete;
-
- private:
-  uint64_t ticket_ = 0;  // 0: ran inline or already waited for
-};
 // Context-owned Merkle tree slot (created on first use).
 stark_status ctx_tree(stark_ctx* ctx, int slot, stark_merkle_tree** out);
 hipStream_t pick_stream(stark_ctx* ctx, void* stream);
@@ -337,6 +316,36 @@ struct JsonPieces {
   void prerender(unsigned max_threads = 16);
 };
 void fri_proof_json_pieces(const stark_fri_proof* proof, JsonPieces& j);
+
+}  // namespace stark
+
+// FRI and StarkProof values held by the library (fri.hip, r1cs.hip, group.hip).
+struct stark_fri_layer {
+  bool last = false;
+  uint8_t root2[32];
+  size_t col_depth = 0, poly_depth = 0;
+  std::vector<size_t> col_idx, poly_idx;
+  std::vector<uint8_t> col_leaves, col_nodes;    // 32 B leaves, depth*32 B paths
+  std::vector<uint8_t> poly_leaves, poly_nodes;
+  std::vector<uint8_t> last_values;              // n * 32 B
+};
+
+struct stark_fri_proof {
+  std::vector<stark_fri_layer> layers;
+};
+
+struct stark_r1cs_proof {
+  uint8_t m_root[32], l_root[32], a_root[32];
+  stark::JsonText json;
+  // The parts, for callers that build their own StarkProof value (stark_r1cs_proof_branches / _fri):
+  // main and linear-combination openings (leaves, then depth siblings per opening, leaf to root).
+  size_t depth = 0;
+  std::vector<uint8_t> m_leaves, m_nodes, l_leaves, l_nodes;
+  stark_fri_proof* fri = nullptr;
+  ~stark_r1cs_proof() { stark_fri_proof_free(fri); }
+};
+
+namespace stark {
 
 // R1CS v1 / wtns v2 headers (circom2bellman_core/src/reader.rs:4-89,
 // r1cs-stark/src/reader.rs:7-42), r1cs_trace.hip.

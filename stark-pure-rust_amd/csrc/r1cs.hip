@@ -36,17 +36,6 @@ void json_branches(std::string& o, const std::vector<uint8_t>& leaves, size_t le
 void fri_proof_json_string(const stark_fri_proof* proof, std::string& o);
 }  // namespace stark
 
-struct stark_r1cs_proof {
-  uint8_t m_root[32], l_root[32], a_root[32];
-  stark::JsonText json;
-  // The parts, for callers that build their own StarkProof value (stark_r1cs_proof_branches / _fri):
-  // main and linear-combination openings (leaves, then depth siblings per opening, leaf to root).
-  size_t depth = 0;
-  std::vector<uint8_t> m_leaves, m_nodes, l_leaves, l_nodes;
-  stark_fri_proof* fri = nullptr;
-  ~stark_r1cs_proof() { stark_fri_proof_free(fri); }
-};
-
 namespace stark {
 
 static inline fe fe_zero_host() {

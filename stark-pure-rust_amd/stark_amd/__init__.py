@@ -157,6 +157,28 @@ _SIGNATURES = {
                                   ctypes.c_int),
     "stark_verify_r1cs_bytes": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                  ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "stark_group_create": ([ctypes.POINTER(ctypes.c_int), ctypes.c_uint32, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_group_destroy": ([_vp], None),
+    "stark_group_size": ([_vp], ctypes.c_uint32),
+    "stark_group_ctx": ([_vp, ctypes.c_uint32], _vp),
+    "stark_group_last_error": ([_vp], ctypes.c_char_p),
+    "stark_group_synchronize": ([_vp], ctypes.c_int),
+    "stark_group_best_fft": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p], ctypes.c_int),
+    "stark_group_inv_best_fft": ([_vp, _u64p, ctypes.c_size_t, _u64p, ctypes.c_uint32, _u64p], ctypes.c_int),
+    "stark_group_ntt_dev": ([_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.c_uint32, _u64p, ctypes.c_int],
+                            ctypes.c_int),
+    "stark_group_merkle_new": ([_vp, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_group_merkle_free": ([_vp], None),
+    "stark_group_merkle_update": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_size_t], ctypes.c_int),
+    "stark_group_merkle_update_dev": ([_vp, ctypes.POINTER(_vp), ctypes.c_size_t, ctypes.c_size_t], ctypes.c_int),
+    "stark_group_merkle_width": ([_vp], ctypes.c_size_t),
+    "stark_group_merkle_get_root": ([_vp, ctypes.c_char_p, _szp], ctypes.c_int),
+    "stark_group_merkle_gen_proofs": ([_vp, _szp, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+    "stark_group_prove_r1cs_bytes": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                      ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_group_circuit_new": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_vp)], ctypes.c_int),
+    "stark_group_prove_r1cs_circuit": ([_vp, ctypes.POINTER(_vp), ctypes.c_char_p, ctypes.c_size_t,
+                                        ctypes.POINTER(_vp)], ctypes.c_int),
     "stark_verify_with_witness": ([_vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                    ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
 }

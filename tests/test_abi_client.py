@@ -5,7 +5,10 @@
 * tests/abi_client/prover_flow.cpp: the whole-prover routes (prove_with_witness on raw bytes, run.rs:
   310-452; mk_r1cs_proof on the exported trace vectors, prove.rs:14) and a StarkProof rebuilt from the
   structured parts (roots, branches, FRI layers) as the shim builds StarkProof<H> without serde; all
-  four texts equal the golden StarkProof digests.
+  four texts equal the golden StarkProof digests;
+* tests/abi_client/group_flow.cpp: the device-group entry points (stark_group_*)
+  at G = 2, 4, 8 members on one GPU: best_fft / inv_best_fft equal the oracle, the group Merkle root and
+  paths equal the oracle's single tree, and the group's proofs (cold and prepared) equal the golden digests.
 CPU: the programs build and link against libstark_hip.so."""
 import os
 import struct
@@ -20,10 +23,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CLIENT = os.path.join(HERE, "abi_client")
 BIN = os.path.join(CLIENT, "shim_flow")
 PROVER = os.path.join(CLIENT, "prover_flow")
+GROUP = os.path.join(CLIENT, "group_flow")
 FIX = os.path.join(HERE, "golden", "r1cs")
 
 
-@pytest.mark.parametrize("prog", [BIN, PROVER])
+@pytest.mark.parametrize("prog", [BIN, PROVER, GROUP])
 def test_client_builds_and_links(prog):
     subprocess.run(["make", "-s", "-C", CLIENT], check=True)
     out = subprocess.run(["ldd", prog], capture_output=True, text=True, check=True).stdout
@@ -70,3 +74,37 @@ def test_client_matches_oracle(oracle, tmp_path, log_n, exclude):
     assert leaves == b"".join(evals[i].tobytes() for i in idx)
     want = oracle.prove_low_degree_json(evals, w, n // 4, exclude, chunks=4)
     assert (tmp_path / "fri.json").read_text() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,name", [(2, "compute"), (4, "poseidon3_test"), (8, "pedersen_test")])
+def test_group_client_matches_oracle(oracle, tmp_path, G, name):
+    """The group entry points from C++ (G members on device 0): NTT and inverse vs the oracle, the Merkle
+    root and paths vs the oracle's single tree, and both proofs vs the golden digest."""
+    import hashlib
+    import json
+    assert os.path.exists(GROUP), "build() compiles tests/abi_client/group_flow"
+    log_n = 16
+    n = 1 << log_n
+    coeffs = O.random_elements(n // 4 + 5, 0x5EED0800 + G)
+    w = O.root_of_unity(log_n)
+    idx = [0, 1, n - 1, 7, 7, n // 2 + 3, n // G]
+    blob = struct.pack("<4I", log_n, len(coeffs), len(idx), 0) + O.to_limbs([w]).tobytes() + \
+        coeffs.tobytes() + np.array(idx, dtype=np.uint64).tobytes()
+    (tmp_path / "in.bin").write_bytes(blob)
+    r = subprocess.run([GROUP, str(G), str(tmp_path / "in.bin"), os.path.join(FIX, f"{name}.r1cs"),
+                        os.path.join(FIX, f"{name}.wtns"), str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    evals = np.frombuffer((tmp_path / "evals.bin").read_bytes(), dtype=np.uint64).reshape(-1, 4)
+    assert np.array_equal(evals, oracle.best_fft(coeffs, w, log_n, cpus=8))
+    back = np.frombuffer((tmp_path / "inv.bin").read_bytes(), dtype=np.uint64).reshape(-1, 4)
+    assert np.array_equal(back[:len(coeffs)], coeffs) and not back[len(coeffs):].any()
+    root, paths = oracle.merkle(evals.tobytes(), n, 32, idx, chunks=4)
+    assert (tmp_path / "merkle_root.bin").read_bytes() == root
+    nodes = (tmp_path / "merkle_nodes.bin").read_bytes()
+    assert [[nodes[(i * log_n + d) * 32:(i * log_n + d + 1) * 32] for d in range(log_n)]
+            for i in range(len(idx))] == paths
+    assert (tmp_path / "merkle_leaves.bin").read_bytes() == b"".join(evals[i].tobytes() for i in idx)
+    want = json.load(open(os.path.join(HERE, "golden", "r1cs_proofs.json")))[name]["json_sha256"]
+    for f in ("proof.json", "proof_circuit.json"):
+        assert hashlib.sha256((tmp_path / f).read_bytes()).hexdigest() == want, f
