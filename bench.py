@@ -405,6 +405,30 @@ CPU_PROVE_2_20 = os.path.join(ROOT, "profiles", "r04_cpu_prove_synth_2_20.json")
 XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (MI355X: 7 links per GPU, task brief)
 
 
+def group_extras(world: int, rank: int, on_gloo: bool) -> dict:
+    """The C ABI's multi-GPU path (stark_group_*: one process drives the N GPUs through peer copies,
+    include/stark_hip.h) timed on the same node: rank 0 runs tools/group_bench.py over devices 0..N-1 as a
+    child process while the other ranks wait on a CPU (gloo) barrier with their GPUs idle.  A failure or a
+    time-out is reported in the line; the headline is unaffected."""
+    if on_gloo:  # the one-GPU rehearsal: its ranks share one device, there is no N-device group to time
+        return {}
+    cpu_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=400))
+    out = {}
+    if rank == 0:
+        devs = ",".join(str(i) for i in range(world))
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "group_bench.py"), "--devices", devs],
+                               capture_output=True, text=True, timeout=240)
+            if r.returncode == 0 and r.stdout.strip():
+                out = {"group": json.loads(r.stdout.strip().splitlines()[-1])}
+            else:
+                out = {"group_error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            out = {"group_error": repr(e)[:300]}
+    dist.barrier(group=cpu_group)
+    return out
+
+
 def distributed_phases(buf, log_total, w_total, ops, stream, on_gloo, local, reps=5) -> dict:
     """Median device time of each phase of one distributed step (the timed loop's transform, run
     unpipelined with HIP events on the step's stream between the phases), max over ranks: the local
@@ -829,6 +853,7 @@ def main():
             extras.update(distributed_prove(ctx, world, rank, on_gloo, local))
         except Exception as e:  # symmetric failures still print the headline line
             extras["distributed_prove_error"] = repr(e)[:300]
+        extras.update(group_extras(world, rank, on_gloo))
 
     # Roofline of the dominant kernel, ntt_pass_kernel: one 2^log_n transform is len(plan)
     # launches; achieved = SURVEY 8(d)'s algorithmic 64 B per element per transform (read 32 +
@@ -1014,13 +1039,19 @@ def main():
             # tools/cpu_prove_baseline.py on the GPU box and committed; reported here with its source.
             try:
                 rec = json.load(open(CPU_PROVE_2_20))
+                rec["timed_in_this_run"] = False
+                rec["provenance"] = (f"committed round-4 record ({os.path.relpath(CPU_PROVE_2_20, ROOT)}), "
+                                     "not timed in this run")
                 legs["prove_synth_2^20_steps"] = rec
             except (OSError, ValueError):
                 pass
             extras["cpu_baselines"] = legs
 
     if rank == 0:
-        line = {"metric": "2^24-pt NTT field-elems/sec", "value": value, "unit": "field-elems/s",
+        # N > 1: the metric names the workload the GPUs share (one 2^(24 + log2 N)-point transform)
+        metric = "2^24-pt NTT field-elems/sec" if world == 1 else \
+            f"2^{log_total}-pt distributed NTT field-elems/sec (2^{log_n} per GPU)"
+        line = {"metric": metric, "value": value, "unit": "field-elems/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "clock_settle_steps": settle, "ms_per_step": ms_per_step,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32x8 (BN254 Fr)",
                 "data": "synthetic (splitmix64 uniform in [0,p), BASELINE.md)",

@@ -252,22 +252,42 @@ stark_status stark_cyclic_ntt_local_dev(stark_ctx* ctx, uint64_t* d_data, uint32
     const uint64_t M = (uint64_t)1 << log_m;
     void* p = nullptr;
     const bool cached = cache_reserve(ctx, M * sizeof(fe), false);
+    if (!cached) {
+      // Larger than the cache cap: this call's own table, allocated and freed in the stream's order (no
+      // host synchronisation: the call stays asynchronous on s).
+      STARK_HIP(ctx, hipMallocAsync(&p, M * sizeof(fe), s));
+      hipLaunchKernelGGL(post_tw_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (fe*)p, M,
+                         (uint64_t)rank, log_n, tn->d_lo, tn->d_hi, tn->kb);
+      const hipError_t ke = hipGetLastError();
+      stark_status st = ke == hipSuccess ? STARK_OK : hip_fail(ctx, ke, "post_tw_kernel");
+      if (st == STARK_OK) st = ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, (const fe*)p);
+      const hipError_t fe_ = hipFreeAsync(p, s);
+      if (st == STARK_OK && fe_ != hipSuccess) st = hip_fail(ctx, fe_, "hipFreeAsync");
+      return st;
+    }
     if (hipMalloc(&p, M * sizeof(fe)) != hipSuccess) {
       hipGetLastError();
       return STARK_ERR_OOM;
     }
     hipLaunchKernelGGL(post_tw_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (fe*)p, M, (uint64_t)rank,
                        log_n, tn->d_lo, tn->d_hi, tn->kb);
-    STARK_HIP(ctx, hipGetLastError());
-    if (!cached) {
-      // Larger than the cache cap: this call's own table, freed once the transform has run.
-      const stark_status st = ntt_device(ctx, (fe*)d_data, log_m, 1, *tl, inverse != 0, s, (const fe*)p);
-      hipStreamSynchronize(s);
-      hipFree(p);
-      return st;
+    {
+      const hipError_t e_ = hipGetLastError();
+      if (e_ != hipSuccess) {
+        hipFree(p);
+        return hip_fail(ctx, e_, "post_tw_kernel");
+      }
     }
     CacheBuf cb{p, M * sizeof(fe), 0};
-    STARK_TRY(fill_mark(ctx, cb.ev, cb.fill, s));  // complete once the fill has run on s
+    {
+      const stark_status st = fill_mark(ctx, cb.ev, cb.fill, s);  // complete once the fill has run on s
+      if (st != STARK_OK) {
+        hipStreamSynchronize(s);  // (the fill may still run)
+        hipFree(p);
+        if (cb.ev) hipEventDestroy(cb.ev);
+        return st;
+      }
+    }
     it = ctx->post_tw.emplace(key, cb).first;
   }
   CacheBuf& e = it->second;

@@ -2,7 +2,7 @@
 //
 // a * w mod p for a constant w without a quotient product: the constant is
 // stored as its eight "digit images" W_i = w * 2^(32 i) mod p, each in nine
-// 29-bit limbs, so for a = sum a_i 2^(32 i) (a < 4p)
+// 29-bit limbs, so for a = sum a_i 2^(32 i) (a < 4p + 2^224)
 //   S = sum_i a_i W_i = sum_j acc_j 2^(29 j),   acc_j = sum_i a_i W_i[j]
 // is congruent to a w and every column sum acc_j fits 64 bits with no carry
 // out (8 (2^32 - 1)(2^29 - 1) < 2^64): 72 v_mad_u64_u32, no carry counting.
@@ -44,11 +44,12 @@ __device__ __forceinline__ uint32_t db_n(int j) {
 #define STARK_DB_C7 2.5225401188032808e-06
 #define STARK_DB_MARGIN 2.44140625e-4
 
-// r = a * w mod p in [0, 2p) for a < 4p (the NTT's lazy range), W the constant's digit-basis table.
+// r = a * w mod p in [0, 2p) for a < 4p + 2^224 (the NTT's lazy range: [0, 4p) in the radix-2^8 passes,
+// [0, 4p + 2^224) in the radix-2^6 ones, csrc/ntt.hip), W the constant's digit-basis table.
 //   acc_j = sum_i a_i W_i[j]: 72 v_mad_u64_u32 into nine 64-bit columns;
 //   q: f = acc_8 2^232 / p + hi(acc_7) 2^235 / p - 2^-12 in doubles (the dropped terms are < 2^-15,
 //      the rounding < 2^-15, so floor(f) is floor(S / p) or one less), q = qh 2^29 + ql;
-//   acc_j += ql N_j + qh N_{j-1} (17 mads; a < 4p bounds a_7 < 2^31.6, so every column stays below
+//   acc_j += ql N_j + qh N_{j-1} (17 mads; a < 4p + 2^224 bounds a_7 < 2^31.6 + 1, so every column stays below
 //      7 2^61 + 2^60.6 + 2^58 < 2^64 with the carry added);
 //   one carry pass to 29-bit limbs (mod 2^261) and the repack to 32-bit words.
 __device__ __forceinline__ fe fe_mul_db(const fe& a, const uint32_t* __restrict__ W) {

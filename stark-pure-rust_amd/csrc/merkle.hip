@@ -477,13 +477,18 @@ struct GatherDescs {
 // bytes), then k * depth digests.
 __global__ __launch_bounds__(64) void merkle_gather_multi_kernel(GatherDescs g, uint32_t n_req,
                                                                   const uint64_t* __restrict__ idx,
-                                                                  uint8_t* __restrict__ out) {
+                                                                  uint8_t* __restrict__ out,
+                                                                  uint32_t* __restrict__ err) {
   const uint32_t p = blockIdx.x;
   uint32_t r = 0;
   while (r + 1 < n_req && g.d[r + 1].first <= p) ++r;
   const GatherDesc& q = g.d[r];
   const uint32_t i = p - q.first;
   const uint64_t id = idx[p];
+  if (id >= q.n) {  // an index written on the device (fri_indices_kernel) out of range: no read, flagged
+    if (threadIdx.x == 0) *err = 1u;
+    return;
+  }
   uint8_t* region = out + q.out_off;
   uint8_t* leaf_out = region + (uint64_t)i * q.leaf_len;
   const uint8_t* leaf_in = q.leaves + id * q.leaf_len;
@@ -527,10 +532,12 @@ stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& r
   if (n_idx > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
   const size_t idx_bytes = n_idx * sizeof(uint64_t);
   uint8_t* host = nullptr;
-  stark_status st = ctx_pinned(ctx, 0, idx_bytes + out_bytes, (void**)&host);
+  stark_status st = ctx_pinned(ctx, 0, idx_bytes + out_bytes + 16, (void**)&host);
   if (st != STARK_OK) return st;
   uint64_t* h_idx = (uint64_t*)host;
   uint8_t* h_out = host + idx_bytes;
+  uint32_t* h_err = (uint32_t*)(h_out + out_bytes);  // (out_bytes is a multiple of 16)
+  *h_err = 0;
   for (size_t r = 0; r < reqs.size(); ++r)
     if (reqs[r].idx)
       for (size_t i = 0; i < reqs[r].k; ++i) h_idx[first[r] + i] = reqs[r].idx[i];
@@ -558,13 +565,17 @@ stark_status merkle_gather_batch(stark_ctx* ctx, const std::vector<GatherReq>& r
     }
     if (m) {
       hipLaunchKernelGGL(merkle_gather_multi_kernel, dim3(proofs), dim3(64), 0, stream, g, m,
-                         (const uint64_t*)(h_idx + p0), h_out);
+                         (const uint64_t*)(h_idx + p0), h_out, h_err);
       STARK_HIP(ctx, hipGetLastError());
     }
     p0 += proofs;
     r0 = r;
   }
   STARK_HIP(ctx, hipStreamSynchronize(stream));
+  if (*(volatile uint32_t*)h_err) {
+    ctx->last_error = "gather index out of range (device-written indices)";
+    return STARK_ERR_BAD_ARG;
+  }
   for (size_t r = 0; r < reqs.size(); ++r) {
     const GatherReq& q = reqs[r];
     const uint8_t* leaf = h_out + off[r];

@@ -61,16 +61,22 @@ struct ProofIn {
   std::vector<Branch> main, lcomb;
   std::vector<FriIn> fri;
   // The openings' bytes: the opening whose text starts at offset t is written from arena + t / 2 (a
-  // number takes two characters at least, so openings never overlap).
+  // number takes two characters at least, so an opening's bytes end before its text's end / 2 and
+  // openings side by side never overlap; pre_parse_branches bounds each parallel parse by the next
+  // candidate's start, so a candidate nested inside another opening cannot write into it).
   std::unique_ptr<uint8_t[]> arena;
 };
 
 class Json;
 
 // Merkle openings parsed ahead of the sequential reader, in parallel: every `{"leaf":` of the text
-// starts a Branch object (leaf and node contents are numbers, so the key occurs nowhere else), and
-// serde_json writes no whitespace.  The reader takes a pre-parsed Branch only when it reaches that
-// exact offset itself, so the result is the sequential parse.
+// starts a candidate Branch object (in serde_json's own output the key occurs nowhere else), and
+// serde_json writes no whitespace.  Candidate i writes its bytes only inside [off_i / 2, off_{i+1} / 2) of
+// the arena, which a Branch that contains no other candidate always fits; one that does not fit (it has
+// an object with a `{"leaf":` key nested in it, which serde accepts as an unknown member) is left to
+// the reader.  The reader takes a pre-parsed Branch only when it reaches that exact offset itself and the
+// parse succeeded, and parses every other Branch itself after the parallel phase, so the result is the
+// sequential parse and no two threads write the same bytes.
 struct PreBranches {
   std::vector<size_t> off, end;
   std::vector<Branch> br;
@@ -83,10 +89,10 @@ class Json {
   static constexpr int kBranchDepth = 6;  // a Proof object's nesting in a StarkProof (at most; FRI branches)
 
  public:
-  Json(const char* s, size_t n, PreBranches* pre = nullptr, uint8_t* arena = nullptr)
-      : p_(s), e_(s + n), base_(s), pre_(pre), arena_(arena) {}
-  Json(const char* base, size_t n, size_t at, uint8_t* arena)
-      : p_(base + at), e_(base + n), base_(base), arena_(arena) {}
+  Json(const char* s, size_t n, PreBranches* pre = nullptr, uint8_t* arena = nullptr, uint8_t* lim = nullptr)
+      : p_(s), e_(s + n), base_(s), pre_(pre), arena_(arena), lim_(lim) {}
+  Json(const char* base, size_t n, size_t at, uint8_t* arena, uint8_t* lim)
+      : p_(base + at), e_(base + n), base_(base), arena_(arena), lim_(lim) {}
   bool ok = true;
   size_t pos() const { return (size_t)(p_ - base_); }
 
@@ -303,7 +309,11 @@ class Json {
       ok = false;
       return;
     }
-    uint8_t* w = arena_ + pos() / 2;  // this opening's part of the arena (ProofIn::arena)
+    uint8_t* w = arena_ + pos() / 2;  // this opening's part of the arena (ProofIn::arena), up to lim_
+    if (w > lim_) {
+      ok = false;
+      return;
+    }
     expect('{');
     bool has_leaf = false, has_nodes = false;
     do {
@@ -311,7 +321,7 @@ class Json {
       if ((k == "leaf" && has_leaf) || (k == "nodes" && has_nodes)) {
         ok = false;  // serde_json: duplicate field
       } else if (k == "leaf") {
-        const size_t n = bytes_to(w, (size_t)(e_ - p_) / 2 + 1);
+        const size_t n = bytes_to(w, std::min((size_t)(e_ - p_) / 2 + 1, (size_t)(lim_ - w)));
         b.leaf = Bytes{w, n};
         w += n;
         has_leaf = true;
@@ -320,6 +330,10 @@ class Json {
         expect('[');
         if (!accept(']')) {
           do {
+            if (lim_ - w < 32) {
+              ok = false;
+              break;
+            }
             digest(w);
             w += 32;
           } while (ok && accept(','));
@@ -467,10 +481,7 @@ class Json {
     while (P.next < P.off.size() && P.off[P.next] < at) ++P.next;
     if (P.next == P.off.size() || P.off[P.next] != at) return false;
     const size_t i = P.next++;
-    if (!P.good[i]) {
-      ok = false;
-      return true;
-    }
+    if (!P.good[i]) return false;  // (parsed here instead: the sequential parse decides)
     b = std::move(P.br[i]);
     p_ = base_ + P.end[i];
     return true;
@@ -480,10 +491,11 @@ class Json {
   const char* base_;
   PreBranches* pre_ = nullptr;
   uint8_t* arena_ = nullptr;
+  uint8_t* lim_ = nullptr;  // arena_'s write bound for this parse
 };
 
 // Finds every Branch start and parses each from its offset on the host workers.
-void pre_parse_branches(const char* s, size_t n, PreBranches& P, uint8_t* arena) {
+void pre_parse_branches(const char* s, size_t n, PreBranches& P, uint8_t* arena, uint8_t* arena_end) {
   static const char kKey[] = "{\"leaf\":";
   const size_t klen = sizeof(kKey) - 1;
   const unsigned parts = n < ((size_t)1 << 18) ? 1u : host_threads();
@@ -510,7 +522,7 @@ void pre_parse_branches(const char* s, size_t n, PreBranches& P, uint8_t* arena)
   host_parallel(std::min<unsigned>(host_threads(), (unsigned)((k + 15) / 16)), [&](unsigned) {
     for (size_t c; (c = next.fetch_add(16)) < k;)
       for (size_t i = c; i < std::min(k, c + 16); ++i) {
-        Json j(s, n, P.off[i], arena);
+        Json j(s, n, P.off[i], arena, i + 1 < k ? arena + P.off[i + 1] / 2 : arena_end);
         j.branch(P.br[i]);
         P.good[i] = j.ok;
         P.end[i] = j.pos();
@@ -954,9 +966,10 @@ static bool read_proof(const char* proof_json, size_t json_len, ProofIn& pr) {
   PhaseClock clk("verify: read proof");
   PreBranches pre;
   pr.arena.reset(new uint8_t[json_len / 2 + 64]);
-  pre_parse_branches(proof_json, json_len, pre, pr.arena.get());
+  uint8_t* const arena_end = pr.arena.get() + json_len / 2 + 64;
+  pre_parse_branches(proof_json, json_len, pre, pr.arena.get(), arena_end);
   clk.mark("openings parsed (parallel)");
-  Json j(proof_json, json_len, &pre, pr.arena.get());
+  Json j(proof_json, json_len, &pre, pr.arena.get(), arena_end);
   j.stark_proof(pr);
   clk.mark("StarkProof JSON parsed");
   return j.ok;

@@ -19,6 +19,7 @@ orchestration is tested on CPU with gloo (tests/test_distributed_cpu.py).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -212,17 +213,32 @@ class GpuOps:
     def transpose(self, src: torch.Tensor, dst: torch.Tensor, rows: int, cols: int) -> None:
         self.ctx.transpose_dev(src.data_ptr(), dst.data_ptr(), rows, cols, 1, stream=self._stream())
 
-    def merkle_commit(self, shard: torch.Tensor, m: int, leaf_len: int) -> bytes:
-        """Subtree over this rank's m leaves (device tensor of m * leaf_len bytes)."""
+    def merkle_commit(self, shard: torch.Tensor, m: int, leaf_len: int) -> torch.Tensor:
+        """Subtree over this rank's m leaves (device tensor of m * leaf_len bytes); its root as a (32,)
+        device tensor, copied on the stream (no host round trip)."""
         from . import MerkleProofInPlace
         self._tree = MerkleProofInPlace(self.ctx)
         self._tree.update_dev(shard.data_ptr(), m, leaf_len, stream=self._stream())
-        torch.cuda.current_stream().synchronize()
-        self._tree.gen_proofs([])  # sets the root (MerkleProofInPlace::get_root semantics)
-        return self._tree.get_root()
+        out = torch.empty(32, dtype=torch.uint8, device=shard.device)
+        self.ctx.check(self.ctx.lib.stark_merkle_root_dev(self._tree.h, out.data_ptr(), self._stream()),
+                       "merkle_root_dev")
+        return out
 
-    def merkle_open(self, local_indices) -> list:
-        return [(p.leaf, p.nodes) for p in self._tree.gen_proofs(local_indices)]
+    def merkle_top(self, roots: torch.Tensor, G: int) -> torch.Tensor:
+        """The G - 1 digests above G subtree roots (device), the root last (stark_merkle_top_dev)."""
+        out = torch.empty(max(G - 1, 1) * 32, dtype=torch.uint8, device=roots.device)
+        if G > 1:
+            self.ctx.check(self.ctx.lib.stark_merkle_top_dev(self.ctx.h, roots.data_ptr(), G, out.data_ptr(),
+                                                             self._stream()), "merkle_top")
+        return out[:(G - 1) * 32]
+
+    def merkle_open(self, local_indices) -> tuple:
+        """(leaves k x leaf_len, nodes k x depth x 32) byte arrays of the local subtree."""
+        ps = self._tree.gen_proofs(local_indices)
+        depth = max(self._tree.width().bit_length() - 1, 0)
+        leaves = np.frombuffer(b"".join(p.leaf for p in ps), dtype=np.uint8).reshape(len(ps), -1)
+        nodes = np.frombuffer(b"".join(b"".join(p.nodes) for p in ps), dtype=np.uint8).reshape(len(ps), depth, 32)
+        return leaves, nodes
 
     def twiddle2d(self, t: torch.Tensor, rows: int, cols: int, row_base: int, col_base: int, root: int,
                   log_order: int) -> None:
@@ -234,16 +250,16 @@ class DistributedMerkle:
     """Blake2s Merkle commitment of n = G * m leaves sharded in rank order
     (rank r holds leaves [r m, (r+1) m)), one GPU per rank.
 
-    commit(): every rank builds its subtree on its GPU (`ops.merkle_commit`);
-    the G subtree roots are all-gathered (RCCL with backend "nccl") and the
-    top log2(G) levels are hashed on the host.  The root is the single-tree
-    root: the reference itself builds 2^k subtrees and a top tree over their
-    roots (gen_multi_proofs_multi_core, merkle_proof_in_place.rs:106-206).
+    commit(): every rank builds its subtree on its GPU (`ops.merkle_commit`, root left in HBM); the G
+    subtree roots are all-gathered as one (G, 32) tensor (RCCL with backend "nccl", device memory) and
+    the top log2(G) levels are hashed on the device (`ops.merkle_top`); one download brings the levels
+    to the host.  The root is the single-tree root: the reference itself builds 2^k subtrees and a top
+    tree over their roots (gen_multi_proofs_multi_core, merkle_proof_in_place.rs:106-206).
 
-    gen_proofs(indices): each rank opens the indices inside its shard (leaf +
-    subtree siblings) and appends the top-tree siblings; the proofs are
-    all-gathered so every rank returns them in the caller's order, duplicates
-    kept (merkle_proof_in_place.rs:191-205).
+    gen_proofs(indices): each rank opens the indices inside its shard (leaf + subtree siblings); one
+    padded tensor all-gather brings every rank's openings to every rank (the byte count of each rank's
+    part follows from the indices, known everywhere), which appends the top-tree siblings and returns
+    them in the caller's order, duplicates kept (merkle_proof_in_place.rs:191-205).
     """
 
     def __init__(self, ops, group=None):
@@ -253,23 +269,38 @@ class DistributedMerkle:
         self.r = dist.get_rank(group)
         self.levels = []      # top tree: levels[0] = subtree roots, ..., levels[-1] = [root]
         self.m = 0
+        self.leaf_len = 0
 
-    def _all_gather_bytes(self, b: bytes) -> list:
-        out = [None] * self.G
-        dist.all_gather_object(out, b, group=self.group)
-        return out
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """(G, *t.shape) concatenation of every rank's t (host tensors under gloo)."""
+        host = dist.get_backend(self.group) == "gloo" and t.is_cuda
+        src = t.cpu() if host else t
+        parts = [torch.empty_like(src) for _ in range(self.G)]
+        dist.all_gather(parts, src, group=self.group)
+        return torch.stack(parts).to(t.device)
 
     def commit(self, shard, m: int, leaf_len: int) -> bytes:
         if m == 0 or m & (m - 1) or self.G & (self.G - 1):
             raise ValueError("DistributedMerkle: power-of-two shard size and world size required")
-        self.m = m
+        self.m, self.leaf_len = m, leaf_len
         local = self.ops.merkle_commit(shard, m, leaf_len)
-        from . import blake
-        roots = self._all_gather_bytes(local)
-        self.levels = [roots]
-        while len(self.levels[-1]) > 1:
-            lv = self.levels[-1]
-            self.levels.append([blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)])
+        if isinstance(local, (bytes, bytearray)):        # host-side ops (the CPU tests' oracle ops)
+            local = torch.frombuffer(bytearray(local), dtype=torch.uint8)
+        roots = self._all_gather(local).reshape(-1)     # (G * 32,)
+        if hasattr(self.ops, "merkle_top"):
+            levels = torch.cat([roots, self.ops.merkle_top(roots, self.G)]).cpu().numpy().tobytes()
+        else:
+            from . import blake
+            lv = [roots.cpu().numpy().tobytes()[32 * i:32 * (i + 1)] for i in range(self.G)]
+            levels = b"".join(lv)
+            while len(lv) > 1:
+                lv = [blake(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)]
+                levels += b"".join(lv)
+        self.levels, at, w = [], 0, self.G
+        while w >= 1:
+            self.levels.append([levels[at + 32 * i:at + 32 * (i + 1)] for i in range(w)])
+            at += 32 * w
+            w //= 2
         return self.levels[-1][0]
 
     def root(self) -> bytes:
@@ -277,19 +308,34 @@ class DistributedMerkle:
 
     def gen_proofs(self, indices) -> list:
         from . import Proof
-        idx = list(indices)
-        mine = [(k, i - self.r * self.m) for k, i in enumerate(idx) if i // self.m == self.r]
-        local = self.ops.merkle_open([li for _, li in mine]) if mine else []
-        part = [(k, leaf, nodes) for (k, _), (leaf, nodes) in zip(mine, local)]
-        parts = [None] * self.G
-        dist.all_gather_object(parts, part, group=self.group)
+        idx = np.asarray(list(indices), dtype=np.int64)
+        m, G, ll = self.m, self.G, self.leaf_len
+        depth = m.bit_length() - 1
+        owner = idx // m
+        mine = np.nonzero(owner == self.r)[0]
+        per = ll + depth * 32
+        counts = [int(np.count_nonzero(owner == p)) for p in range(G)]
+        width = max(max(counts), 1) * per
+        blob = np.zeros(width, dtype=np.uint8)
+        if len(mine):
+            leaves, nodes = self.ops.merkle_open([int(i) - self.r * m for i in idx[mine]])
+            part = np.concatenate([np.asarray(leaves, dtype=np.uint8).reshape(len(mine), ll),
+                                   np.asarray(nodes, dtype=np.uint8).reshape(len(mine), depth * 32)], axis=1)
+            blob[:part.size] = part.reshape(-1)
+        t = torch.from_numpy(blob)
+        if dist.get_backend(self.group) == "nccl":
+            t = t.to(torch.device("cuda", torch.cuda.current_device()))
+        allb = self._all_gather(t).cpu().numpy()      # (G, width)
         out = [None] * len(idx)
-        for p in parts:
-            for k, leaf, nodes in p:
-                pos = idx[k] // self.m
-                top = []
-                for lv in self.levels[:-1]:   # siblings of the subtree root up to the top
-                    top.append(lv[pos ^ 1])
-                    pos >>= 1
-                out[k] = Proof(leaf, list(nodes) + top)
+        at = [0] * G
+        for k, i in enumerate(idx):
+            p = int(owner[k])
+            row = allb[p, at[p] * per:(at[p] + 1) * per].tobytes()
+            at[p] += 1
+            pos = p
+            top = []
+            for lv in self.levels[:-1]:   # siblings of the subtree root up to the top
+                top.append(lv[pos ^ 1])
+                pos >>= 1
+            out[k] = Proof(row[:ll], [row[ll + 32 * d:ll + 32 * (d + 1)] for d in range(depth)] + top)
         return out

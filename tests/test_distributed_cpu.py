@@ -51,8 +51,11 @@ class OracleOps:
         return root
 
     def merkle_open(self, local_indices):
+        """(leaves k x leaf_len, nodes k x depth x 32) of the local subtree."""
         _, paths = self.o.merkle(self._leaves, self._m, self._ll, list(local_indices))
-        return [(self._leaves[i * self._ll:(i + 1) * self._ll], paths[k]) for k, i in enumerate(local_indices)]
+        leaves = b"".join(self._leaves[i * self._ll:(i + 1) * self._ll] for i in local_indices)
+        nodes = b"".join(b"".join(p) for p in paths)
+        return np.frombuffer(leaves, dtype=np.uint8), np.frombuffer(nodes, dtype=np.uint8)
 
     def transpose(self, src, dst, rows, cols):
         s = self._u64(src).reshape(rows, cols, 4)

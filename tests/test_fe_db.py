@@ -1,7 +1,7 @@
 """Digit-basis constant product (csrc/fe_db.h), checked on the CPU.
 
 `tools/db_check.py:db_emulate` restates fe_mul_db step by step with exact integers and IEEE doubles;
-here it is run on random and edge inputs in the NTT's lazy range [0, 4p), on inputs whose quotient
+here it is run on random and edge inputs in the NTT's lazy range [0, 4p + 2^224), on inputs whose quotient
 estimate sits next to the margin, and the header's constants are checked against their definitions.
 The GPU side is exercised bit-exactly by every NTT parity test (tests/test_gpu_ntt.py,
 tests/test_gpu_large.py) and by tools/microbench/db_rate.hip (65,536 products vs Python).
@@ -51,6 +51,12 @@ def test_random_and_edges():
                 _check(a, w)
     for _ in range(3000):
         _check(rng.randrange(4 * D.P), rng.randrange(D.P))
+    # the radix-2^6 passes' lazy range reaches 4p + 2^224: the top word stays below 2^31.6 + 1
+    top = 4 * D.P + (1 << 224) - 1
+    for w in edges_w:
+        _check(top, w)
+    for _ in range(500):
+        _check(rng.randrange(4 * D.P, top + 1), rng.randrange(D.P))
 
 
 def test_quotient_next_to_margin():

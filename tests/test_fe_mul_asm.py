@@ -125,8 +125,13 @@ def _out(R, base):
 
 def _mont_cases():
     rnd = random.Random(7)
-    cases = [(0, 0), (1, 1), (P - 1, P - 1), (4 * P - 1, P - 1), (4 * P - 1, 1), (2 ** 255, P - 1)]
-    return cases + [(rnd.randrange(4 * P), rnd.randrange(P)) for _ in range(1500)]
+    # [0, 4p + 2^224): the lazy range of the radix-2^6 NTT passes, whose butterflies reduce by 2p only
+    # when the top word exceeds 2p's (csrc/ntt.hip)
+    top = 4 * P + (1 << 224) - 1
+    cases = [(0, 0), (1, 1), (P - 1, P - 1), (4 * P - 1, P - 1), (4 * P - 1, 1), (2 ** 255, P - 1),
+             (top, P - 1), (top, 1), (top, top % P)]
+    return cases + [(rnd.randrange(4 * P), rnd.randrange(P)) for _ in range(1500)] + \
+        [(rnd.randrange(4 * P, top + 1), rnd.randrange(P)) for _ in range(200)]
 
 
 def test_generated_montgomery_product():

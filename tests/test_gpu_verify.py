@@ -273,3 +273,32 @@ def test_json_reader_follows_serde_on_fields(ctx, proofs):
     for t in (dup_top, dup_leaf, bad_escape, lead_zero):
         with pytest.raises(StarkError):
             verify_with_wtns(ctx, r1, wt, t)
+
+
+@pytest.mark.parametrize("name", ["compute", "pedersen_test"])
+def test_json_reader_nested_branch_objects(ctx, proofs, name):
+    """An unknown member whose value is itself Branch-shaped ({"leaf":..,"nodes":..}) inside an opening is
+    skipped by serde_json, so the proof still verifies; the reader's parallel pre-parse starts a parse at
+    the nested key too, and must neither let it overwrite the opening's bytes nor take it for the opening
+    (ADVICE r5).  pedersen's text is large enough for the parallel parse to run on several threads.  The
+    same nesting with the real bytes inside and wrong ones outside is refused."""
+    from stark_amd import StarkError
+    from stark_amd.verify import verify_with_wtns
+    r1, wt, js = proofs[name]
+    p = json.loads(js)
+    mb = p["main_branches"]
+    for i in range(0, len(mb), 7):            # every 7th main opening gets a decoy with other bytes
+        other = mb[(i + 1) % len(mb)]
+        decoy = {"leaf": other["leaf"] + other["leaf"], "nodes": other["nodes"] + other["nodes"]}
+        mb[i] = {"leaf": mb[i]["leaf"], "x": decoy, "nodes": mb[i]["nodes"]}
+    lb = p["linear_comb_branches"]
+    lb[0] = {"x": {"leaf": [9] * 300, "nodes": [[1] * 32] * 40}, "leaf": lb[0]["leaf"], "nodes": lb[0]["nodes"]}
+    text = json.dumps(p, separators=(",", ":"))
+    assert verify_with_wtns(ctx, r1, wt, text)
+    # the real opening inside, a wrong one outside: the outer is what serde reads, so it fails
+    q = json.loads(js)
+    b = q["main_branches"][3]
+    wrong = {"leaf": [(v + 1) % 256 for v in b["leaf"]], "nodes": b["nodes"]}
+    q["main_branches"][3] = {"leaf": wrong["leaf"], "x": b, "nodes": wrong["nodes"]}
+    with pytest.raises((StarkError, AssertionError)):
+        verify_with_wtns(ctx, r1, wt, json.dumps(q, separators=(",", ":")))

@@ -43,8 +43,8 @@ def _trunc_u32(x):
 
 
 def db_emulate(a, table):
-    """fe_mul_db (csrc/fe_db.h) step by step; a < 4p."""
-    assert 0 <= a < 4 * P
+    """fe_mul_db (csrc/fe_db.h) step by step; a < 4p + 2^224."""
+    assert 0 <= a < 4 * P + (1 << 224)
     aw = [(a >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
     acc = [sum(aw[i] * table[9 * i + j] for i in range(8)) for j in range(9)]
     d8 = _fma(float(acc[8] >> 32), 2.0 ** 32, float(acc[8] & 0xFFFFFFFF))
