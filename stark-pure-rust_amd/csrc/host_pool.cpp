@@ -2,10 +2,12 @@
 // tests/host_pool builds it alone with a race-window hook (STARK_POOL_TEST) and under ThreadSanitizer.
 #include "host_pool.h"
 
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -28,40 +30,55 @@ class HostWorkers {
     return *w;
   }
   unsigned threads() const { return (unsigned)workers_ + 1; }
-  // Each call is a Job of its own (on the caller's stack): a worker takes a reference to the current
-  // job under the lock and claims items from that job's counter only, and the caller returns once
-  // every item is done AND every worker that joined has let go of the job.  (The previous form kept
-  // one counter for all calls: a worker still leaving call k could claim, run and count an item of
-  // call k + 1 while that call was being set up, so the call could return with an item unfinished.)
+  // One call at a time (call_).  A call is published as a 64-bit ticket (generation << 32 | next item);
+  // an item is claimed by a compare-exchange of the ticket, which fails for a worker still holding a
+  // ticket of an earlier call, so a late worker can neither run nor skip an item of the current call
+  // (the round-4 pool's shared counter let it do both: DESIGN.md 7.1, tests/host_pool).  The call
+  // returns once `done` counts all of its items; nothing of a call is read after its last item ends.
+  // Workers and the caller spin briefly before they sleep: a proof makes its calls in bursts, and a
+  // wake-up through a condition variable costs each worker tens of microseconds.
   void run(unsigned n, const std::function<void(unsigned)>& fn) {
     if (n == 0) return;
     if (n == 1 || workers_ == 0 || in_job()) {  // a job that calls host_parallel runs the inner one serially
       for (unsigned k = 0; k < n; ++k) fn(k);
       return;
     }
-    std::lock_guard<std::mutex> serial(call_);  // one parallel call at a time
-    Job job{&fn, n};
-    {
-      std::lock_guard<std::mutex> g(m_);
-      cur_ = &job;
-      ++gen_;
-    }
-    cv_.notify_all();
+    std::lock_guard<std::mutex> serial(call_);
+    // Seal the previous call's ticket first: a worker that read that call's exhausted ticket and then
+    // this call's n_ (below) could otherwise claim "item n_old" of the old generation, i.e. run an item
+    // of this call under the old ticket, and count it twice (tests/host_pool caught exactly this).
+    ticket_.store((ticket_.load(std::memory_order_relaxed) & ~(uint64_t)0xFFFFFFFFu) | 0xFFFFFFFFu,
+                  std::memory_order_relaxed);
+    fn_.store(&fn, std::memory_order_release);
+    n_.store(n, std::memory_order_release);  // (a worker that sees this n also sees the seal)
+    done_.store(0, std::memory_order_relaxed);
+    const uint64_t gen = ++gen_;
+    ticket_.store(gen << 32, std::memory_order_release);  // (publishes fn_, n_, done_)
+    { std::lock_guard<std::mutex> g(m_); }  // a worker between its check and its sleep is asleep now
+    wake_.notify_all();
     in_job() = true;
-    work(job);
+    work(gen);
     in_job() = false;
-    std::unique_lock<std::mutex> g(m_);
-    cur_ = nullptr;  // no worker joins from here on
-    done_.wait(g, [&] { return job.done == job.n && job.refs == 0; });
+    auto finished = [&] { return done_.load(std::memory_order_acquire) == n; };
+    if (!spin_until(finished)) {
+      std::unique_lock<std::mutex> g(m_);
+      finished_.wait(g, finished);
+    }
   }
 
  private:
-  struct Job {
-    const std::function<void(unsigned)>* fn;
-    unsigned n;
-    std::atomic<unsigned> next{0};
-    unsigned done = 0, refs = 0;  // under m_
-  };
+  static constexpr int kSpinUs = 40;
+  template <class Pred>
+  static bool spin_until(Pred pred) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned i = 0;; ++i) {
+      if (pred()) return true;
+      if ((i & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) return false;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
   HostWorkers() {
     unsigned hw = std::thread::hardware_concurrency();
     hw = hw < 1 ? 1 : (hw > 16 ? 16 : hw);
@@ -72,44 +89,63 @@ class HostWorkers {
     thread_local bool flag = false;
     return flag;
   }
-  void work(Job& job) {
-    unsigned mine = 0;
-    for (;; ++mine) {
-      const unsigned k = job.next.fetch_add(1);
-      STARK_POOL_WINDOW();  // (tests/host_pool: a claim descheduled before its bound check)
-      if (k >= job.n) break;
-      (*job.fn)(k);
-    }
-    if (mine) {
-      std::lock_guard<std::mutex> g(m_);
-      job.done += mine;
-      if (job.done == job.n) done_.notify_all();
+  // Claims and runs items of call `gen` until none is left (or the call is no longer current).
+  void work(uint64_t gen) {
+    uint64_t t = ticket_.load(std::memory_order_acquire);
+    for (;;) {
+      const unsigned n = n_.load(std::memory_order_acquire);  // (validated by the exchange below)
+      if ((t >> 32) != gen || (uint32_t)t >= n) return;
+      if (!ticket_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+      STARK_POOL_WINDOW();  // (tests/host_pool: a claimant descheduled before it runs the item)
+#ifdef STARK_POOL_TEST
+      {
+        const uint64_t now = ticket_.load(std::memory_order_acquire);
+        if ((now >> 32) != gen) {  // the call ended early
+          fprintf(stderr, "pool: claimed (%llu, %u) of n %u, ticket now (%llu, %u), done %u, n_ %u\n",
+                  (unsigned long long)gen, (unsigned)(uint32_t)t, n, (unsigned long long)(now >> 32),
+                  (unsigned)(uint32_t)now, done_.load(), n_.load());
+          __builtin_trap();
+        }
+      }
+#endif
+      (*fn_.load(std::memory_order_acquire))((uint32_t)t);
+      const unsigned prev = done_.fetch_add(1, std::memory_order_acq_rel);
+#ifdef STARK_POOL_TEST
+      if (prev >= n) {
+        fprintf(stderr, "pool: done %u >= n %u after item (%llu, %u); ticket (%llu, %u)\n", prev, n,
+                (unsigned long long)gen, (unsigned)(uint32_t)t, (unsigned long long)(ticket_.load() >> 32),
+                (unsigned)(uint32_t)ticket_.load());
+        __builtin_trap();
+      }
+#endif
+      if (prev + 1 == n) {
+        std::lock_guard<std::mutex> g(m_);
+        finished_.notify_all();
+      }
+      t = ticket_.load(std::memory_order_acquire);
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
-      Job* job;
-      {
+      auto fresh = [&] { return (ticket_.load(std::memory_order_acquire) >> 32) != seen; };
+      if (!spin_until(fresh)) {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return gen_ != seen; });
-        seen = gen_;
-        job = cur_;
-        if (!job) continue;  // that call has already finished
-        ++job->refs;
+        wake_.wait(g, fresh);
       }
+      seen = ticket_.load(std::memory_order_acquire) >> 32;
       in_job() = true;
-      work(*job);
+      work(seen);
       in_job() = false;
-      std::lock_guard<std::mutex> g(m_);
-      if (--job->refs == 0) done_.notify_all();
     }
   }
   size_t workers_ = 0;
   std::mutex call_, m_;
-  std::condition_variable cv_, done_;
-  Job* cur_ = nullptr;
-  uint64_t gen_ = 0;
+  std::condition_variable wake_, finished_;
+  std::atomic<const std::function<void(unsigned)>*> fn_{nullptr};
+  std::atomic<unsigned> n_{0}, done_{0};
+  std::atomic<uint64_t> ticket_{0};
+  uint64_t gen_ = 0;  // under call_
 };
 
 // One side thread for HostTask: one task at a time, tickets in submission order.

@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -27,9 +28,11 @@
 #include "host_pool.h"
 
 static std::atomic<uint64_t> g_seed{12345};
+static bool g_window = true;  // off for the latency diagnostic
 
 // a short random pause in the claim window on about one claim in four
 void stark_pool_test_window() {
+  if (!g_window) return;
   thread_local std::minstd_rand rng((uint32_t)g_seed.fetch_add(7919));
   if (rng() % 4 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 200));
 }
@@ -147,6 +150,8 @@ static void one_call(unsigned n, unsigned spin_us, const char* who, unsigned id)
     for (unsigned i = 0; i < n; ++i)
       if (hits[i].load() != 1) fprintf(stderr, " [%u]=%d", i, hits[i].load());
     fprintf(stderr, "\n");
+    fflush(stderr);
+    std::_Exit(1);  // (a broken pool may also hang or crash from here on: stop at the first violation)
   }
   // (a late item of a returned call may still touch hits/running: give it time before they go)
   if (bad) std::this_thread::sleep_for(std::chrono::milliseconds(50));
@@ -161,9 +166,34 @@ static void caller(unsigned calls, unsigned seed, const char* who) {
   }
 }
 
+// Dispatch latency of the product pool (a diagnostic, not a test): wall time of host_parallel(16, ~2 us
+// items), back to back and after an idle gap that lets the workers fall asleep.
+static int latency() {
+  g_window = false;
+  const unsigned n = std::min(16u, stark::host_threads());
+  for (int gap_us : {0, 300}) {
+    std::vector<double> ts;
+    for (int i = 0; i < 400; ++i) {
+      if (gap_us) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+      const auto t0 = std::chrono::steady_clock::now();
+      stark::host_parallel(n, [](unsigned) {
+        const auto s0 = std::chrono::steady_clock::now();
+        while (std::chrono::steady_clock::now() - s0 < std::chrono::microseconds(2)) {
+        }
+      });
+      ts.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(ts.begin(), ts.end());
+    printf("host_parallel(%u) after %d us idle: median %.1f us, p90 %.1f us, min %.1f us\n", n, gap_us,
+           ts[ts.size() / 2], ts[ts.size() * 9 / 10], ts[0]);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 2 && !strcmp(argv[1], "latency")) return latency();
   if (argc < 2 || (strcmp(argv[1], "product") && strcmp(argv[1], "r4"))) {
-    fprintf(stderr, "usage: pool_check product|r4 [calls]\n");
+    fprintf(stderr, "usage: pool_check product|r4|latency [calls]\n");
     return 2;
   }
   g_r4 = strcmp(argv[1], "r4") == 0;
