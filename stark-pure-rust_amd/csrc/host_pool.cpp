@@ -23,6 +23,22 @@ namespace stark {
 
 namespace {
 
+// Spin-then-block: poll for up to kSpinUs before sleeping on a condition variable.  A proof makes its
+// host_parallel calls and side tasks in bursts, and a wake-up through a condition variable costs each
+// thread tens of microseconds (tests/host_pool/pool_check latency).
+constexpr int kSpinUs = 40;
+template <class Pred>
+bool spin_until(Pred pred) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
+    if (pred()) return true;
+    if ((i & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) return false;
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+}
+
 class HostWorkers {
  public:
   static HostWorkers& get() {
@@ -67,18 +83,6 @@ class HostWorkers {
   }
 
  private:
-  static constexpr int kSpinUs = 40;
-  template <class Pred>
-  static bool spin_until(Pred pred) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned i = 0;; ++i) {
-      if (pred()) return true;
-      if ((i & 63) == 63 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) return false;
-#if defined(__x86_64__)
-      __builtin_ia32_pause();
-#endif
-    }
-  }
   HostWorkers() {
     unsigned hw = std::thread::hardware_concurrency();
     hw = hw < 1 ? 1 : (hw > 16 ? 16 : hw);
@@ -160,10 +164,12 @@ class SideWorker {
     if (task_) return 0;
     task_ = std::move(fn);
     const uint64_t t = ++submitted_;
+    submitted_a_.store(t, std::memory_order_release);
     cv_.notify_all();
     return t;
   }
   void wait(uint64_t ticket) {
+    if (spin_until([&] { return done_a_.load(std::memory_order_acquire) >= ticket; })) return;
     std::unique_lock<std::mutex> g(m_);
     done_cv_.wait(g, [&] { return done_ >= ticket; });
   }
@@ -171,7 +177,8 @@ class SideWorker {
  private:
   SideWorker() { std::thread([this] { loop(); }).detach(); }
   void loop() {
-    for (;;) {
+    for (uint64_t seen = 0;; ++seen) {
+      spin_until([&] { return submitted_a_.load(std::memory_order_acquire) > seen; });
       std::function<void()> fn;
       {
         std::unique_lock<std::mutex> g(m_);
@@ -182,12 +189,14 @@ class SideWorker {
       std::lock_guard<std::mutex> g(m_);
       task_ = nullptr;
       ++done_;
+      done_a_.store(done_, std::memory_order_release);
       done_cv_.notify_all();
     }
   }
   std::mutex m_;
   std::condition_variable cv_, done_cv_;
   std::function<void()> task_;
+  std::atomic<uint64_t> submitted_a_{0}, done_a_{0};
   uint64_t submitted_ = 0, done_ = 0;
 };
 
