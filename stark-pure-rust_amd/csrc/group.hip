@@ -924,12 +924,28 @@ stark_status stark_group_prove_r1cs_bytes(stark_group* g, const uint8_t* r1cs, s
   g->last_error.clear();
   if (g->m.size() == 1) return gfail(g, 0, stark_prove_r1cs_bytes(g->m[0], r1cs, r1cs_len, wtns, wtns_len, out));
   const uint32_t G = (uint32_t)g->m.size();
-  return group_prove(
+  // The host stage of the trace build (headers, record walk, uploads) runs once, on member 0; the others
+  // copy its raw bytes and walk tables device to device and build their own traces from them
+  // (r1cs_trace_device's producer / consumer modes), instead of G walks queued on the one host pool.
+  TraceShare share;
+  const stark_status st = group_prove(
       g,
       [&](size_t r, stark_dprove** h) {
-        return stark_dprove_begin_bytes(g->m[r], G, (uint32_t)r, r1cs, r1cs_len, wtns, wtns_len, nullptr, h);
+        stark_ctx* c = g->m[r];
+        if (hipSetDevice(c->device) != hipSuccess) {
+          if (r == 0) {  // (the consumers wait for member 0's publication)
+            share.status = STARK_ERR_HIP;
+            share.ready_p.set_value();
+          }
+          return STARK_ERR_HIP;
+        }
+        DevTrace dt;
+        STARK_TRY(r1cs_trace_device(c, r1cs, r1cs_len, wtns, wtns_len, &dt, false, &share, r == 0));
+        return dprove_begin_trace(c, G, (uint32_t)r, dt, nullptr, h);
       },
       out);
+  if (share.ev) hipEventDestroy(share.ev);
+  return st;
 }
 
 stark_status stark_group_circuit_new(stark_group* g, const uint8_t* r1cs, size_t r1cs_len,

@@ -8,6 +8,7 @@
 #include <chrono>
 
 #include <functional>
+#include <future>
 #include <map>
 #include <memory>
 #include <string>
@@ -373,10 +374,35 @@ struct DevTrace {
   std::vector<size_t> public_first_indices;  // (wire, slot) pairs
   const uint32_t* d_err = nullptr;           // defer_err: the device's wire-id flag, not yet read
 };
+// A device trace build whose host part (headers, public wires, record walk, the upload of the raw bytes)
+// runs once for several contexts: the producer (a group's member 0) does it all and publishes its
+// results and its device copies of the raw bytes and walk tables; each consumer waits for `ready`, copies
+// those from the producer's device (peer copies, stream-ordered behind `ev`) and builds its own columns.
+struct TraceShare {
+  R1csHeader hd{};
+  WtnsHeader wh{};
+  size_t n_public = 0, cons_len = 0, o_raw_w = 0, wbytes = 0, fac_n = 0, base_n = 0;
+  uint64_t a_len = 0;
+  std::vector<uint64_t> public_wires;
+  bool pf_ok = false;
+  std::vector<uint64_t> pf_host;
+  stark_ctx* src = nullptr;             // the producer's context
+  const uint8_t* raw = nullptr;         // its raw bytes (constraint section, then the witness at o_raw_w)
+  const uint32_t *fac = nullptr, *base = nullptr;  // its walk tables (device)
+  hipEvent_t ev = nullptr;              // recorded on the producer's stream behind those copies
+  stark_status status = STARK_OK;       // the producer's host stage (consumers stop on an error)
+  std::promise<void> ready_p;           // set once the fields above are final
+  std::shared_future<void> ready = ready_p.get_future().share();
+};
 // defer_err: no read-back when the host finds the public wires' first uses itself; the caller then
 // reads d_err (non-zero: a wire id >= n_wires, STARK_ERR_BAD_ARG) at its own first synchronisation.
+// share: null (a build of its own), or the group's shared host stage; producer: this call runs it.
 stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
-                               size_t wtns_len, DevTrace* out, bool defer_err = false);
+                               size_t wtns_len, DevTrace* out, bool defer_err = false, TraceShare* share = nullptr,
+                               bool producer = false);
+// mk_r1cs_proof for rank `rank` of `world` on a device trace (r1cs.hip; stark_dprove_begin_bytes' second half).
+stark_status dprove_begin_trace(stark_ctx* ctx, uint32_t world, uint32_t rank, const DevTrace& dt, void* stream,
+                                stark_dprove** out);
 // mk_r1cs_proof on trace columns given as host or device pointers, flags as
 // bytes (r1cs.hip).
 // The witness-independent columns of a circuit: the LDEs of K F0 F1 F2 IDX PIDX and the

@@ -2101,13 +2101,24 @@ stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t r
   DevTrace dt;
   stark_status st = r1cs_trace_device(ctx, r1cs, r1cs_len, wtns, wtns_len, &dt);
   if (st != STARK_OK) return st;
+  return dprove_begin_trace(ctx, world, rank, dt, stream, out);
+}
+
+}  // extern "C"
+
+stark_status stark::dprove_begin_trace(stark_ctx* ctx, uint32_t world, uint32_t rank, const DevTrace& dt, void* stream,
+                                       stark_dprove** out) {
+  if (!ctx || !out) return STARK_ERR_BAD_ARG;
+  *out = nullptr;
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
   STARK_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the trace builder runs on the context stream
   auto h = std::make_unique<stark_dprove>();
   hipStream_t s = pick_stream(ctx, stream);
-  st = dprove_begin(ctx, world, rank, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
-                    dt.public_wires.data(), dt.public_wires.size() / 4, dt.public_first_indices.data(),
-                    dt.public_first_indices.size() / 2, (const size_t*)dt.perm, (const uint64_t*)dt.coef, nullptr,
-                    nullptr, nullptr, dt.flags, dt.n_constraints, dt.n_wires, s, h.get());
+  const stark_status st = dprove_begin(ctx, world, rank, (const uint64_t*)dt.wit, (const uint64_t*)dt.comp, dt.os,
+                                       dt.public_wires.data(), dt.public_wires.size() / 4,
+                                       dt.public_first_indices.data(), dt.public_first_indices.size() / 2,
+                                       (const size_t*)dt.perm, (const uint64_t*)dt.coef, nullptr, nullptr, nullptr,
+                                       dt.flags, dt.n_constraints, dt.n_wires, s, h.get());
   if (st != STARK_OK) {
     hipStreamSynchronize(s);
     return st;
@@ -2115,6 +2126,8 @@ stark_status stark_dprove_begin_bytes(stark_ctx* ctx, uint32_t world, uint32_t r
   *out = h.release();
   return STARK_OK;
 }
+
+extern "C" {
 
 stark_status stark_dprove_info(stark_dprove* h, size_t* precision, size_t* n_local, size_t* original_steps,
                                uint64_t g2[4], uint8_t a_root[32]) {

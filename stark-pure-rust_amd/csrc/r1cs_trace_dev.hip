@@ -394,66 +394,128 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
   return STARK_OK;
 }
 
+// The producer's half of a shared build (TraceShare): publishes what the consumers read, and releases them
+// (also on an error, with its status).
+struct ShareGuard {
+  TraceShare* sh;
+  bool done = false;
+  void publish(stark_status st) {
+    if (!sh || done) return;
+    sh->status = st;
+    done = true;
+    sh->ready_p.set_value();
+  }
+  ~ShareGuard() { publish(STARK_ERR_STATE); }
+};
+
+static stark_status peer_copy(stark_ctx* dst_ctx, void* dst, const stark_ctx* src_ctx, const void* src, size_t bytes,
+                              hipStream_t s) {
+  if (!bytes) return STARK_OK;
+  if (dst_ctx->device == src_ctx->device) {
+    STARK_HIP(dst_ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+  } else {
+    STARK_HIP(dst_ctx, hipMemcpyPeerAsync(dst, dst_ctx->device, src, src_ctx->device, bytes, s));
+  }
+  return STARK_OK;
+}
+
 stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, const uint8_t* wtns,
-                               size_t wtns_len, DevTrace* out, bool defer_err) {
+                               size_t wtns_len, DevTrace* out, bool defer_err, TraceShare* share, bool producer) {
   PhaseClock clk("r1cs trace build (device)");
   const FieldHost& F = FieldHost::get();
+  ShareGuard guard{producer ? share : nullptr};
+  const bool consumer = share && !producer;
   R1csHeader hd;
-  stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
-  if (st != STARK_OK) return st;
   WtnsHeader wh;
-  st = parse_wtns_header(wtns, wtns_len, &wh);
-  if (st != STARK_OK) return st;
-  const uint32_t n_c = hd.n_constraints, n_wires = hd.n_wires, n_wit = wh.n_wit;
-  const size_t n_public = 1 + (size_t)hd.n_pub_in + hd.n_pub_out;  // run.rs:359-360
-  if (n_wit < n_wires || n_public > n_wit) return STARK_ERR_BAD_ARG;
-  // witness[0] must be 1 (run.rs:358); the public wires are the first n_public values.
-  const uint8_t* wv = wtns + wh.values_off;
-  {
-    const HostFp w0 = F.reduce_bytes_le(wv, wh.field_size);
-    if (!(w0.v[0] == 1 && w0.v[1] == 0 && w0.v[2] == 0 && w0.v[3] == 0)) return STARK_ERR_BAD_ARG;
-  }
-  out->public_wires.resize(4 * n_public);
-  for (size_t i = 0; i < n_public; ++i) {
-    const HostFp v = F.reduce_bytes_le(wv + i * wh.field_size, wh.field_size);
-    memcpy(&out->public_wires[4 * i], v.v, 32);
-  }
-
-  // Host walk: record counts only (the records themselves are read on the GPU).  It runs on a host
-  // worker while this thread uploads the raw constraint section and witness (pageable memory: the
-  // copies block), and it writes straight into pinned memory, so its tables go up asynchronously.
-  const uint8_t* cons = r1cs + hd.cons_off;
-  const size_t cons_len = r1cs_len - hd.cons_off;
-  const size_t wbytes = (size_t)n_wit * wh.field_size;
-  const size_t fac_n = (size_t)6 * n_c + 1, base_n = (size_t)n_c + 1;
-  uint32_t* walk = nullptr;
-  st = ctx_pinned(ctx, 2, (fac_n + base_n) * 4, (void**)&walk);
-  if (st != STARK_OK) return st;
-  uint32_t* fac = walk;
-  uint32_t* base = walk + fac_n;
-  const size_t o_raw_w = (cons_len + 255) & ~(size_t)255;
-  st = ensure_buf(ctx, ctx->trace_raw, o_raw_w + wbytes);
-  if (st != STARK_OK) return st;
-  uint8_t* RAW = (uint8_t*)ctx->trace_raw.ptr;
+  size_t n_public, cons_len, wbytes, fac_n, base_n, o_raw_w;
+  uint64_t a_len;
+  stark_status st;
+  uint8_t* RAW;
   hipStream_t s = ctx->stream;
-  stark_status walk_st = STARK_OK;
-  const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
-  // defer_err: the public wires' first uses are also read on the host beside the uploads (a bounded scan
-  // that usually ends in the first constraints), so the build needs no read-back and the caller checks
-  // the device's wire-id flag at its own first synchronisation (d_err).
   std::vector<uint64_t> pf_host;
   bool pf_ok = false;
-  st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers, [&] {
-    walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
-    if (walk_st == STARK_OK && defer_err && n_wires > 0)
-      pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
-  });
-  if (st != STARK_OK) return st;
-  if (walk_st != STARK_OK) return walk_st;
-  const uint64_t a_len = base[n_c];
+  const uint32_t* fac_src = nullptr;   // the walk tables to upload (host pinned) or copy (a producer's device)
+  const uint32_t* base_src = nullptr;
+  if (consumer) {
+    // The producer's host stage: headers, public wires and walk, raw bytes already on its device.
+    share->ready.wait();
+    if (share->status != STARK_OK) return share->status;
+    hd = share->hd;
+    wh = share->wh;
+    n_public = share->n_public;
+    cons_len = share->cons_len;
+    wbytes = share->wbytes;
+    fac_n = share->fac_n;
+    base_n = share->base_n;
+    o_raw_w = share->o_raw_w;
+    a_len = share->a_len;
+    out->public_wires = share->public_wires;
+    pf_ok = share->pf_ok;
+    pf_host = share->pf_host;
+    st = ensure_buf(ctx, ctx->trace_raw, o_raw_w + wbytes);
+    if (st != STARK_OK) return st;
+    RAW = (uint8_t*)ctx->trace_raw.ptr;
+    STARK_HIP(ctx, hipStreamWaitEvent(s, share->ev, 0));
+    STARK_TRY(peer_copy(ctx, RAW, share->src, share->raw, o_raw_w + wbytes, s));
+    clk.mark("raw bytes from the producer (peer copy)");
+  } else {
+    st = parse_r1cs_header(r1cs, r1cs_len, &hd);
+    if (st != STARK_OK) return st;
+    st = parse_wtns_header(wtns, wtns_len, &wh);
+    if (st != STARK_OK) return st;
+  }
+  const uint32_t n_c = hd.n_constraints, n_wires = hd.n_wires, n_wit = wh.n_wit;
+  if (!consumer) {
+    n_public = 1 + (size_t)hd.n_pub_in + hd.n_pub_out;  // run.rs:359-360
+    if (n_wit < n_wires || n_public > n_wit) return STARK_ERR_BAD_ARG;
+    // witness[0] must be 1 (run.rs:358); the public wires are the first n_public values.
+    const uint8_t* wv = wtns + wh.values_off;
+    {
+      const HostFp w0 = F.reduce_bytes_le(wv, wh.field_size);
+      if (!(w0.v[0] == 1 && w0.v[1] == 0 && w0.v[2] == 0 && w0.v[3] == 0)) return STARK_ERR_BAD_ARG;
+    }
+    out->public_wires.resize(4 * n_public);
+    for (size_t i = 0; i < n_public; ++i) {
+      const HostFp v = F.reduce_bytes_le(wv + i * wh.field_size, wh.field_size);
+      memcpy(&out->public_wires[4 * i], v.v, 32);
+    }
+
+    // Host walk: record counts only (the records themselves are read on the GPU).  It runs on a host
+    // worker while this thread uploads the raw constraint section and witness (pageable memory: the
+    // copies block), and it writes straight into pinned memory, so its tables go up asynchronously.
+    const uint8_t* cons = r1cs + hd.cons_off;
+    cons_len = r1cs_len - hd.cons_off;
+    wbytes = (size_t)n_wit * wh.field_size;
+    fac_n = (size_t)6 * n_c + 1;
+    base_n = (size_t)n_c + 1;
+    uint32_t* walk = nullptr;
+    st = ctx_pinned(ctx, 2, (fac_n + base_n) * 4, (void**)&walk);
+    if (st != STARK_OK) return st;
+    uint32_t* fac = walk;
+    uint32_t* base = walk + fac_n;
+    fac_src = fac;
+    base_src = base;
+    o_raw_w = (cons_len + 255) & ~(size_t)255;
+    st = ensure_buf(ctx, ctx->trace_raw, o_raw_w + wbytes);
+    if (st != STARK_OK) return st;
+    RAW = (uint8_t*)ctx->trace_raw.ptr;
+    stark_status walk_st = STARK_OK;
+    const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
+    // defer_err: the public wires' first uses are also read on the host beside the uploads (a bounded scan
+    // that usually ends in the first constraints), so the build needs no read-back and the caller checks
+    // the device's wire-id flag at its own first synchronisation (d_err).
+    st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers, [&] {
+      walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
+      if (walk_st == STARK_OK && defer_err && n_wires > 0)
+        pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
+    });
+    if (st != STARK_OK) return st;
+    if (walk_st != STARK_OK) return walk_st;
+    a_len = base[n_c];
+    clk.mark("headers + record walk || uploads");
+  }
   const uint64_t os = 3 * a_len;
   if (a_len == 0) return STARK_ERR_BAD_ARG;
-  clk.mark("headers + record walk || uploads");
 
   // Device buffers (context-owned arena).
   uint32_t key_bits = 1;
@@ -477,8 +539,35 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   st = ensure_buf(ctx, ctx->trace_arena, off);
   if (st != STARK_OK) return st;
   uint8_t* A = (uint8_t*)ctx->trace_arena.ptr;
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac, fac_n * 4, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base, base_n * 4, hipMemcpyHostToDevice, s));
+  if (consumer) {
+    STARK_TRY(peer_copy(ctx, A + o_fac, share->src, share->fac, fac_n * 4, s));
+    STARK_TRY(peer_copy(ctx, A + o_base, share->src, share->base, base_n * 4, s));
+  } else {
+    STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac_src, fac_n * 4, hipMemcpyHostToDevice, s));
+    STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base_src, base_n * 4, hipMemcpyHostToDevice, s));
+  }
+  if (producer) {
+    // the consumers copy the raw bytes and walk tables from here, behind this event
+    if (!share->ev) STARK_HIP(ctx, hipEventCreateWithFlags(&share->ev, hipEventDisableTiming));
+    STARK_HIP(ctx, hipEventRecord(share->ev, s));
+    share->hd = hd;
+    share->wh = wh;
+    share->n_public = n_public;
+    share->cons_len = cons_len;
+    share->wbytes = wbytes;
+    share->fac_n = fac_n;
+    share->base_n = base_n;
+    share->o_raw_w = o_raw_w;
+    share->a_len = a_len;
+    share->public_wires = out->public_wires;
+    share->pf_ok = pf_ok;
+    share->pf_host = pf_host;
+    share->src = ctx;
+    share->raw = RAW;
+    share->fac = (const uint32_t*)(A + o_fac);
+    share->base = (const uint32_t*)(A + o_base);
+    guard.publish(STARK_OK);
+  }
   fe* wcan = (fe*)(A + o_wcan);
   fe* wmont = (fe*)(A + o_wmont);
   uint32_t* err = (uint32_t*)(A + o_err);
