@@ -447,9 +447,16 @@ __global__ __launch_bounds__(kPassThreads, (DbPlan<LOG_R, COL>::occupancy)) void
       const uint32_t t = q & ((1u << LT) - 1), a = q >> LT;
       const uint32_t i0 = (((a << (LT + 2)) + t) << log_b) + b, st = (1u << LT) << log_b;
       fe x[4];
+      // (group g = 0's twiddle is w^0: with one a per wave the a = 0 waves skip that product)
+      const bool unit0 = ((64u >> log_b) <= (1u << LT) ? __builtin_amdgcn_readfirstlane(a) : a) == 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const fe v = XI.ld(i0 + k * st);
+        if (k == 0 && unit0) {
+          x[0] = v;
+          fe_csub2p(x[0]);  // [0, 4p) -> [0, 2p)
+          continue;
+        }
         const uint32_t e = (__builtin_bitreverse32((a << 2) + k) >> 28) * t;  // rev4(g) k1, < R
         x[k] = fe_mul_shoup(v, sm[2 * e], sm[2 * e + 1]);                      // [0, 2p)
       }
