@@ -47,8 +47,8 @@ SIMDS = 1024
 SHOUP_PRODUCT_PEAK = 138.71e9
 DB_PRODUCT_PEAK = 199.98e9
 LOG_N = 24
-PROFILE = os.path.join(ROOT, "profiles", "r05_summary.json")
-PMC = os.path.join(ROOT, "profiles", "r05_pmc_ntt.json")
+PROFILE = os.path.join(ROOT, "profiles", "r06_summary.json")
+PMC = os.path.join(ROOT, "profiles", "r06_pmc_ntt.json")
 LARGE = os.path.join(ROOT, "tests", "golden", "large_digests.json")
 
 
