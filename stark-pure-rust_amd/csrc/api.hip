@@ -44,6 +44,9 @@ stark_status ensure_buf(stark_ctx* ctx, DevBuf& b, size_t bytes) {
     b.bytes = 0;
     if (e != hipSuccess) return hip_fail(ctx, e, "hipFree");
   }
+  // (on the context's device whatever the calling thread's current one is: group members run on
+  // threads of their own)
+  STARK_HIP(ctx, hipSetDevice(ctx->device));
   hipError_t e = hipMalloc(&b.ptr, bytes ? bytes : 16);
   if (e != hipSuccess) {
     b.ptr = nullptr;
