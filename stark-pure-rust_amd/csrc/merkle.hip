@@ -224,16 +224,12 @@ constexpr uint32_t kTailThreads = 1024;
 constexpr uint32_t kTailBlock = kTailThreads / 4;  // input-level nodes per workgroup
 constexpr uint64_t kTailFrom = 65536;              // pair levels narrower than this take the quad kernel
 
-// Pair mode only: input level (count nodes) from `below`, then `extra` more
-// levels in LDS; same LevelPtrs convention as merkle_build_kernel.
-__global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest* __restrict__ below, uint64_t count,
-                                                                   uint32_t extra, LevelPtrs out) {
-  __shared__ __attribute__((aligned(16))) uint32_t msg[2 * kTailBlock * 8];
-  const uint64_t base = (uint64_t)blockIdx.x * kTailBlock;
-  const uint32_t here = (uint32_t)((count - base) < kTailBlock ? (count - base) : kTailBlock);
-  const uint4* src = reinterpret_cast<const uint4*>(below + 2 * base);
-  for (uint32_t i = threadIdx.x; i < here * 4; i += blockDim.x) reinterpret_cast<uint4*>(msg)[i] = src[i];
-  __syncthreads();
+// The levels of one workgroup's block: `here` nodes of the input level from the pairs in msg (LDS, already
+// loaded), then `extra` more levels; level k's nodes go to out.lv[k] + (base >> k).  With `coherent`, the
+// block's last node is written by agent-scope stores (write-through to the chip's coherence point), so
+// another workgroup can read it in the same launch.
+__device__ __forceinline__ void tail_levels(uint32_t* msg, uint64_t base, uint32_t here, uint32_t extra,
+                                            const LevelPtrs& out, bool coherent) {
   const uint32_t node = threadIdx.x >> 2, q = threadIdx.x & 3;
   uint32_t width = here;
   for (uint32_t k = 0; k <= extra; ++k) {
@@ -245,12 +241,51 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
       msg[node * 8 + q] = lo;
       msg[node * 8 + 4 + q] = hi;
       uint32_t* g = reinterpret_cast<uint32_t*>(out.lv[k] + (base >> k) + node);
-      g[q] = lo;
-      g[4 + q] = hi;
+      if (coherent && k == extra) {
+        __hip_atomic_store(g + q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 4 + q, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        g[q] = lo;
+        g[4 + q] = hi;
+      }
     }
     __syncthreads();
     width >>= 1;
   }
+}
+
+// Pair mode only: input level (count nodes) from `below`, then `extra` more levels in LDS; same LevelPtrs
+// convention as merkle_build_kernel.  extra2 > 0 (grid > 1): the launch also does the next launch's work,
+// i.e. the levels above its workgroups' top nodes (gridDim.x / 2 nodes, then extra2 - 1 more levels, into
+// out2), in the workgroup that finishes last.  Each workgroup publishes its top node with agent-scope
+// stores, waits for them, and counts itself in *done (agent scope); the workgroup that counts last reads
+// the gridDim.x top nodes with agent-scope loads and resets *done for the tree's next build.  (No release
+// fence: it would write back the XCD's whole L2, and only these nodes are read in this launch.)
+__global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest* __restrict__ below, uint64_t count,
+                                                                   uint32_t extra, LevelPtrs out, uint32_t extra2,
+                                                                   LevelPtrs out2, uint32_t* done) {
+  __shared__ __attribute__((aligned(16))) uint32_t msg[2 * kTailBlock * 8];
+  __shared__ uint32_t last;
+  const uint64_t base = (uint64_t)blockIdx.x * kTailBlock;
+  const uint32_t here = (uint32_t)((count - base) < kTailBlock ? (count - base) : kTailBlock);
+  const uint4* src = reinterpret_cast<const uint4*>(below + 2 * base);
+  for (uint32_t i = threadIdx.x; i < here * 4; i += blockDim.x) reinterpret_cast<uint4*>(msg)[i] = src[i];
+  __syncthreads();
+  tail_levels(msg, base, here, extra, out, extra2 > 0);
+  if (extra2 == 0) return;  // (uniform)
+  if (threadIdx.x < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top node's stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;  // (uniform)
+  const uint32_t n_top = gridDim.x;  // one top node per workgroup, at out.lv[extra]
+  const uint32_t* top = reinterpret_cast<const uint32_t*>(out.lv[extra]);
+  for (uint32_t i = threadIdx.x; i < n_top * 8; i += blockDim.x)
+    msg[i] = __hip_atomic_load(top + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  tail_levels(msg, 0, n_top / 2, extra2 - 1, out2, false);
 }
 
 // Proof gather: for proof i (index idx[i]): the leaf bytes and the depth
@@ -331,6 +366,21 @@ __global__ __launch_bounds__(kTopMax / 2) void merkle_top_kernel(const Digest* _
   }
 }
 
+// The node buffer holds the 2n - 1 digests and, in its last 32 bytes, the fused tail's workgroup counter
+// (merkle_tail_kernel), zeroed when the buffer is allocated and reset by every launch that uses it.
+static uint32_t* tail_counter(stark_merkle_tree* t) {
+  return reinterpret_cast<uint32_t*>((uint8_t*)t->nodes.ptr + t->nodes.bytes - 32);
+}
+static stark_status ensure_nodes(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipStream_t stream) {
+  const void* before = t->nodes.ptr;
+  const size_t before_bytes = t->nodes.bytes;
+  STARK_TRY(ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest) + 32));
+  // (a reallocation can return the old address, so the size tells it too)
+  if (t->nodes.ptr != before || t->nodes.bytes != before_bytes)
+    STARK_HIP(ctx, hipMemsetAsync(tail_counter(t), 0, 32, stream));
+  return STARK_OK;
+}
+
 // Builds every level of the tree over d_leaves (n leaves of leaf_len bytes);
 // with d_leaves == nullptr level 0 (the leaf digests) is already in place.
 // plane_stride != 0: leaf i's bytes [32 c, 32 c + 32) are at d_leaves + c * plane_stride + 32 i
@@ -344,27 +394,45 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
     return STARK_ERR_BAD_ARG;
   uint32_t depth = 0;
   while (((size_t)1 << depth) < n) ++depth;
-  stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
+  stark_status st = ensure_nodes(ctx, t, n, stream);
   if (st != STARK_OK) return st;
   Digest* nodes = (Digest*)t->nodes.ptr;
+  uint32_t* done = tail_counter(t);
   const bool have_level0 = d_leaves == nullptr;
   uint32_t level = have_level0 ? 1 : 0;
   uint64_t count = have_level0 ? n / 2 : n;
   bool leaf_mode = !have_level0;
   while (depth > 0 || !have_level0) {
     if (!leaf_mode && count < kTailFrom) {
-      // Narrow pair levels: quad kernel, up to 8 levels per launch.
+      // Narrow pair levels: quad kernel, up to 8 levels per launch; with more than one workgroup, the
+      // levels above the workgroups' top nodes (the next launch's) run in the last workgroup to finish.
       const uint64_t blk = count < kTailBlock ? count : kTailBlock;
       uint32_t extra = 0;
       while ((blk >> (extra + 1)) >= 1 && level + extra + 1 <= depth) ++extra;
       LevelPtrs lp;
       for (uint32_t k = 0; k <= extra; ++k) lp.lv[k] = nodes + level_offset(n, level + k);
       const unsigned grid = (unsigned)((count + kTailBlock - 1) / kTailBlock);
+      uint32_t extra2 = 0;
+      LevelPtrs lp2{};
+      const bool fuse = grid > 1 && (count >> extra) == grid && level + extra < depth;
+      if (fuse) {  // the next launch: count2 = grid / 2 nodes at level + extra + 1 (grid <= kTailBlock)
+        const uint32_t level2 = level + extra + 1;
+        const uint64_t blk2 = grid / 2;
+        while ((blk2 >> (extra2 + 1)) >= 1 && level2 + extra2 + 1 <= depth) ++extra2;
+        for (uint32_t k = 0; k <= extra2; ++k) lp2.lv[k] = nodes + level_offset(n, level2 + k);
+      }
       hipLaunchKernelGGL(merkle_tail_kernel, dim3(grid), dim3(kTailThreads), 0, stream,
-                         (const Digest*)(nodes + level_offset(n, level - 1)), count, extra, lp);
+                         (const Digest*)(nodes + level_offset(n, level - 1)), count, extra, lp,
+                         fuse ? extra2 + 1 : 0u, lp2, done);
       STARK_HIP(ctx, hipGetLastError());
       level += extra;
       count >>= extra;
+      if (fuse) {
+        ++level;
+        count >>= 1;
+        level += extra2;
+        count >>= extra2;
+      }
     } else {
       // Wide levels: one lane per node, blocks of 1024 nodes reduced by 2
       // more levels in LDS (1024 -> 512 -> 256, one node per thread).  A
@@ -651,7 +719,7 @@ stark_status stark_merkle_update_digests_dev(stark_merkle_tree* t, const uint8_t
   stark_ctx* ctx = t->ctx;
   STARK_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = pick_stream(ctx, stream);
-  stark_status st = ensure_buf(ctx, t->nodes, (2 * n - 1) * sizeof(Digest));
+  stark_status st = ensure_nodes(ctx, t, n, s);
   if (st != STARK_OK) return st;
   uint32_t log_g = 0;
   while ((1u << log_g) < interleave) ++log_g;
