@@ -108,8 +108,8 @@ __device__ __forceinline__ void b2s_short(const uint32_t* w, uint32_t extra_byte
   b2s_compress(out, m, len, 0, true);
 }
 
-// The digit-basis table of a canonical constant c: limb j of c 2^(32 i) mod p at 9 i + j (two32_m = the
-// Montgomery image of 2^32, so fe_mul(c, two32_m) = c 2^32 mod p).
+// The digit-basis table of a canonical constant c: limb j of c 2^(32 i) mod p at 9 i + j, each row one
+// product by the Montgomery image of 2^(32 i) (Pow32), one row per thread.
 __device__ __forceinline__ void db_limbs(const fe& c, uint32_t* __restrict__ out) {  // 9 x 29-bit limbs of c
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
@@ -117,12 +117,6 @@ __device__ __forceinline__ void db_limbs(const fe& c, uint32_t* __restrict__ out
     uint32_t v = c.w[w] >> sh;
     if (sh > 3 && w < 7) v |= c.w[w + 1] << (32 - sh);
     out[j] = v & STARK_DB_M29;
-  }
-}
-__device__ void db_table_dev(fe c, const fe& two32_m, uint32_t* __restrict__ out) {
-  for (int i = 0; i < 8; ++i) {
-    db_limbs(c, out + 9 * i);
-    c = fe_mul(c, two32_m);
   }
 }
 
@@ -175,11 +169,13 @@ struct XsPowers {
   fe v[8];
 };
 
+constexpr uint32_t kKThreads = 256;  // r1cs_k_kernel: kLincombConsts x 8 table rows
+static_assert(kLincombConsts * 8 <= kKThreads, "r1cs_k_kernel rows");
 // k_0 = 1, k_i = from_str(mk_seed([m_root, [i]])) = BE integer of
 // Blake2s(m_root || i) mod p (prove.rs:274-283, utils.rs:25-27, 51-57); then the
 // three per-residue coefficients of L, kx[t] = (k3 + k4 xs_t, k5 + k6 xs_t,
 // k7 + k8 xs_t), so the L kernel needs 8 products per point instead of 14.
-__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, XsPowers xs, fe two32_m,
+__global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one_m, XsPowers xs, Pow32 p32,
                               Transcript* __restrict__ tr) {
   __shared__ fe ks[11];
   __shared__ fe kx[8][3];
@@ -210,12 +206,15 @@ __global__ void r1cs_k_kernel(const uint32_t* __restrict__ m_root, fe r2, fe one
     tr->kx_m[i][2] = kx[i][2];
   }
   __syncthreads();
-  if (i < kLincombConsts) {
+  // The constants' digit-basis tables, one row c 2^(32 r) mod p per thread (kKThreads threads)
+  if (i < kLincombConsts * 8) {
     static constexpr int kIdx[5] = {0, 1, 2, 9, 10};
-    const fe m = i < 5 ? ks[kIdx[i]] : kx[(i - 5) / 3][(i - 5) % 3];
+    const uint32_t c = i >> 3, r = i & 7;
+    const fe m = c < 5 ? ks[kIdx[c]] : kx[(c - 5) / 3][(c - 5) % 3];
     fe unit = fe_zero();
     unit.w[0] = 1;
-    db_table_dev(fe_mul(m, unit), two32_m, tr->k_db[i]);  // canonical constant (Montgomery image x R^-1)
+    const fe canon = fe_mul(m, unit);  // canonical constant (Montgomery image x R^-1)
+    db_limbs(fe_mul(canon, p32.m[r]), tr->k_db[c] + 9 * r);
   }
 }
 
@@ -1292,8 +1291,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
       xs.v[t] = to_dev(wt);
       wt = F.mul(wt, w8);
     }
-    hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(m_tree), mc.r2,
-                       mc.one, xs, to_dev(F.from_u64((uint64_t)1 << 32)), d_tr);
+    hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(kKThreads), 0, s, (const uint32_t*)merkle_root_dev(m_tree),
+                       mc.r2, mc.one, xs, pow32(), d_tr);
     STARK_HIP(ctx, hipGetLastError());
   }
   LincombArgs la;
@@ -1575,13 +1574,13 @@ struct SpotPos {
 };
 
 __global__ void spot_setup_kernel(SpotPos pos, uint32_t n, uint32_t log_s, uint64_t P, const fe* __restrict__ lo,
-                                  const fe* __restrict__ hi, uint32_t kb, fe two32_m, uint32_t* __restrict__ tabs) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                  const fe* __restrict__ hi, uint32_t kb, Pow32 p32, uint32_t* __restrict__ tabs) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, i = t >> 3, r = t & 7;  // row r of position i's table
   if (i >= n) return;
   fe unit = fe_zero();
   unit.w[0] = 1;
   const fe xs = fe_mul(pow_tab(lo, hi, kb, (pos.e[i] << log_s) & (P - 1)), unit);  // x^S, canonical
-  db_table_dev(xs, two32_m, tabs + 72 * i);
+  db_limbs(fe_mul(xs, p32.m[r]), tabs + 72 * i + 9 * r);
 }
 
 struct SpotCols {
@@ -1669,8 +1668,8 @@ stark_status circuit_spot_values(stark_ctx* ctx, const PreparedCircuit& c, const
   fe* vals = (fe*)(d + tab_bytes + part_bytes);
   uint8_t* host = nullptr;
   STARK_TRY(ctx_pinned(ctx, 0, 6 * n * sizeof(fe), (void**)&host));
-  hipLaunchKernelGGL(spot_setup_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sp, (uint32_t)n, log_s, P,
-                     tw.d_lo, tw.d_hi, tw.kb, to_dev(F.from_u64((uint64_t)1 << 32)), tabs);
+  hipLaunchKernelGGL(spot_setup_kernel, dim3((unsigned)((8 * n + 255) / 256)), dim3(256), 0, s, sp, (uint32_t)n, log_s,
+                     P, tw.d_lo, tw.d_hi, tw.kb, pow32(), tabs);
   SpotCols cols;
   for (int k = 0; k < 6; ++k) {
     if (!c.col[k]) return STARK_ERR_BAD_ARG;
@@ -2168,8 +2167,8 @@ static stark_status dprove_lincomb(stark_dprove* h, const uint8_t* m_root, const
   }
   XsPowers xs;
   for (int t = 0; t < 8; ++t) xs.v[t] = d.xs_m[t];
-  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(64), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs,
-                     to_dev(FieldHost::get().from_u64((uint64_t)1 << 32)), d.d_tr);
+  hipLaunchKernelGGL(r1cs_k_kernel, dim3(1), dim3(kKThreads), 0, d.s, (const uint32_t*)d_root, mc.r2, mc.one, xs,
+                     pow32(), d.d_tr);
   STARK_HIP(d.ctx, hipGetLastError());
   LincombArgs la;
   la.rows = d.rows;
