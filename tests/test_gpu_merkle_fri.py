@@ -51,6 +51,26 @@ def test_merkle_multi_core_kat(ctx, oracle):
     assert [p.leaf for p in proofs] == [leaves[i] for i in k["indices"]]
 
 
+def test_merkle_tail_one_launch_sizes(ctx, oracle):
+    """The narrow levels' one-launch form (merkle.hip merkle_tail_kernel: the last workgroup to finish hashes
+    the levels above the blocks' top nodes, counted with an agent-scope atomic kept in the node buffer): one
+    tree object rebuilt at sizes that take it (a tail level of 512 to 32768 nodes) and sizes that do not,
+    growing and shrinking so that its node buffer is reallocated (possibly at the same address) and reused,
+    three rounds; every root and path against the oracle's tree."""
+    t = S.MerkleProofInPlace(ctx)
+    sizes = [1 << 10, 1 << 16, 1 << 12, 1 << 17, 1 << 9, 1 << 14, 1 << 11, 1 << 13, 1 << 15]
+    rng = np.random.default_rng(61)
+    for rnd in range(3):
+        for n in sizes:
+            blob = rng.integers(0, 256, n * 32, dtype=np.uint8).tobytes()
+            idx = sorted(int(i) for i in rng.choice(n, 6, replace=False))
+            root, paths = oracle.merkle(blob, n, 32, idx, chunks=4)
+            t.update_bytes(blob, n, 32)
+            proofs = t.gen_proofs(idx)
+            assert t.get_root() == root, (rnd, n)
+            assert [p.nodes for p in proofs] == paths, (rnd, n)
+
+
 def test_golden_merkle(ctx):
     for v in GOLD["merkle"]:
         leaves = b"".join(O.to_bytes_le(x) for x in O.from_limbs(O.random_elements(v["n"], v["seed"])))
