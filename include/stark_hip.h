@@ -450,7 +450,8 @@ void stark_dprove_free(stark_dprove* h);
  * passed to the group entry points, which keep the reference's signatures and return what the
  * single-context calls return, bit for bit.  The members exchange data by peer copies on their own
  * streams (xGMI between devices); no collective library and no process per GPU is needed.  A group is
- * not shared between threads (it runs its members on threads of its own). */
+ * not shared between threads (it runs its members on g - 1 host threads of its own, parked between calls
+ * and joined by stark_group_destroy). */
 typedef struct stark_group stark_group;
 typedef struct stark_group_tree stark_group_tree;
 /* g = 1, 2, 4 or 8 members on devices[0..g). */
