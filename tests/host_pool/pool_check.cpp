@@ -125,6 +125,7 @@ static void par(unsigned n, const std::function<void(unsigned)>& fn) {
 }
 
 static std::atomic<int> g_fail{0};
+static std::atomic<uint64_t> g_done_calls{0};  // progress, for the watchdog
 
 // One call of n items; checks exactly-once and nothing running after return.
 static void one_call(unsigned n, unsigned spin_us, const char* who, unsigned id) {
@@ -155,6 +156,7 @@ static void one_call(unsigned n, unsigned spin_us, const char* who, unsigned id)
   }
   // (a late item of a returned call may still touch hits/running: give it time before they go)
   if (bad) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  g_done_calls.fetch_add(1);
 }
 
 static void caller(unsigned calls, unsigned seed, const char* who) {
@@ -198,6 +200,22 @@ int main(int argc, char** argv) {
   }
   g_r4 = strcmp(argv[1], "r4") == 0;
   const unsigned calls = argc > 2 ? (unsigned)atoi(argv[2]) : 400;
+  // A broken pool can also lose an item's completion and wait forever (the round-4 pool's double-counted
+  // pending_): no call finishing for 10 s is reported as a violation too.
+  std::thread([] {
+    uint64_t last = g_done_calls.load();
+    for (;;) {
+      std::this_thread::sleep_for(std::chrono::seconds(10));
+      const uint64_t now = g_done_calls.load();
+      if (now == last) {
+        fprintf(stderr, "no call returned in 10 s after %llu calls (a lost completion); hits: hang\n",
+                (unsigned long long)now);
+        fflush(stderr);
+        std::_Exit(1);
+      }
+      last = now;
+    }
+  }).detach();
   std::thread a([&] { caller(calls, 1, "caller A"); });
   std::thread b([&] { caller(calls, 2, "caller B"); });
   // side-thread tasks that make host_parallel calls of their own while the callers run

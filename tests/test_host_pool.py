@@ -33,8 +33,9 @@ def test_product_pool_exactly_once(built):
 
 
 def test_round4_pool_fails_exactly_once(built):
-    """The counter-example: the same harness catches the round-4 handoff (an item run twice or never;
-    a stale worker may then also crash the process, which counts as the same failure)."""
+    """The counter-example: the same harness catches the round-4 handoff (an item run twice or never, or
+    a call that never returns, which the harness's watchdog reports; a stale worker may then also crash
+    the process, which counts as the same failure)."""
     r = _run("pool_check", "r4", 600)
     assert r.returncode != 0, (r.returncode, r.stdout, r.stderr)
     assert "hits:" in r.stderr
