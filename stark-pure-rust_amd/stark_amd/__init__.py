@@ -250,6 +250,15 @@ def _elems(a) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.uint64).reshape(-1, 4)
 
 
+def _out_array(out, log_n: int) -> np.ndarray:
+    if out is None:
+        return np.empty((1 << log_n, 4), dtype=np.uint64)
+    if not (isinstance(out, np.ndarray) and out.dtype == np.uint64 and out.flags["C_CONTIGUOUS"]
+            and out.shape == (1 << log_n, 4)):
+        raise ValueError("out must be a C-contiguous (2^log_n, 4) uint64 array")
+    return out
+
+
 class Context:
     """One GPU (replaces commitment::multicore::Worker, multicore.rs:43-45)."""
 
@@ -296,19 +305,20 @@ class Context:
         return {"cached": c.value, "cache_limit": l.value, "resident": r.value}
 
     # ---- fri::fft ----------------------------------------------------------
-    def best_fft(self, coefficients, root_of_unity, log_order_of_root: int) -> np.ndarray:
-        """fft.rs:327-357."""
+    def best_fft(self, coefficients, root_of_unity, log_order_of_root: int, out=None) -> np.ndarray:
+        """fft.rs:327-357.  `out` (optional): a C-contiguous (2^log, 4) uint64 array to write into, as the
+        reference's best_fft writes into the caller's Vec; a fresh array costs its page faults on every call."""
         c = _elems(coefficients)
-        out = np.empty((1 << log_order_of_root, 4), dtype=np.uint64)
+        out = _out_array(out, log_order_of_root)
         r = _limbs(root_of_unity)
         self.check(self.lib.stark_best_fft(self.h, _p64(c), len(c), _p64(r), log_order_of_root, _p64(out)),
                    "best_fft")
         return out
 
-    def inv_best_fft(self, evaluations, root_of_unity, log_order_of_root: int) -> np.ndarray:
-        """fft.rs:359-379."""
+    def inv_best_fft(self, evaluations, root_of_unity, log_order_of_root: int, out=None) -> np.ndarray:
+        """fft.rs:359-379 (`out` as in best_fft)."""
         c = _elems(evaluations)
-        out = np.empty((1 << log_order_of_root, 4), dtype=np.uint64)
+        out = _out_array(out, log_order_of_root)
         r = _limbs(root_of_unity)
         self.check(self.lib.stark_inv_best_fft(self.h, _p64(c), len(c), _p64(r), log_order_of_root, _p64(out)),
                    "inv_best_fft")
