@@ -21,7 +21,7 @@ import ctypes
 
 import numpy as np
 
-from . import Proof, StarkError, _elems, _limbs, _p64, _vp, load_library
+from . import Proof, StarkError, _elems, _limbs, _out_array, _p64, _vp, load_library
 
 
 def _lib():
@@ -65,18 +65,18 @@ class Group:
         self.check(self.lib.stark_group_synchronize(self.h), "group_synchronize")
 
     # ---- fri::fft -------------------------------------------------------------------------------
-    def best_fft(self, coefficients, root_of_unity, log_order_of_root: int) -> np.ndarray:
-        """fft.rs:327-357 over the group."""
+    def best_fft(self, coefficients, root_of_unity, log_order_of_root: int, out=None) -> np.ndarray:
+        """fft.rs:327-357 over the group (`out`: a caller buffer, as Context.best_fft)."""
         c = _elems(coefficients)
-        out = np.empty((1 << log_order_of_root, 4), dtype=np.uint64)
+        out = _out_array(out, log_order_of_root)
         self.check(self.lib.stark_group_best_fft(self.h, _p64(c), len(c), _p64(_limbs(root_of_unity)),
                                                  log_order_of_root, _p64(out)), "group_best_fft")
         return out
 
-    def inv_best_fft(self, evaluations, root_of_unity, log_order_of_root: int) -> np.ndarray:
-        """fft.rs:359-379 over the group."""
+    def inv_best_fft(self, evaluations, root_of_unity, log_order_of_root: int, out=None) -> np.ndarray:
+        """fft.rs:359-379 over the group (`out` as in best_fft)."""
         c = _elems(evaluations)
-        out = np.empty((1 << log_order_of_root, 4), dtype=np.uint64)
+        out = _out_array(out, log_order_of_root)
         self.check(self.lib.stark_group_inv_best_fft(self.h, _p64(c), len(c), _p64(_limbs(root_of_unity)),
                                                      log_order_of_root, _p64(out)), "group_inv_best_fft")
         return out
