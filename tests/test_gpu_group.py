@@ -41,13 +41,14 @@ def _fixture(name):
     return (open(os.path.join(FIX, f"{name}.r1cs"), "rb").read(), open(os.path.join(FIX, f"{name}.wtns"), "rb").read())
 
 
-@pytest.mark.parametrize("G", [2, 4, 8])
-@pytest.mark.parametrize("log_n,length", [(6, 64), (10, 700), (16, 1 << 14)])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("log_n,length", [(3, 5), (6, 64), (10, 700), (10, 0), (16, 1 << 14)])
 def test_group_best_fft_small_vs_oracle(oracle, G, log_n, length):
-    """Zero padding (len < 2^log_n), both directions, sizes from the smallest the group splits."""
+    """Zero padding (len < 2^log_n, down to an empty input), both directions, from sizes the group does not
+    split (n < G^2: member 0 alone, and a one-member group) to sizes it does."""
     g = _group(G)
     try:
-        c = O.random_elements(length, 0x5EED0600 + log_n)
+        c = O.random_elements(max(length, 1), 0x5EED0600 + log_n)[:length]
         w = O.root_of_unity(log_n)
         assert np.array_equal(g.best_fft(c, w, log_n), oracle.best_fft(c, w, log_n, cpus=8))
         assert np.array_equal(g.inv_best_fft(c, w, log_n), oracle.inv_best_fft(c, w, log_n, cpus=8))
@@ -156,8 +157,8 @@ def test_group_merkle_vs_oracle(oracle, G, log_n, leaf_len):
         g.close()
 
 
-@pytest.mark.parametrize("name,G", [("compute", 2), ("compute", 8), ("poseidon3_test", 4), ("pedersen_test", 2),
-                                    ("pedersen_test", 8), ("bits", 4)])
+@pytest.mark.parametrize("name,G", [("compute", 1), ("compute", 2), ("compute", 8), ("poseidon3_test", 4),
+                                    ("pedersen_test", 2), ("pedersen_test", 8), ("bits", 4)])
 def test_group_prove_vs_golden(name, G):
     """One proof over G members equals the golden StarkProof digest (BASELINE config 4: poseidon3 on 4)."""
     r1, wt = _fixture(name)
