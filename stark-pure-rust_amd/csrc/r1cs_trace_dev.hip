@@ -276,13 +276,6 @@ stark_status walk_records_into(const uint8_t* cons, size_t cons_len, uint32_t n_
   return STARK_OK;
 }
 
-stark_status walk_records(const uint8_t* cons, size_t cons_len, uint32_t n_c, std::vector<uint32_t>& fac,
-                          std::vector<uint32_t>& base) {
-  fac.resize((size_t)6 * n_c + 1);
-  base.resize((size_t)n_c + 1);
-  return walk_records_into(cons, cons_len, n_c, fac.data(), base.data());
-}
-
 // The first use of every public wire (run.rs:411-419) read from the records on the host, in push order
 // (constraint, factor, slot; a factor's padding slots use the last wire), as perm_kernel finds it after
 // the sort.  Stops once every public wire is found; false (undecided) past `budget` slots or at a wire
@@ -662,6 +655,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
 // extends only S, P and A: 3 of the 9 LDE columns.
 
 stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len, PreparedCircuit& c) {
+  PhaseClock clk("circuit_build");
   R1csHeader hd;
   stark_status st = parse_r1cs_header(r1cs, r1cs_len, &hd);
   if (st != STARK_OK) return st;
@@ -670,15 +664,35 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   if (n_wires == 0 || n_public > n_wires) return STARK_ERR_BAD_ARG;
   const uint8_t* cons = r1cs + hd.cons_off;
   const size_t cons_len = r1cs_len - hd.cons_off;
-  std::vector<uint32_t> fac, base;
-  st = walk_records(cons, cons_len, n_c, fac, base);
+  hipStream_t s = ctx->stream;
+  // As in r1cs_trace_device: the raw constraint section goes up through the staging buffer (into the
+  // context's trace_raw, scratch here) while a host worker walks the records into pinned memory and
+  // looks for the public wires' first uses, so the build needs no read-back before its LDE.
+  const size_t fac_n = (size_t)6 * n_c + 1, base_n = (size_t)n_c + 1;
+  uint32_t* walk = nullptr;
+  STARK_TRY(ctx_pinned(ctx, 2, (fac_n + base_n + 1) * 4, (void**)&walk));
+  uint32_t* const fac = walk;
+  uint32_t* const base = walk + fac_n;
+  uint32_t* const h_err = base + base_n;  // the wire-id flag's read-back (pinned: an async copy)
+  STARK_TRY(ensure_buf(ctx, ctx->trace_raw, cons_len));
+  uint8_t* const RAW = (uint8_t*)ctx->trace_raw.ptr;
+  stark_status walk_st = STARK_OK;
+  std::vector<uint64_t> pf_host;
+  bool pf_ok = false;
+  const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
+  st = staged_upload(ctx, {{RAW, cons, cons_len}}, s, stagers, [&] {
+    walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
+    if (walk_st == STARK_OK)
+      pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
+  });
   if (st != STARK_OK) return st;
+  if (walk_st != STARK_OK) return walk_st;
+  clk.mark("record walk || upload");
   const uint64_t a_len = base[n_c];
   const uint64_t os = 3 * a_len;
   if (a_len == 0) return STARK_ERR_BAD_ARG;
   uint32_t key_bits = 1;
   while (key_bits < 32 && (1ull << key_bits) < n_wires) ++key_bits;
-  hipStream_t s = ctx->stream;
   size_t sort_tmp = 0;
   STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
@@ -690,20 +704,19 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
     return o;
   };
   // Kept: base, coef, flags, perm, slot wires.  Scratch (the circuit's own arena, so a
-  // prepared circuit never aliases the context's trace arena): records, sort buffers.
-  const size_t o_base = take(base.size() * 4), o_coef = take(os * 32), o_flags = take(3 * os),
-               o_perm = take(os * 8), o_sw = take(os * 4), o_cons = take(cons_len), o_fac = take(fac.size() * 4),
-               o_k = take(os * 4), o_v = take(os * 4), o_k2 = take(os * 4), o_v2 = take(os * 4),
-               o_last = take((size_t)n_wires * 4), o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp);
+  // prepared circuit never aliases the context's trace arena): walk tables, sort buffers.
+  const size_t o_base = take(base_n * 4), o_coef = take(os * 32), o_flags = take(3 * os), o_perm = take(os * 8),
+               o_sw = take(os * 4), o_fac = take(fac_n * 4), o_k = take(os * 4), o_v = take(os * 4),
+               o_k2 = take(os * 4), o_v2 = take(os * 4), o_last = take((size_t)n_wires * 4),
+               o_pf = take(n_public * 8), o_err = take(4), o_tmp = take(sort_tmp);
   st = ensure_buf(ctx, c.arena, off);
   if (st != STARK_OK) return st;
   uint8_t* A = (uint8_t*)c.arena.ptr;
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_cons, cons, cons_len, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac.data(), fac.size() * 4, hipMemcpyHostToDevice, s));
-  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base.data(), base.size() * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_fac, fac, fac_n * 4, hipMemcpyHostToDevice, s));
+  STARK_HIP(ctx, hipMemcpyAsync(A + o_base, base, base_n * 4, hipMemcpyHostToDevice, s));
   STARK_HIP(ctx, hipMemsetAsync(A + o_err, 0, 4, s));
   FillArgs fa;
-  fa.cons = A + o_cons;
+  fa.cons = RAW;
   fa.fac_rec = (const uint32_t*)(A + o_fac);
   fa.fac_cnt = (const uint32_t*)(A + o_fac) + (size_t)3 * n_c;
   fa.base = (const uint32_t*)(A + o_base);
@@ -738,12 +751,20 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
                      (const uint32_t*)(A + o_v2), os, (const uint32_t*)(A + o_last), (uint32_t)n_public,
                      (uint64_t*)(A + o_perm), (uint64_t*)(A + o_pf));
   STARK_HIP(ctx, hipGetLastError());
+  // The wire-id flag comes back behind the LDE (circuit_lde ends in a synchronisation; the slot kernels
+  // clamp a bad wire id, so what runs before the check stays in bounds).  The first uses come from the
+  // host scan, or, where it gave up, from the device with the one read-back.
+  *h_err = 0;
+  STARK_HIP(ctx, hipMemcpyAsync(h_err, A + o_err, 4, hipMemcpyDeviceToHost, s));
   std::vector<uint64_t> pf(n_public);
-  uint32_t h_err = 0;
-  STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipMemcpyAsync(&h_err, A + o_err, 4, hipMemcpyDeviceToHost, s));
-  STARK_HIP(ctx, hipStreamSynchronize(s));
-  if (h_err) return STARK_ERR_BAD_ARG;
+  if (pf_ok) {
+    pf = pf_host;
+  } else {
+    STARK_HIP(ctx, hipMemcpyAsync(pf.data(), A + o_pf, n_public * 8, hipMemcpyDeviceToHost, s));
+    STARK_HIP(ctx, hipStreamSynchronize(s));
+    if (*h_err) return STARK_ERR_BAD_ARG;
+  }
+  clk.mark("slots, sort, perm enqueued");
   c.pfi.clear();
   for (size_t wi = 0; wi < n_public; ++wi)
     if (pf[wi] != ~0ull) {
@@ -760,8 +781,12 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   c.flags = flags;
   c.perm = (const uint64_t*)(A + o_perm);
   c.slot_wire = (const uint32_t*)(A + o_sw);
-  return circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s,
-                     c.with_zb, c.col, c.spot ? &c.spot_log_t : nullptr);
+  st = circuit_lde(ctx, c.coef, c.flags, c.perm, os, c.pfi.data(), c.pfi.size() / 2, c.world, c.rank, c.lde, s,
+                   c.with_zb, c.col, c.spot ? &c.spot_log_t : nullptr);
+  clk.mark("circuit LDE (synced)");
+  if (hipStreamSynchronize(s) != hipSuccess && st == STARK_OK) st = STARK_ERR_HIP;
+  if (*h_err) return STARK_ERR_BAD_ARG;  // a wire id >= n_wires (reader.rs:4-89 bounds)
+  return st;
 }
 
 // The witness of one proof: decode, then S and P from the circuit's slot wires.
