@@ -23,6 +23,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "host_walk.h"
 #include "internal.h"
 
 namespace stark {
@@ -244,38 +245,6 @@ __global__ void wit_fill_kernel(uint64_t n_slots, const uint32_t* __restrict__ s
 
 unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
-// One host pass over the constraint records' counts: fac = fac_rec[3 n_c] (byte
-// offset of each factor's first record) | fac_cnt[3 n_c] | pad, and base[ci] = the
-// first slot of constraint ci (n_c + 1 entries; run.rs:109-137 slot counts).  Every
-// entry is written (no zero fill), so the arrays may be reused uninitialised memory.
-stark_status walk_records_into(const uint8_t* cons, size_t cons_len, uint32_t n_c, uint32_t* fac, uint32_t* base) {
-  if (cons_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
-  uint32_t* fac_rec = fac;
-  uint32_t* fac_cnt = fac + (size_t)3 * n_c;
-  fac[(size_t)6 * n_c] = 0;
-  base[0] = 0;
-  size_t pos = 0;
-  uint64_t b = 0;
-  for (uint32_t ci = 0; ci < n_c; ++ci) {
-    uint32_t n_coeff = 0;
-    for (int f = 0; f < 3; ++f) {
-      if (cons_len - pos < 4) return STARK_ERR_BAD_ARG;
-      uint32_t nc;
-      memcpy(&nc, cons + pos, 4);
-      pos += 4;
-      if (nc > (cons_len - pos) / 36) return STARK_ERR_BAD_ARG;
-      fac_rec[3 * (size_t)ci + f] = (uint32_t)pos;
-      fac_cnt[3 * (size_t)ci + f] = nc;
-      pos += (size_t)nc * 36;
-      if (nc > n_coeff) n_coeff = nc;
-    }
-    b += n_coeff;
-    if (b > 0xFFFFFFFFull / 3) return STARK_ERR_BAD_LENGTH;
-    base[ci + 1] = (uint32_t)b;
-  }
-  return STARK_OK;
-}
-
 // The first use of every public wire (run.rs:411-419) read from the records on the host, in push order
 // (constraint, factor, slot; a factor's padding slots use the last wire), as perm_kernel finds it after
 // the sort.  Stops once every public wire is found; false (undecided) past `budget` slots or at a wire
@@ -312,6 +281,15 @@ bool host_first_uses(const uint8_t* cons, const uint32_t* fac, const uint32_t* b
 
 }  // namespace
 
+// The host threads of an upload with the record walk beside it: the walk's parts (each a share of the
+// section, so as many as can run at once; a part's task stages chunks once its part is walked) and the tasks
+// that only stage, together no more tasks than threads.
+static void split_host_threads(unsigned* walkers, unsigned* stagers) {
+  const unsigned t = host_threads();
+  *walkers = std::max(1u, std::min(8u, t / 2));
+  *stagers = std::max(1u, t > *walkers ? t - *walkers : 1u);
+}
+
 // Host-to-device copies of caller (pageable) memory through the context's pinned staging buffer:
 // the copy is split in 2 MB chunks that `workers` host threads memcpy into the staging buffer, each
 // thread enqueueing the DMA of a chunk as soon as it is staged, so the DMAs overlap the memcpys.  A
@@ -324,7 +302,7 @@ struct Upload {
   size_t len;
 };
 static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups, hipStream_t s, unsigned workers,
-                                  const std::function<void()>& beside) {
+                                  unsigned sides, const std::function<void(unsigned)>& side) {
   constexpr size_t kChunk = (size_t)2 << 20;
   size_t total = 0;
   for (const Upload& u : ups) total += u.len;
@@ -355,14 +333,12 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
   // The first failing copy's error, recorded by the worker that saw it (HIP's last-error state is
   // per thread, so the caller could not read it back with hipGetLastError).
   std::atomic<int> failed{(int)hipSuccess};
-  // thread 1 runs `beside` (the record walk); every other thread stages chunks in order of claim
-  host_parallel(workers + 1, [&](unsigned t) {
-    if (t == 1) {
-      beside();
-      return;
-    }
+  // tasks 1 .. sides run side(0 .. sides - 1) (the record walk's parts) and then stage too; the caller and the
+  // other `workers - 1` tasks stage chunks in order of claim from the start
+  host_parallel(workers + sides, [&](unsigned t) {
+    if (t >= 1 && t <= sides) side(t - 1);
     // (a worker's current device is whatever it last ran for: the context's, for its copies)
-    if (t > 1 && hipSetDevice(ctx->device) != hipSuccess) {
+    if (t > 0 && hipSetDevice(ctx->device) != hipSuccess) {
       int ok = (int)hipSuccess;
       failed.compare_exchange_strong(ok, (int)hipErrorInvalidDevice);
       return;
@@ -492,18 +468,20 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
     st = ensure_buf(ctx, ctx->trace_raw, o_raw_w + wbytes);
     if (st != STARK_OK) return st;
     RAW = (uint8_t*)ctx->trace_raw.ptr;
-    stark_status walk_st = STARK_OK;
-    const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
-    // defer_err: the public wires' first uses are also read on the host beside the uploads (a bounded scan
-    // that usually ends in the first constraints), so the build needs no read-back and the caller checks
-    // the device's wire-id flag at its own first synchronisation (d_err).
-    st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers, [&] {
-      walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
-      if (walk_st == STARK_OK && defer_err && n_wires > 0)
-        pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
-    });
+    // The walk's parts run beside the stagers (RecordWalk, host_walk.h), then link on this thread.
+    // defer_err: the public wires' first uses are also read on the host (a bounded scan that usually ends
+    // in the first constraints), so the build needs no read-back and the caller checks the device's
+    // wire-id flag at its own first synchronisation (d_err).
+    unsigned walkers, stagers;
+    split_host_threads(&walkers, &stagers);
+    RecordWalk rw(cons, cons_len, n_c, n_wires, walkers);
+    st = staged_upload(ctx, {{RAW, cons, cons_len}, {RAW + o_raw_w, wv, wbytes}}, s, stagers, rw.parts(),
+                       [&](unsigned k) { rw.part(k); });
     if (st != STARK_OK) return st;
+    const stark_status walk_st = rw.finish(fac, base);
     if (walk_st != STARK_OK) return walk_st;
+    if (defer_err && n_wires > 0)
+      pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
     a_len = base[n_c];
     clk.mark("headers + record walk || uploads");
   }
@@ -676,17 +654,16 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   uint32_t* const h_err = base + base_n;  // the wire-id flag's read-back (pinned: an async copy)
   STARK_TRY(ensure_buf(ctx, ctx->trace_raw, cons_len));
   uint8_t* const RAW = (uint8_t*)ctx->trace_raw.ptr;
-  stark_status walk_st = STARK_OK;
-  std::vector<uint64_t> pf_host;
-  bool pf_ok = false;
-  const unsigned stagers = std::max(1u, std::min(6u, host_threads() - 1));
-  st = staged_upload(ctx, {{RAW, cons, cons_len}}, s, stagers, [&] {
-    walk_st = walk_records_into(cons, cons_len, n_c, fac, base);
-    if (walk_st == STARK_OK)
-      pf_ok = host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
-  });
+  unsigned walkers, stagers;
+  split_host_threads(&walkers, &stagers);
+  RecordWalk rw(cons, cons_len, n_c, n_wires, walkers);
+  st = staged_upload(ctx, {{RAW, cons, cons_len}}, s, stagers, rw.parts(), [&](unsigned k) { rw.part(k); });
   if (st != STARK_OK) return st;
+  const stark_status walk_st = rw.finish(fac, base);
   if (walk_st != STARK_OK) return walk_st;
+  std::vector<uint64_t> pf_host;
+  const bool pf_ok =
+      host_first_uses(cons, fac, base, n_c, base[n_c], n_public, n_wires, (uint64_t)1 << 18, pf_host);
   clk.mark("record walk || upload");
   const uint64_t a_len = base[n_c];
   const uint64_t os = 3 * a_len;

@@ -1,6 +1,7 @@
 """Same-box A/B of whole proofs across library builds (any ABI revision: raw ctypes, no header check), one
 child process per build per round, rounds alternating so that clock and thermal drift hit every build alike:
     python tools/ab_prove.py [--fixtures compute,pedersen_test] [--reps 20] [--rounds 3] a.so b.so ...
+Fixtures are names under tests/golden/r1cs or synthK (the synthetic 2^K-step circuit).
 Prints per build and fixture the best and median host wall-clock of prove_with_witness on raw bytes
 (stark_prove_r1cs_bytes + reading the JSON) and the JSON's digest (must agree across builds)."""
 import argparse
@@ -24,7 +25,12 @@ assert lib.stark_ctx_create(0, ctypes.byref(ctx)) == 0
 out = {}
 d = os.path.join(sys.argv[2], "tests", "golden", "r1cs")
 for name in sys.argv[3].split(","):
-    r, w = open(f"{d}/{name}.r1cs", "rb").read(), open(f"{d}/{name}.wtns", "rb").read()
+    if name.startswith("synth"):  # synthK: the synthetic 2^K-step circuit (tools/synth_r1cs.py)
+        sys.path.insert(0, os.path.join(sys.argv[2], "tools"))
+        import synth_r1cs
+        r, w = synth_r1cs.for_steps(int(name[5:]))
+    else:
+        r, w = open(f"{d}/{name}.r1cs", "rb").read(), open(f"{d}/{name}.wtns", "rb").read()
     ts, dig = [], None
     for i in range(int(sys.argv[4]) + 2):
         t = time.perf_counter()
