@@ -21,7 +21,7 @@
 #include <atomic>
 #include <vector>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "host_walk.h"
 #include "internal.h"
@@ -244,6 +244,22 @@ __global__ void wit_fill_kernel(uint64_t n_slots, const uint32_t* __restrict__ s
 }
 
 unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// The slots' (wire, slot) pairs sorted by wire (stable: both algorithms below are).  rocPRIM's default
+// dispatch takes its merge sort for 4-byte keys up to 2^20 items: about 20 launches of ~5 us at 2^19 slots;
+// from 2^18 slots its onesweep radix sort (a histogram, a scan and one pass per 8 key bits) is used instead
+// (profiles/r06_slot_sort_ab.txt: 0.1 ms off the 2^20-step proof; below, on pedersen, the merge sort is faster).
+constexpr int kOnesweepFrom = 1 << 18;
+using OnesweepConfig =
+    rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+hipError_t sort_slots(void* tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                      const uint32_t* vals_in, uint32_t* vals_out, int n, int begin_bit, int end_bit, hipStream_t s) {
+  if (n >= kOnesweepFrom)
+    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                                     (unsigned)n, (unsigned)begin_bit, (unsigned)end_bit, s);
+  return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out, (unsigned)n,
+                                   (unsigned)begin_bit, (unsigned)end_bit, s);
+}
 
 // The first use of every public wire (run.rs:411-419) read from the records on the host, in push order
 // (constraint, factor, slot; a factor's padding slots use the last wire), as perm_kernel finds it after
@@ -492,7 +508,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
   uint32_t key_bits = 1;
   while (key_bits < 32 && (1ull << key_bits) < n_wires) ++key_bits;
   size_t sort_tmp = 0;
-  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+  STARK_HIP(ctx, sort_slots(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
                                                    (int)key_bits, ctx->stream));
   size_t off = 0;
@@ -582,7 +598,7 @@ stark_status r1cs_trace_device(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_
                      flags + os, flags + 2 * os);
   STARK_HIP(ctx, hipGetLastError());
   size_t tmp_bytes = sort_tmp;
-  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
+  STARK_HIP(ctx, sort_slots(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
                                                    (uint32_t*)(A + o_k2), (const uint32_t*)(A + o_v),
                                                    (uint32_t*)(A + o_v2), (int)os, 0, (int)key_bits, s));
   const uint32_t* keys = (const uint32_t*)(A + o_k2);
@@ -671,7 +687,7 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
   uint32_t key_bits = 1;
   while (key_bits < 32 && (1ull << key_bits) < n_wires) ++key_bits;
   size_t sort_tmp = 0;
-  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+  STARK_HIP(ctx, sort_slots(nullptr, sort_tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)os, 0,
                                                    (int)key_bits, s));
   size_t off = 0;
@@ -719,7 +735,7 @@ stark_status circuit_build(stark_ctx* ctx, const uint8_t* r1cs, size_t r1cs_len,
                      flags + os, flags + 2 * os);
   STARK_HIP(ctx, hipGetLastError());
   size_t tmp_bytes = sort_tmp;
-  STARK_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
+  STARK_HIP(ctx, sort_slots(A + o_tmp, tmp_bytes, (const uint32_t*)(A + o_k),
                                                    (uint32_t*)(A + o_k2), (const uint32_t*)(A + o_v),
                                                    (uint32_t*)(A + o_v2), (int)os, 0, (int)key_bits, s));
   hipLaunchKernelGGL(group_last_kernel, dim3(blocks(os)), dim3(256), 0, s, (const uint32_t*)(A + o_k2), os,
