@@ -264,7 +264,8 @@ struct Sparse {
 
 // Merkle internals (merkle.hip).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream, size_t plane_stride = 0);
+                          hipStream_t stream, size_t plane_stride = 0, bool level0_ready = false);
+stark_status merkle_level0(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipStream_t stream, uint32_t** level0);
 stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t);
 size_t merkle_device_bytes(const stark_merkle_tree* t);  // device memory the tree owns (0 for null)

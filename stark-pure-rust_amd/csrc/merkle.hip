@@ -381,12 +381,23 @@ static stark_status ensure_nodes(stark_ctx* ctx, stark_merkle_tree* t, size_t n,
   return STARK_OK;
 }
 
+// Level 0 of the tree over n leaves (the leaf digests, 8 words each), for a kernel that hashes the leaves as
+// it makes them (the constraint kernel: the main tree's rows); merkle_build(..., level0_ready) then builds the
+// levels above.
+stark_status merkle_level0(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipStream_t stream, uint32_t** level0) {
+  if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
+  STARK_TRY(ensure_nodes(ctx, t, n, stream));
+  *level0 = reinterpret_cast<uint32_t*>(t->nodes.ptr);  // (level_offset(n, 0) = 0)
+  return STARK_OK;
+}
+
 // Builds every level of the tree over d_leaves (n leaves of leaf_len bytes);
-// with d_leaves == nullptr level 0 (the leaf digests) is already in place.
+// with d_leaves == nullptr or level0_ready level 0 (the leaf digests) is already in place (with
+// level0_ready the proofs still open d_leaves).
 // plane_stride != 0: leaf i's bytes [32 c, 32 c + 32) are at d_leaves + c * plane_stride + 32 i
 // (leaf_len a multiple of 32, 16-B aligned planes).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream, size_t plane_stride) {
+                          hipStream_t stream, size_t plane_stride, bool level0_ready) {
   if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
   if (leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
   if (plane_stride && (!d_leaves || leaf_len == 0 || leaf_len % 32 || plane_stride % 16 || plane_stride < 32 * n ||
@@ -398,7 +409,7 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   if (st != STARK_OK) return st;
   Digest* nodes = (Digest*)t->nodes.ptr;
   uint32_t* done = tail_counter(t);
-  const bool have_level0 = d_leaves == nullptr;
+  const bool have_level0 = d_leaves == nullptr || level0_ready;
   uint32_t level = have_level0 ? 1 : 0;
   uint64_t count = have_level0 ? n / 2 : n;
   bool leaf_mode = !have_level0;
@@ -464,8 +475,8 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
   t->n = n;
   t->leaf_len = leaf_len;
   t->depth = depth;
-  t->d_leaves = have_level0 ? (const uint8_t*)nodes : d_leaves;
-  t->plane_stride = have_level0 ? 0 : plane_stride;
+  t->d_leaves = d_leaves ? d_leaves : (const uint8_t*)nodes;
+  t->plane_stride = d_leaves ? plane_stride : 0;
   t->built = true;
   return STARK_OK;
 }

@@ -439,6 +439,7 @@ struct ConstraintArgs {
   // R^-k (one product fewer per conversion it skips) and undoes the scale in D = Q inv(Z).
   fe invz_m[3][8];
   int mont_cols;         // K, F0-F2 are Montgomery images (prepared circuits); inv Zb2/Zb3 always are
+  uint32_t* leaf = nullptr;  // non-null: each row's Blake2s (the main tree's level 0, merkle_level0), 8 words
 };
 
 // Q1/Q2/Q3 (utils.rs:181-248, 344-376) -> D1..D3 (utils.rs:379-418), I2/I3
@@ -543,6 +544,25 @@ __global__ __launch_bounds__(256, 3) void r1cs_constraint_kernel(ConstraintArgs 
   fe_store(row + 5 * cs, d3);
   fe_store(row + 6 * cs, b2);
   fe_store(row + 7 * cs, b3);
+  if (a.leaf) {  // (uniform) the main tree's leaf: Blake2s of the 256-B row, 4 blocks of two values each
+    uint32_t h[8], m[16];
+    b2s_init(h);
+    auto block = [&](const fe& x, const fe& y, uint32_t t_bytes, bool last) {
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        m[w] = x.w[w];
+        m[8 + w] = y.w[w];
+      }
+      b2s_compress(h, m, t_bytes, 0, last);
+    };
+    block(p, av, 64, false);
+    block(s, d1, 128, false);
+    block(d2, d3, 192, false);
+    block(b2, b3, 256, true);
+    uint4* q = reinterpret_cast<uint4*>(a.leaf + 8 * i);
+    q[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    q[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  }
 }
 
 struct LincombArgs {
@@ -1279,10 +1299,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   set_inv_z(ca, g2, steps);
   ca.mont_cols = pre ? 1 : 0;
   STARK_TRY(upload_constraint_tables(ctx, d_tr, ca, s));
+  // Main tree over the 256-B rows (prove.rs:261-264): the constraint kernel hashes each row as it makes it
+  // (level 0), the tree's levels above are built from those digests; the proofs open the rows as 8 planes.
+  STARK_TRY(merkle_level0(ctx, m_tree, prec, s, &ca.leaf));
   hipLaunchKernelGGL(r1cs_constraint_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, ca);
   STARK_HIP(ctx, hipGetLastError());
-  // Main tree over the 256-B rows (prove.rs:261-264), read as 8 column planes.
-  STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s, prec * sizeof(fe)));
+  STARK_TRY(merkle_build(ctx, m_tree, (const uint8_t*)rows, prec, 256, s, prec * sizeof(fe), true));
   {
     XsPowers xs;
     const HostFp w8 = F.pow_u64(g2, steps);
