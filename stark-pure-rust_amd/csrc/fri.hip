@@ -48,7 +48,7 @@ __global__ void fri_special_x_kernel(const uint32_t* __restrict__ root, fe* __re
 // Row i of q (local rows; global row g_add + (i << log_g) on a distributed
 // prover whose values are the residue class g_add mod 2^log_g, where the four
 // points of a row are local too since n/4 is a multiple of 2^log_g).
-__device__ __forceinline__ void fri_fold_row(const fe* __restrict__ v, fe* __restrict__ col, uint64_t i, uint64_t q,
+__device__ __forceinline__ fe fri_fold_row(const fe* __restrict__ v, fe* __restrict__ col, uint64_t i, uint64_t q,
                                              uint32_t shift, uint64_t g_add, uint32_t log_g,
                                              const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
                                              const fe& s_m, const fe& zeta_m, const fe& inv4_m) {
@@ -64,16 +64,32 @@ __device__ __forceinline__ void fri_fold_row(const fe* __restrict__ v, fe* __res
   fe acc = fe_add(fe_mul(d3, u_m), d2);
   acc = fe_add(fe_mul(acc, u_m), d1);
   acc = fe_add(fe_mul(acc, u_m), d0);
-  fe_store(col + i, fe_mul(acc, inv4_m));
+  const fe out = fe_mul(acc, inv4_m);
+  fe_store(col + i, out);
+  return out;
 }
 
+// leaf non-null: each output's Blake2s too (the next layer tree's level 0, merkle_level0), 8 words.
 __global__ void fri_fold_kernel(const fe* __restrict__ v, fe* __restrict__ col, uint64_t q, uint32_t shift,
                                 uint64_t g_add, uint32_t log_g,
                                 const fe* __restrict__ lo, const fe* __restrict__ hi, uint32_t kb,
-                                const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m) {
+                                const fe* __restrict__ s_ptr, fe zeta_m, fe inv4_m, uint32_t* __restrict__ leaf) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= q) return;
-  fri_fold_row(v, col, i, q, shift, g_add, log_g, lo, hi, kb, *s_ptr, zeta_m, inv4_m);
+  const fe x = fri_fold_row(v, col, i, q, shift, g_add, log_g, lo, hi, kb, *s_ptr, zeta_m, inv4_m);
+  if (leaf) {  // (uniform)
+    uint32_t h[8], m[16];
+    b2s_init(h);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      m[w] = x.w[w];
+      m[8 + w] = 0;
+    }
+    b2s_compress(h, m, 32, 0, true);
+    uint4* d = reinterpret_cast<uint4*>(leaf + 8 * i);
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  }
 }
 
 // Roots of up to 16 trees gathered into one buffer (one D2H for the transcript).
@@ -224,11 +240,14 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
     const size_t q = m / 4;
     const HostFp zeta = F.pow_u64(w, q);  // w^(n/4)
     const unsigned blocks = (unsigned)((q + 255) / 256);
+    // The next layer's tree: the fold hashes each value it makes (level 0: no leaf pass of its own).
+    uint32_t* leaf = nullptr;
+    STARK_TRY(merkle_level0(ctx, trees[layer + 1], q, s, &leaf));
     hipLaunchKernelGGL(fri_fold_kernel, dim3(blocks), dim3(256), 0, s, cur, next, (uint64_t)q, (uint32_t)(2 * layer),
                        (uint64_t)0, (uint32_t)0,
-                       tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4));
+                       tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4), leaf);
     STARK_HIP(ctx, hipGetLastError());
-    st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s);
+    st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s, 0, leaf != nullptr);
     if (st != STARK_OK) return st;
     p->qs.push_back(q);
     // Recurse on the column with w^4 (fri.rs:215-223).
@@ -646,7 +665,7 @@ static stark_status fri_fold(stark_ctx* ctx, const uint64_t* values, uint64_t* c
   const size_t q = n / 4 / world;
   hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)((q + 255) / 256)), dim3(256), 0, s, (const fe*)values,
                      (fe*)column, (uint64_t)q, (uint32_t)0, (uint64_t)rank, log_g, tw->d_lo, tw->d_hi, tw->kb,
-                     (const fe*)d_sx, to_dev(zeta), to_dev(F.inv(F.from_u64(4))));
+                     (const fe*)d_sx, to_dev(zeta), to_dev(F.inv(F.from_u64(4))), (uint32_t*)nullptr);
   STARK_HIP(ctx, hipGetLastError());
   STARK_TRY(buf_release(ctx, ctx->fri_misc, s));
   if (m_root) STARK_HIP(ctx, hipStreamSynchronize(s));  // sx lives on this stack frame

@@ -231,8 +231,10 @@ __device__ __forceinline__ fe pow_tab(const fe* __restrict__ lo, const fe* __res
 // prove.rs:55-56) and the accumulator leaves u64 LE index || to_bytes_le(w)
 // (utils.rs:254-263).
 // (IDX itself is not written: its extension is the context's shared ext_index_column.)
+// (dig non-null: each 40-B leaf's Blake2s too, the accumulator tree's level 0 (merkle_level0), 8 words.)
 __global__ void r1cs_index_kernel(const uint64_t* __restrict__ perm, uint64_t os, uint64_t steps,
-                                  const fe* __restrict__ w, fe* __restrict__ pidx, uint64_t* __restrict__ acc_leaves) {
+                                  const fe* __restrict__ w, fe* __restrict__ pidx, uint64_t* __restrict__ acc_leaves,
+                                  uint32_t* __restrict__ dig) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= steps) return;
   const uint64_t p = i < os ? perm[i] : i;
@@ -242,6 +244,20 @@ __global__ void r1cs_index_kernel(const uint64_t* __restrict__ perm, uint64_t os
   leaf[0] = p;
 #pragma unroll
   for (int k = 0; k < 4; ++k) leaf[1 + k] = (uint64_t)x.w[2 * k] | ((uint64_t)x.w[2 * k + 1] << 32);
+  if (dig) {  // (uniform) one zero-padded block of the 40 leaf bytes
+    uint32_t h[8], m[16];
+    b2s_init(h);
+    m[0] = (uint32_t)p;
+    m[1] = (uint32_t)(p >> 32);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[2 + k] = x.w[k];
+#pragma unroll
+    for (int k = 10; k < 16; ++k) m[k] = 0;
+    b2s_compress(h, m, 40, 0, true);
+    uint4* d = reinterpret_cast<uint4*>(dig + 8 * i);
+    d[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    d[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  }
 }
 
 // Flag columns F0, F1, F2 (run.rs:283-308) from bytes: dst[f * steps + i] = fb[f * os + i].
@@ -573,6 +589,7 @@ struct LincombArgs {
   uint64_t g_add;        // local point i is global point g_add + (i << log_g)
   uint32_t log_g;
   const Transcript* tr;  // k and kx (device transcript)
+  uint32_t* leaf = nullptr;  // non-null: each value's Blake2s (the L tree's level 0, merkle_level0), 8 words
 };
 
 // L = k0 D1 + k1 D2 + k2 D3 + k3 P + k4 P x^steps + k5 B2 + k6 B2 x^steps +
@@ -608,6 +625,19 @@ __global__ __launch_bounds__(256) void r1cs_lincomb_kernel(LincombArgs a) {
   add(acc, fe_mul_db(s, T(4)));           // k10 S
   fe_reduce_once(acc);
   fe_store(a.out + i, acc);
+  if (a.leaf) {  // (uniform) the L tree's leaf: Blake2s of the 32-B value
+    uint32_t h[8], m[16];
+    b2s_init(h);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      m[w] = acc.w[w];
+      m[8 + w] = 0;
+    }
+    b2s_compress(h, m, 32, 0, true);
+    uint4* q = reinterpret_cast<uint4*>(a.leaf + 8 * i);
+    q[0] = make_uint4(h[0], h[1], h[2], h[3]);
+    q[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  }
 }
 
 // ---- host helpers -----------------------------------------------------------
@@ -1189,18 +1219,20 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
     STARK_HIP(ctx, hipMemsetAsync(d_tr, 0, sizeof(Transcript), s));
   }
   clk.mark("setup + uploads enqueued");
-  // (IDX is not materialised: idx_ext is the shared extension.)
-  hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves);
-  STARK_HIP(ctx, hipGetLastError());
-
   auto proof = std::make_unique<stark_r1cs_proof>();
-  // Accumulator tree -> a_root (utils.rs:250-270) -> r (utils.rs:272-290).
+  // Accumulator tree -> a_root (utils.rs:250-270) -> r (utils.rs:272-290): the index kernel hashes each
+  // 40-B leaf as it writes it (level 0).
   stark_merkle_tree *acc_tree, *m_tree, *l_tree;
   STARK_TRY(ctx_tree(ctx, 2, &acc_tree));
   STARK_TRY(ctx_tree(ctx, 3, &m_tree));
   STARK_TRY(ctx_tree(ctx, 4, &l_tree));
-  STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s));
+  uint32_t* acc_dig = nullptr;
+  STARK_TRY(merkle_level0(ctx, acc_tree, steps, s, &acc_dig));
+  // (IDX is not materialised: idx_ext is the shared extension.)
+  hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves, acc_dig);
+  STARK_HIP(ctx, hipGetLastError());
+  STARK_TRY(merkle_build(ctx, acc_tree, (const uint8_t*)acc_leaves, steps, 40, s, 0, true));
   // A (utils.rs:293-339, prove.rs:183-184): r from a_root, the running products of the numerators and
   // denominators over the steps, their batch inverse (whose top level is the proof's one mid-pipeline host
   // round trip) and A = nmr / dnm.  It reads the trace and a_root only (IDX and PIDX at the step points
@@ -1325,9 +1357,11 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   la.g_add = 0;
   la.log_g = 0;
   la.tr = d_tr;
+  // L tree (prove.rs:329-332): the linear-combination kernel hashes each value as it makes it (level 0).
+  STARK_TRY(merkle_level0(ctx, l_tree, prec, s, &la.leaf));
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s));
+  STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s, 0, true));
   hipLaunchKernelGGL(r1cs_l_root_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(l_tree), d_tr);
   STARK_HIP(ctx, hipGetLastError());
   // The roots and the constraint flags come down behind the L tree; an event marks them.
@@ -1887,7 +1921,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
   STARK_HIP(ctx, hipMemsetAsync(d.d_tr, 0, sizeof(Transcript), s));
   // (PIDX in slot 6; IDX is not materialised: idx_ext)
   hipLaunchKernelGGL(r1cs_index_kernel, dim3(blocks_for(steps)), dim3(256), 0, s, (const uint64_t*)perm,
-                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves);
+                     (uint64_t)os, steps, (const fe*)wcopy, raw + 6 * steps, acc_leaves, (uint32_t*)nullptr);
   STARK_HIP(ctx, hipGetLastError());
   // Accumulator tree -> a_root -> r (utils.rs:250-290), on every rank.
   STARK_TRY(stark_merkle_new(ctx, &d.acc_tree));
