@@ -230,13 +230,15 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   HostFp w = F.from_canonical(root);
   const HostFp inv4 = F.inv(F.from_u64(4));
   const fe r2 = to_dev(F.from_canonical(F.one().v));  // Montgomery image of R
+  bool sx_made = false;  // special_x of this layer already made by its tree's root launch
   for (size_t layer = 0; layer < layers; ++layer) {
     if (layer == 0 && !tree0) {
       st = merkle_build(ctx, trees[0], (const uint8_t*)cur, m, 32, s);
       if (st != STARK_OK) return st;
     }
-    hipLaunchKernelGGL(fri_special_x_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(trees[layer]),
-                       d_sx + layer, r2);
+    if (!sx_made)
+      hipLaunchKernelGGL(fri_special_x_kernel, dim3(1), dim3(64), 0, s,
+                         (const uint32_t*)merkle_root_dev(trees[layer]), d_sx + layer, r2);
     const size_t q = m / 4;
     const HostFp zeta = F.pow_u64(w, q);  // w^(n/4)
     const unsigned blocks = (unsigned)((q + 255) / 256);
@@ -247,8 +249,12 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
                        (uint64_t)0, (uint32_t)0,
                        tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4), leaf);
     STARK_HIP(ctx, hipGetLastError());
-    st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s, 0, leaf != nullptr);
+    // (the next layer's special_x from its tree's root launch where that is the tail kernel)
+    RootFe rf{d_sx + layer + 1, r2};
+    st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s, 0, leaf != nullptr,
+                      layer + 1 < layers ? &rf : nullptr);
     if (st != STARK_OK) return st;
+    sx_made = layer + 1 < layers && rf.out != nullptr;
     p->qs.push_back(q);
     // Recurse on the column with w^4 (fri.rs:215-223).
     cur = next;

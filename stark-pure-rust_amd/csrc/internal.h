@@ -263,8 +263,15 @@ struct Sparse {
 };
 
 // Merkle internals (merkle.hip).
+// The root as a field element (fri.rs:135's special_x: the root's LE words reduced mod p, times r2) into
+// *out, made by the kernel that makes the root (merkle_build's root_fe; out cleared where it cannot).
+struct RootFe {
+  fe* out;
+  fe r2;
+};
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream, size_t plane_stride = 0, bool level0_ready = false);
+                          hipStream_t stream, size_t plane_stride = 0, bool level0_ready = false,
+                          RootFe* root_fe = nullptr);
 stark_status merkle_level0(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipStream_t stream, uint32_t** level0);
 stark_status merkle_root_d2h(stark_ctx* ctx, stark_merkle_tree* t, hipStream_t stream, uint8_t out[32]);
 const uint8_t* merkle_root_dev(const stark_merkle_tree* t);

@@ -261,9 +261,22 @@ __device__ __forceinline__ void tail_levels(uint32_t* msg, uint64_t base, uint32
 // stores, waits for them, and counts itself in *done (agent scope); the workgroup that counts last reads
 // the gridDim.x top nodes with agent-scope loads and resets *done for the tree's next build.  (No release
 // fence: it would write back the XCD's whole L2, and only these nodes are read in this launch.)
+// The root as a field element (RootFe, internal.h): its LE words reduced mod p, times r2, from the root in
+// msg[0..7] (the workgroup's last level, node 0).
+__device__ __forceinline__ void root_fe_out(const uint32_t* msg, const RootFe& rf) {
+  fe x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x.w[i] = msg[i];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) fe_reduce_once(x);  // x < 2^256 < 6p
+  *rf.out = fe_mul(x, rf.r2);
+}
+
+// rf.out non-null: this launch reaches the root (one workgroup, or the fused top), which is also written
+// out as a field element (the FRI fold's special_x, fri.rs:135) by the workgroup that made it.
 __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest* __restrict__ below, uint64_t count,
                                                                    uint32_t extra, LevelPtrs out, uint32_t extra2,
-                                                                   LevelPtrs out2, uint32_t* done) {
+                                                                   LevelPtrs out2, uint32_t* done, RootFe rf) {
   __shared__ __attribute__((aligned(16))) uint32_t msg[2 * kTailBlock * 8];
   __shared__ uint32_t last;
   const uint64_t base = (uint64_t)blockIdx.x * kTailBlock;
@@ -272,7 +285,10 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
   for (uint32_t i = threadIdx.x; i < here * 4; i += blockDim.x) reinterpret_cast<uint4*>(msg)[i] = src[i];
   __syncthreads();
   tail_levels(msg, base, here, extra, out, extra2 > 0);
-  if (extra2 == 0) return;  // (uniform)
+  if (extra2 == 0) {  // (uniform)
+    if (rf.out && gridDim.x == 1 && threadIdx.x == 0) root_fe_out(msg, rf);
+    return;
+  }
   if (threadIdx.x < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top node's stores have landed
   __syncthreads();
   if (threadIdx.x == 0)
@@ -286,6 +302,7 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
   if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   tail_levels(msg, 0, n_top / 2, extra2 - 1, out2, false);
+  if (rf.out && threadIdx.x == 0) root_fe_out(msg, rf);
 }
 
 // Proof gather: for proof i (index idx[i]): the leaf bytes and the depth
@@ -397,7 +414,12 @@ stark_status merkle_level0(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipSt
 // plane_stride != 0: leaf i's bytes [32 c, 32 c + 32) are at d_leaves + c * plane_stride + 32 i
 // (leaf_len a multiple of 32, 16-B aligned planes).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
-                          hipStream_t stream, size_t plane_stride, bool level0_ready) {
+                          hipStream_t stream, size_t plane_stride, bool level0_ready, RootFe* root_fe) {
+  // (root_fe: the root as a field element too, when the tail kernel makes the root; root_fe->out is
+  // cleared where it does not, and the caller computes it itself)
+  RootFe rf_none{};
+  fe* const rf_out = root_fe ? root_fe->out : nullptr;
+  if (root_fe) root_fe->out = nullptr;
   if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
   if (leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
   if (plane_stride && (!d_leaves || leaf_len == 0 || leaf_len % 32 || plane_stride % 16 || plane_stride < 32 * n ||
@@ -432,9 +454,16 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
         while ((blk2 >> (extra2 + 1)) >= 1 && level2 + extra2 + 1 <= depth) ++extra2;
         for (uint32_t k = 0; k <= extra2; ++k) lp2.lv[k] = nodes + level_offset(n, level2 + k);
       }
+      const bool to_root = fuse ? level + extra + 1 + extra2 == depth : (grid == 1 && level + extra == depth);
+      RootFe rf = rf_none;
+      if (rf_out && to_root) {
+        rf = *root_fe;
+        rf.out = rf_out;
+        root_fe->out = rf_out;
+      }
       hipLaunchKernelGGL(merkle_tail_kernel, dim3(grid), dim3(kTailThreads), 0, stream,
                          (const Digest*)(nodes + level_offset(n, level - 1)), count, extra, lp,
-                         fuse ? extra2 + 1 : 0u, lp2, done);
+                         fuse ? extra2 + 1 : 0u, lp2, done, rf);
       STARK_HIP(ctx, hipGetLastError());
       level += extra;
       count >>= extra;
