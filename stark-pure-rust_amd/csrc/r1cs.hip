@@ -327,9 +327,18 @@ __global__ void r1cs_a_vals_kernel(const fe* __restrict__ ext_idx, const fe* __r
 // Inclusive product scan, phase 1: each workgroup scans kScanBlock Montgomery
 // values in place (4 per thread, then a 256-entry scan of the thread
 // products in LDS) and writes the block product to tot[blockIdx].
-__global__ __launch_bounds__(256) void scan_block_kernel(fe* __restrict__ v, uint64_t n, fe* __restrict__ tot,
-                                                         fe one_m) {
+// The scans run over one or two arrays at once (blockIdx.y picks the array: the A column's numerators and
+// denominators, one launch per phase for both).
+struct ScanArrays {
+  fe* v[2];
+  fe* tot[2];
+  fe* canon[2];
+};
+
+__global__ __launch_bounds__(256) void scan_block_kernel(ScanArrays a, uint64_t n, fe one_m) {
   __shared__ fe part[256];
+  fe* __restrict__ v = a.v[blockIdx.y];
+  fe* __restrict__ tot = a.tot[blockIdx.y];
   const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + 4 * threadIdx.x;
   fe x[4];
   fe acc = one_m;
@@ -358,8 +367,9 @@ __global__ __launch_bounds__(256) void scan_block_kernel(fe* __restrict__ v, uin
 
 // Phase 2: exclusive scan of the block products (one workgroup; each thread
 // owns a contiguous run).
-__global__ __launch_bounds__(256) void scan_tot_kernel(fe* __restrict__ tot, uint32_t nb, fe one_m) {
+__global__ __launch_bounds__(256) void scan_tot_kernel(ScanArrays a, uint32_t nb, fe one_m) {
   __shared__ fe part[256];
+  fe* __restrict__ tot = a.tot[blockIdx.y];
   const uint32_t per = (nb + 255) / 256;
   const uint32_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   fe acc = one_m;
@@ -389,10 +399,12 @@ __global__ __launch_bounds__(256) void scan_tot_kernel(fe* __restrict__ tot, uin
 
 // Phase 3: block b (> 0) times the product of blocks before it; also emits
 // the canonical value into `canon` when given.
-__global__ void scan_apply_kernel(fe* __restrict__ v, uint64_t n, const fe* __restrict__ tot, fe unit,
-                                  fe* __restrict__ canon) {
+__global__ void scan_apply_kernel(ScanArrays a, uint64_t n, fe unit) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  fe* __restrict__ v = a.v[blockIdx.y];
+  const fe* __restrict__ tot = a.tot[blockIdx.y];
+  fe* __restrict__ canon = a.canon[blockIdx.y];
   fe x = fe_load(v + i);
   const uint64_t b = i / kScanBlock;
   if (b) x = fe_mul(x, tot[b]);
@@ -792,12 +804,14 @@ struct Carve {
 static unsigned blocks_for(uint64_t n, unsigned t = 256) { return (unsigned)((n + t - 1) / t); }
 
 // In-place inclusive product scan of n Montgomery values; canonical copy to `canon` if non-null.
-static stark_status product_scan(stark_ctx* ctx, fe* v, uint64_t n, fe* tot, fe* canon, const Mont& mc,
+// Inclusive product scans of the arrays a.v[0 .. count) (n elements each, in place, Montgomery images), their
+// canonical values into a.canon[k] where given; a.tot[k] holds ceil(n / kScanBlock) block products.
+static stark_status product_scan(stark_ctx* ctx, const ScanArrays& a, uint32_t count, uint64_t n, const Mont& mc,
                                  hipStream_t s) {
   const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
-  hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(256), 0, s, v, n, tot, mc.one);
-  hipLaunchKernelGGL(scan_tot_kernel, dim3(1), dim3(256), 0, s, tot, nb, mc.one);
-  hipLaunchKernelGGL(scan_apply_kernel, dim3(blocks_for(n)), dim3(256), 0, s, v, n, (const fe*)tot, mc.unit, canon);
+  hipLaunchKernelGGL(scan_block_kernel, dim3(nb, count), dim3(256), 0, s, a, n, mc.one);
+  hipLaunchKernelGGL(scan_tot_kernel, dim3(1, count), dim3(256), 0, s, a, nb, mc.one);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(blocks_for(n), count), dim3(256), 0, s, a, n, mc.unit);
   STARK_HIP(ctx, hipGetLastError());
   return STARK_OK;
 }
@@ -1254,8 +1268,7 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
                      (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
                      (const Transcript*)d_tr, mc.r2, nmr, dnm);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, sa));
-  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, sa));
+  STARK_TRY(product_scan(ctx, ScanArrays{{nmr, dnm}, {tot, tot + nb}, {nullptr, dnm_c}}, 2, steps, mc, sa));
   // The cold proof's two batch inverses (the A denominators over the steps; Zb2, Zb3 over the precision
   // domain, which prepared circuits carry) share one host round trip: both up passes, one
   // synchronisation, both top levels on the host, then the down passes.
@@ -1941,8 +1954,7 @@ static stark_status dprove_begin(stark_ctx* ctx, uint32_t world, uint32_t rank, 
                      (const fe*)nullptr, (const uint64_t*)perm, (uint64_t)os, (const fe*)wcopy, steps,
                      (const Transcript*)d.d_tr, mc.r2, nmr, dnm);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(product_scan(ctx, nmr, steps, tot, nullptr, mc, sa));
-  STARK_TRY(product_scan(ctx, dnm, steps, tot + nb, dnm_c, mc, sa));
+  STARK_TRY(product_scan(ctx, ScanArrays{{nmr, dnm}, {tot, tot + nb}, {nullptr, dnm_c}}, 2, steps, mc, sa));
   InvPlan inv_d;
   fe* const top_d = multi_inv_h_top(ctx, 0);
   if (!top_d) return STARK_ERR_OOM;
