@@ -162,7 +162,7 @@ struct FriPending {
 void FriPendingDeleter::operator()(FriPending* p) const { delete p; }
 
 stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
-                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0) {
+                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0, bool sx0_made) {
   const FieldHost& F = FieldHost::get();
   hipStream_t s = ctx->stream;
   FriPendingPtr p(new FriPending());
@@ -204,7 +204,7 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   }
   stark_status st = ensure_buf(ctx, ctx->fri_cols, (col_total ? col_total : 1) * sizeof(fe));
   if (st != STARK_OK) return st;
-  st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
+  st = ensure_buf(ctx, ctx->fri_misc, kFriMiscBytes);
   if (st != STARK_OK) return st;
   STARK_TRY(buf_acquire(ctx, ctx->fri_misc, s));  // (the distributed fold's slot 15 is on the caller's stream)
   uint8_t* pinned = nullptr;
@@ -230,7 +230,9 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
   HostFp w = F.from_canonical(root);
   const HostFp inv4 = F.inv(F.from_u64(4));
   const fe r2 = to_dev(F.from_canonical(F.one().v));  // Montgomery image of R
-  bool sx_made = false;  // special_x of this layer already made by its tree's root launch
+  // special_x of this layer already made by its tree's root launch (layer 0: by the caller's tree0 build,
+  // into slot 0 of fri_misc)
+  bool sx_made = tree0 && sx0_made;
   for (size_t layer = 0; layer < layers; ++layer) {
     if (layer == 0 && !tree0) {
       st = merkle_build(ctx, trees[0], (const uint8_t*)cur, m, 32, s);
@@ -250,11 +252,11 @@ stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uin
                        tw->d_lo, tw->d_hi, tw->kb, (const fe*)(d_sx + layer), to_dev(zeta), to_dev(inv4), leaf);
     STARK_HIP(ctx, hipGetLastError());
     // (the next layer's special_x from its tree's root launch where that is the tail kernel)
-    RootFe rf{d_sx + layer + 1, r2};
+    RootFe rf{d_sx + layer + 1, r2, nullptr, false};
     st = merkle_build(ctx, trees[layer + 1], (const uint8_t*)next, q, 32, s, 0, leaf != nullptr,
                       layer + 1 < layers ? &rf : nullptr);
     if (st != STARK_OK) return st;
-    sx_made = layer + 1 < layers && rf.out != nullptr;
+    sx_made = rf.made;
     p->qs.push_back(q);
     // Recurse on the column with w^4 (fri.rs:215-223).
     cur = next;
@@ -654,7 +656,7 @@ static stark_status fri_fold(stark_ctx* ctx, const uint64_t* values, uint64_t* c
   const Twiddles* tw = nullptr;
   stark_status st = get_twiddles(ctx, inv_root, log_n, &tw);
   if (st != STARK_OK) return st;
-  st = ensure_buf(ctx, ctx->fri_misc, 16 * sizeof(fe) + 16 * 32);
+  st = ensure_buf(ctx, ctx->fri_misc, kFriMiscBytes);
   if (st != STARK_OK) return st;
   STARK_TRY(buf_acquire(ctx, ctx->fri_misc, s));  // (prove_low_degree writes slots 0-14 on the context stream)
   fe* d_sx = (fe*)ctx->fri_misc.ptr + 15;  // slot 15: unused by prove_low_degree's <= 15 layers

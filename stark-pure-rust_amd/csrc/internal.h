@@ -263,11 +263,14 @@ struct Sparse {
 };
 
 // Merkle internals (merkle.hip).
-// The root as a field element (fri.rs:135's special_x: the root's LE words reduced mod p, times r2) into
-// *out, made by the kernel that makes the root (merkle_build's root_fe; out cleared where it cannot).
+// Made by the kernel that makes a tree's root (merkle_build's root_fe, where that is the tail kernel; made
+// tells whether it was): the root as a field element (fri.rs:135's special_x: the root's LE words reduced
+// mod p, times r2) into *out, and the root's words into copy[0..8) (each when non-null).
 struct RootFe {
   fe* out;
   fe r2;
+  uint32_t* copy;
+  bool made;
 };
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
                           hipStream_t stream, size_t plane_stride = 0, bool level0_ready = false,
@@ -483,8 +486,11 @@ struct FriPendingDeleter {
   void operator()(FriPending* p) const;
 };
 using FriPendingPtr = std::unique_ptr<FriPending, FriPendingDeleter>;
+// ctx->fri_misc: 16 special_x slots (one per FRI layer; 15 is the distributed fold's) and 16 roots.
+constexpr size_t kFriMiscBytes = 16 * sizeof(fe) + 16 * 32;
 stark_status fri_enqueue(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4], size_t max_deg_plus_1,
-                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0 = nullptr);
+                         uint32_t excl, FriPendingPtr* out, stark_merkle_tree* tree0 = nullptr,
+                         bool sx0_made = false);
 stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& extra, stark_fri_proof** out);
 stark_status fri_prove_device(stark_ctx* ctx, const fe* d_values, size_t n, const uint64_t root[4],
                               size_t max_deg_plus_1, uint32_t excl, stark_fri_proof** out);

@@ -267,13 +267,19 @@ __device__ __forceinline__ void root_fe_out(const uint32_t* msg, const RootFe& r
   fe x;
 #pragma unroll
   for (int i = 0; i < 8; ++i) x.w[i] = msg[i];
+  if (rf.copy) {
 #pragma unroll
-  for (int k = 0; k < 5; ++k) fe_reduce_once(x);  // x < 2^256 < 6p
-  *rf.out = fe_mul(x, rf.r2);
+    for (int i = 0; i < 8; ++i) rf.copy[i] = x.w[i];
+  }
+  if (rf.out) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) fe_reduce_once(x);  // x < 2^256 < 6p
+    *rf.out = fe_mul(x, rf.r2);
+  }
 }
 
-// rf.out non-null: this launch reaches the root (one workgroup, or the fused top), which is also written
-// out as a field element (the FRI fold's special_x, fri.rs:135) by the workgroup that made it.
+// rf.made: this launch reaches the root (one workgroup, or the fused top), which the workgroup that made it
+// also writes out as a field element (the FRI fold's special_x, fri.rs:135) and / or copies (RootFe).
 __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest* __restrict__ below, uint64_t count,
                                                                    uint32_t extra, LevelPtrs out, uint32_t extra2,
                                                                    LevelPtrs out2, uint32_t* done, RootFe rf) {
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
   __syncthreads();
   tail_levels(msg, base, here, extra, out, extra2 > 0);
   if (extra2 == 0) {  // (uniform)
-    if (rf.out && gridDim.x == 1 && threadIdx.x == 0) root_fe_out(msg, rf);
+    if (rf.made && gridDim.x == 1 && threadIdx.x == 0) root_fe_out(msg, rf);
     return;
   }
   if (threadIdx.x < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the top node's stores have landed
@@ -302,7 +308,7 @@ __global__ __launch_bounds__(kTailThreads) void merkle_tail_kernel(const Digest*
   if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   tail_levels(msg, 0, n_top / 2, extra2 - 1, out2, false);
-  if (rf.out && threadIdx.x == 0) root_fe_out(msg, rf);
+  if (rf.made && threadIdx.x == 0) root_fe_out(msg, rf);
 }
 
 // Proof gather: for proof i (index idx[i]): the leaf bytes and the depth
@@ -415,11 +421,10 @@ stark_status merkle_level0(stark_ctx* ctx, stark_merkle_tree* t, size_t n, hipSt
 // (leaf_len a multiple of 32, 16-B aligned planes).
 stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d_leaves, size_t n, size_t leaf_len,
                           hipStream_t stream, size_t plane_stride, bool level0_ready, RootFe* root_fe) {
-  // (root_fe: the root as a field element too, when the tail kernel makes the root; root_fe->out is
-  // cleared where it does not, and the caller computes it itself)
-  RootFe rf_none{};
-  fe* const rf_out = root_fe ? root_fe->out : nullptr;
-  if (root_fe) root_fe->out = nullptr;
+  // (root_fe: made by the tail launch that makes the root; root_fe->made false where no tail launch does,
+  // and the caller makes it itself)
+  const RootFe rf_none{};
+  if (root_fe) root_fe->made = false;
   if (n == 0 || (n & (n - 1)) != 0) return STARK_ERR_BAD_LENGTH;
   if (leaf_len > 0xFFFFFFFFull) return STARK_ERR_BAD_ARG;
   if (plane_stride && (!d_leaves || leaf_len == 0 || leaf_len % 32 || plane_stride % 16 || plane_stride < 32 * n ||
@@ -456,10 +461,9 @@ stark_status merkle_build(stark_ctx* ctx, stark_merkle_tree* t, const uint8_t* d
       }
       const bool to_root = fuse ? level + extra + 1 + extra2 == depth : (grid == 1 && level + extra == depth);
       RootFe rf = rf_none;
-      if (rf_out && to_root) {
+      if (root_fe && to_root) {
+        root_fe->made = true;
         rf = *root_fe;
-        rf.out = rf_out;
-        root_fe->out = rf_out;
       }
       hipLaunchKernelGGL(merkle_tail_kernel, dim3(grid), dim3(kTailThreads), 0, stream,
                          (const Digest*)(nodes + level_offset(n, level - 1)), count, extra, lp,

@@ -1374,9 +1374,16 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   STARK_TRY(merkle_level0(ctx, l_tree, prec, s, &la.leaf));
   hipLaunchKernelGGL(r1cs_lincomb_kernel, dim3(blocks_for(prec)), dim3(256), 0, s, la);
   STARK_HIP(ctx, hipGetLastError());
-  STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s, 0, true));
-  hipLaunchKernelGGL(r1cs_l_root_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(l_tree), d_tr);
-  STARK_HIP(ctx, hipGetLastError());
+  // Its root launch also copies the root into the transcript (l_root) and writes FRI layer 0's special_x
+  // (fri.rs:135) into the FRI's slot 0 of fri_misc; where no tail launch makes the root, kernels do.
+  STARK_TRY(ensure_buf(ctx, ctx->fri_misc, kFriMiscBytes));
+  STARK_TRY(buf_acquire(ctx, ctx->fri_misc, s));
+  RootFe l_rf{(fe*)ctx->fri_misc.ptr, mc.r2, &d_tr->roots[2][0], false};
+  STARK_TRY(merkle_build(ctx, l_tree, (const uint8_t*)lvals, prec, 32, s, 0, true, &l_rf));
+  if (!l_rf.made) {
+    hipLaunchKernelGGL(r1cs_l_root_kernel, dim3(1), dim3(64), 0, s, (const uint32_t*)merkle_root_dev(l_tree), d_tr);
+    STARK_HIP(ctx, hipGetLastError());
+  }
   // The roots and the constraint flags come down behind the L tree; an event marks them.
   Transcript* h_tr = nullptr;
   // (slot 1 layout: internal.h kPinned1Bytes)
@@ -1394,7 +1401,8 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   // prove_low_degree(L, g2, precision / 4, skips) on the resident L (prove.rs:367), enqueued behind the rest.
   FriPendingPtr fri_pending;
   clk.mark("prover kernels enqueued");
-  STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending, l_tree));
+  STARK_TRY(fri_enqueue(ctx, (const fe*)lvals, prec, g2c, prec / 4, (uint32_t)skips, &fri_pending, l_tree,
+                        l_rf.made));
   clk.mark("FRI kernels enqueued");
   // While the FRI layers run: the roots, the spot checks (prove.rs:337-362), their openings (gathered on
   // the second stream) and the StarkProof JSON up to fri_proof.
