@@ -135,8 +135,8 @@ struct stark_ctx {
   stark_merkle_tree* trees[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<stark_merkle_tree*> fri_trees;  // one per FRI layer (+ the input's), reused across proofs
   stark::DevBuf fri_misc;                     // per-layer special_x (device transcript)
-  void* pinned[4] = {nullptr, nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
-  size_t pinned_bytes[4] = {0, 0, 0, 0};
+  void* pinned[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // pinned host scratch (ctx_pinned)
+  size_t pinned_bytes[5] = {0, 0, 0, 0, 0};
   hipEvent_t staged = nullptr;  // the last DMA out of pinned slot 3 (r1cs_trace_dev.hip staged_upload)
   // A second stream and an event for work the host overlaps with the main stream (the prover's spot-check
   // openings gathered while its FRI layers still run, r1cs.hip); created on first use.
@@ -198,7 +198,10 @@ size_t cache_bytes(const stark_ctx* ctx);
 bool cache_reserve(stark_ctx* ctx, size_t need, bool evict_ext);
 // Context-owned pinned host scratch of at least `bytes` (async copy target).
 // Slot 0: gather batches; slot 1: transcript values and roots; slot 2: the device trace builder's
-// record-walk tables; slot 3: its upload staging (the raw .r1cs constraint section and witness).
+// record-walk tables; slot 3: its upload staging (the raw .r1cs constraint section and witness); slot 4:
+// the prover's small host-made uploads (constraint tables at 0, boundary constants from kPinned4ConstsOff),
+// so they are asynchronous copies (a pageable copy blocks the host).
+constexpr size_t kPinned4ConstsOff = 16384;
 stark_status ctx_pinned(stark_ctx* ctx, int slot, size_t bytes, void** out);
 // Pinned slot 1 (always this size, so no caller's pointer into it moves): [0, 2048) the prover's
 // transcript head, [2048, 2560) FRI roots, [2560, 3584) two batch inverses' top levels, [3584, 3588) the

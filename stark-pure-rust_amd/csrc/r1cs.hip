@@ -1025,7 +1025,11 @@ static Pow32 pow32() {
 static stark_status upload_constraint_tables(stark_ctx* ctx, Transcript* d_tr, const ConstraintArgs& ca,
                                              hipStream_t s) {
   const FieldHost& F = FieldHost::get();
-  uint32_t t[33][72];
+  // built in pinned slot 4 (its first kPinned4ConstsOff bytes), so the copy is asynchronous
+  static_assert(sizeof(uint32_t) * 33 * 72 <= kPinned4ConstsOff, "pinned slot 4 layout");
+  void* pin = nullptr;
+  STARK_TRY(ctx_pinned(ctx, 4, kPinned4ConstsOff, &pin));
+  uint32_t(&t)[33][72] = *reinterpret_cast<uint32_t(*)[33][72]>(pin);
   db_table(F.inv(F.pow_u64(F.from_u64(2), 256)), t[0]);  // R^-1
   const uint32_t n = ca.tinv ? ca.n_pf : 0;
   for (uint32_t k = 0; k < 8; ++k) {
@@ -1188,7 +1192,12 @@ static stark_status prove_r1cs(stark_ctx* ctx, const uint64_t* witness_trace, co
   HostFp x_last;
   // alive until the proof's final synchronisation
   const std::vector<fe> h = boundary_consts(g2, prec, skips, public_wires, public_first_indices, n_pfi, &x_last);
-  STARK_HIP(ctx, hipMemcpyAsync(consts, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+  {  // through pinned slot 4 (an asynchronous copy; a pageable one blocks the host)
+    uint8_t* pin = nullptr;
+    STARK_TRY(ctx_pinned(ctx, 4, kPinned4ConstsOff + h.size() * sizeof(fe), (void**)&pin));
+    memcpy(pin + kPinned4ConstsOff, h.data(), h.size() * sizeof(fe));
+    STARK_HIP(ctx, hipMemcpyAsync(consts, pin + kPinned4ConstsOff, h.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+  }
   // Upload the six value columns, zero tails (prove.rs:59-69; inv_best_fft pads the flags).  The
   // inputs may be host or device pointers (the device trace builder's columns): hipMemcpyDefault.
   const uint64_t* src[6] = {coefficients, flag0, flag1, flag2, witness_trace, computational_trace};

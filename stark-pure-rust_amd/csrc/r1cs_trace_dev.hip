@@ -317,6 +317,7 @@ struct Upload {
   const void* src;
   size_t len;
 };
+constexpr size_t kStageAlone = (size_t)1 << 20;  // smaller uploads: one thread, no pool
 static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups, hipStream_t s, unsigned workers,
                                   unsigned sides, const std::function<void(unsigned)>& side) {
   constexpr size_t kChunk = (size_t)2 << 20;
@@ -327,6 +328,24 @@ static stark_status staged_upload(stark_ctx* ctx, const std::vector<Upload>& ups
   uint8_t* stage = nullptr;
   stark_status st = ctx_pinned(ctx, 3, total, (void**)&stage);
   if (st != STARK_OK) return st;
+  if (total < kStageAlone) {
+    // A small circuit: the side tasks and the copies on this thread (waking the pool costs more than they do)
+    for (unsigned k = 0; k < sides; ++k) side(k);
+    size_t at = 0;
+    hipError_t e = hipSuccess;
+    for (const Upload& u : ups) {
+      memcpy(stage + at, u.src, u.len);
+      if (e == hipSuccess && u.len) e = hipMemcpyAsync(u.dst, stage + at, u.len, hipMemcpyHostToDevice, s);
+      at += u.len;
+    }
+    const hipError_t rec = hipEventRecord(ctx->staged, s);  // (also on the error path: see below)
+    if (e != hipSuccess) {
+      if (rec != hipSuccess) hipStreamSynchronize(s);
+      return hip_fail(ctx, e, "r1cs/wtns upload");
+    }
+    if (rec != hipSuccess) return hip_fail(ctx, rec, "hipEventRecord(staged)");
+    return STARK_OK;
+  }
   struct Piece {
     uint8_t* dst;
     const uint8_t* src;
