@@ -28,6 +28,7 @@
 #include "internal.h"
 #include "blake2s.h"
 #include "host_json.h"
+#include "merkle_dev.h"
 
 
 namespace stark {
@@ -111,35 +112,41 @@ struct FriIdxArgs {
   uint32_t q[16];
   uint64_t col_at[16], poly_at[16];  // first slots in the index array
 };
-__global__ void fri_indices_kernel(FriIdxArgs a, uint32_t layers, uint32_t excl, uint64_t* __restrict__ idx) {
-  const uint32_t l = threadIdx.x;
-  if (l >= layers) return;
-  uint32_t data[40];  // 160 bytes, little-endian words
-#pragma unroll
-  for (int k = 0; k < 8; ++k) data[k] = a.root[l][k];
-#pragma unroll
-  for (int b = 1; b < 5; ++b) {
-    uint32_t h[8], m[16];
-    b2s_init(h);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      m[k] = data[8 * (b - 1) + k];
-      m[k + 8] = 0;
-    }
-    b2s_compress(h, m, 32, 0, true);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) data[8 * b + k] = h[k];
+// One 64-lane workgroup per layer: a quad of lanes hashes the chain (hash_pair_quad, merkle_dev.h; one
+// compression's latency is about a quarter of a lane's), then 40 lanes write one index each.
+__global__ __launch_bounds__(64) void fri_indices_kernel(FriIdxArgs a, uint32_t excl, uint64_t* __restrict__ idx) {
+  __shared__ uint32_t data[40];   // 160 bytes, little-endian words
+  __shared__ uint32_t msg[16];
+  const uint32_t l = blockIdx.x, t = threadIdx.x;
+  if (t < 8) {
+    data[t] = a.root[l][t];
+    msg[t] = data[t];
+  } else if (t < 16) {
+    msg[t] = 0;
   }
+  __syncthreads();
+#pragma unroll 1
+  for (int b = 1; b < 5; ++b) {
+    uint32_t lo = 0, hi = 0;
+    if (t < 4) hash_pair_quad(msg, t, lo, hi, 32);
+    __syncthreads();
+    if (t < 4) {
+      data[8 * b + t] = lo;
+      data[8 * b + 4 + t] = hi;
+      msg[t] = lo;
+      msg[4 + t] = hi;
+    }
+    __syncthreads();
+  }
+  if (t >= 40) return;
   const uint32_t q = a.q[l];
   const uint32_t real_mod = excl ? (uint32_t)((uint64_t)q * (excl - 1) / excl) : q;
-  for (int i = 0; i < 40; ++i) {
-    const uint32_t w = __builtin_bswap32(data[i]);
-    const uint32_t v = w % real_mod;
-    const uint64_t y = excl ? v + 1 + v / (excl - 1) : v;
-    idx[a.col_at[l] + i] = y;
+  const uint32_t w = __builtin_bswap32(data[t]);
+  const uint32_t v = w % real_mod;
+  const uint64_t y = excl ? v + 1 + v / (excl - 1) : v;
+  idx[a.col_at[l] + t] = y;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) idx[a.poly_at[l] + 4 * i + j] = y + (uint64_t)q * j;
-  }
+  for (int j = 0; j < 4; ++j) idx[a.poly_at[l] + 4 * t + j] = y + (uint64_t)q * j;
 }
 
 // Pinned slot 1 layout: [0, 2048) mk_r1cs_proof's transcript, [2048, 2560) FRI roots.
@@ -317,8 +324,10 @@ stark_status fri_finish(stark_ctx* ctx, FriPending* p, std::vector<GatherReq>& e
       a.col_at[l] = f[n_extra + 2 * l];
       a.poly_at[l] = f[n_extra + 2 * l + 1];
     }
-    hipLaunchKernelGGL(fri_indices_kernel, dim3(1), dim3(64), 0, s, a, (uint32_t)p->layers, p->excl, hi);
-    STARK_HIP(ctx, hipGetLastError());
+    if (p->layers) {
+      hipLaunchKernelGGL(fri_indices_kernel, dim3((unsigned)p->layers), dim3(64), 0, s, a, p->excl, hi);
+      STARK_HIP(ctx, hipGetLastError());
+    }
     return STARK_OK;
   };
   // The last layer's values come down with the gather (one synchronisation) when they fit the pinned slot.
