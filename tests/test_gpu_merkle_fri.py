@@ -56,9 +56,9 @@ def test_merkle_tail_one_launch_sizes(ctx, oracle):
     the levels above the blocks' top nodes, counted with an agent-scope atomic kept in the node buffer): one
     tree object rebuilt at sizes that take it (a tail level of 512 to 32768 nodes) and sizes that do not,
     growing and shrinking so that its node buffer is reallocated (possibly at the same address) and reused,
-    three rounds; every root and path against the oracle's tree."""
+    three rounds; every root and path against the oracle's tree (2^18 and 2^19 leaves: wide levels first)."""
     t = S.MerkleProofInPlace(ctx)
-    sizes = [1 << 10, 1 << 16, 1 << 12, 1 << 17, 1 << 9, 1 << 14, 1 << 11, 1 << 13, 1 << 15]
+    sizes = [1 << 10, 1 << 16, 1 << 12, 1 << 17, 1 << 9, 1 << 19, 1 << 14, 1 << 11, 1 << 18, 1 << 13, 1 << 15]
     rng = np.random.default_rng(61)
     for rnd in range(3):
         for n in sizes:
